@@ -1,0 +1,26 @@
+# Build of the MI355X-native AnySeq engine (gfx950) and the CPU oracle.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-parameter
+SRC := anyseq_amd/csrc
+LIB := anyseq_amd/libanyseq.so
+
+all: $(LIB) oracle
+
+$(SRC)/anyseq_kernels.o: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_internal.h
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -c $< -o $@
+
+$(SRC)/anyseq_engine.o: $(SRC)/anyseq_engine.cpp $(SRC)/anyseq_internal.h include/anyseq.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(SRC)/anyseq_kernels.o $(SRC)/anyseq_engine.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -f $(SRC)/*.o $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,549 @@
+// anyseq_engine.cpp — host side of the MI355X AnySeq engine: per-device state,
+// the score driver (align.impala:218-235) and the linear-space construct driver
+// (the reference's column-split Hirschberg, align.impala:237-311,
+// traceback_lintime.impala:1-148) over the HIP kernels of anyseq_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/anyseq.h"
+#include "anyseq_internal.h"
+
+using namespace anyseq;
+
+extern "C" {
+hipError_t anyseq_launch_fill(int R, int NW, const DPProblem* probs, const GroupRef* groups, int ngroups,
+                              uint32_t* dq, uint32_t* err, const FillParams* fp, int grid, hipStream_t st);
+hipError_t anyseq_launch_semiglobal_reduce(const int32_t* row_g, int m, const int32_t* col_h, int n, int ng,
+                                           int32_t* out, hipStream_t st);
+hipError_t anyseq_launch_hb_sum(const void* parts, int nparts, int bpp, int half, const int32_t* L, const int32_t* R,
+                                int kind, int gap, int32_t* bmax, int32_t* bind, int32_t* splits, hipStream_t st);
+hipError_t anyseq_launch_pred(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
+                              const FillParams* fp, hipStream_t st);
+hipError_t anyseq_launch_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
+                              const uint8_t* pred, int kind, uint8_t* alq, uint8_t* als, hipStream_t st);
+}
+
+namespace {
+
+constexpr int32_t SCORE_MIN_VALUE = -2147483647;  // align.impala:16
+constexpr int32_t SPLIT_UNSET = 0x7fff0000;
+constexpr int MIN_PART_WIDTH_HB = 128;             // align.impala:18
+constexpr int CPU_BLOCK_WIDTH = 1024;              // iteration_cpu.impala:1 (hb_sum stride)
+
+thread_local std::string g_last_error;
+thread_local double g_fill_ms = 0.0;
+thread_local int g_fill_launches = 0;
+
+struct Failure {
+    std::string msg;
+};
+
+[[noreturn]] void fail(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    throw Failure{buf};
+}
+
+#define HIPCHECK(x)                                                                       \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) fail("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void* get(size_t bytes) {
+        if (bytes == 0) bytes = 16;
+        if (bytes > cap) {
+            if (p) HIPCHECK(hipFree(p));
+            p = nullptr;
+            size_t c = std::max(bytes, cap * 3 / 2);
+            c = (c + 255) & ~size_t(255);
+            HIPCHECK(hipMalloc(&p, c));
+            cap = c;
+        }
+        return p;
+    }
+};
+
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+struct Tuning {
+    int R = 1;
+    int NW = 8;
+    int grid = 0;
+};
+
+struct Engine {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::mutex mu;
+    DevBuf q, s, probs, groups, rowbuf, flags, ctr, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq,
+        als;
+    std::vector<int32_t> host_i32;
+
+    explicit Engine(int dev) : device(dev) {
+        HIPCHECK(hipSetDevice(dev));
+        hipDeviceProp_t prop;
+        HIPCHECK(hipGetDeviceProperties(&prop, dev));
+        num_cus = prop.multiProcessorCount;
+        HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIPCHECK(hipEventCreate(&ev0));
+        HIPCHECK(hipEventCreate(&ev1));
+    }
+};
+
+std::mutex g_engines_mu;
+std::vector<std::unique_ptr<Engine>> g_engines;
+int g_device = -1;
+Tuning g_tuning;
+bool g_tuning_init = false;
+
+Engine& engine() {
+    std::lock_guard<std::mutex> lk(g_engines_mu);
+    if (!g_tuning_init) {
+        g_tuning.R = env_int("ANYSEQ_R", g_tuning.R);
+        g_tuning.NW = env_int("ANYSEQ_NW", g_tuning.NW);
+        g_tuning.grid = env_int("ANYSEQ_GRID", g_tuning.grid);
+        g_tuning_init = true;
+    }
+    if (g_device < 0) g_device = env_int("ANYSEQ_DEVICE", 0);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) fail("no HIP device available (hipGetDeviceCount)");
+    if (g_device >= ndev) fail("device %d out of range (%d devices)", g_device, ndev);
+    if ((int)g_engines.size() < ndev) g_engines.resize(ndev);
+    if (!g_engines[g_device]) g_engines[g_device].reset(new Engine(g_device));
+    HIPCHECK(hipSetDevice(g_device));
+    return *g_engines[g_device];
+}
+
+int rows_per_lane() { return g_tuning.R == 2 ? 2 : (g_tuning.R >= 4 ? 4 : 1); }
+int waves_per_group() { return g_tuning.NW == 4 ? 4 : 8; }
+
+// ---------------------------------------------------------------- fill --
+// Runs one batched fill launch over `probs` (host copies; device pointers set).
+void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st) {
+    const int R = rows_per_lane(), NW = waves_per_group();
+    size_t rowbuf_ints = 0, flag_words = 0;
+    int max_groups = 0;
+    for (auto& P : probs) {
+        P.nbands = (P.h + 64 * R - 1) / (64 * R);
+        P.ngroups = (P.nbands + NW - 1) / NW;
+        P.wpad = (P.w + 63) & ~63;
+        rowbuf_ints += (size_t)std::max(P.ngroups - 1, 0) * P.wpad;
+        flag_words += P.ngroups;
+        max_groups = std::max(max_groups, P.ngroups);
+    }
+    int32_t* rowbuf = (int32_t*)E.rowbuf.get(rowbuf_ints * 4);
+    uint32_t* flags = (uint32_t*)E.flags.get((flag_words + 4) * 4);
+    size_t ro = 0, fo = 0;
+    for (auto& P : probs) {
+        P.rowbuf = rowbuf + ro;
+        P.flags = flags + fo;
+        ro += (size_t)std::max(P.ngroups - 1, 0) * P.wpad;
+        fo += P.ngroups;
+    }
+    // group table: round-robin over problems so every sub-problem progresses
+    std::vector<GroupRef> groups;
+    for (int k = 0; k < max_groups; ++k)
+        for (size_t p = 0; p < probs.size(); ++p)
+            if (k < probs[p].ngroups) groups.push_back(GroupRef{(int32_t)p, k});
+    if (groups.empty()) return;
+    DPProblem* d_probs = (DPProblem*)E.probs.get(probs.size() * sizeof(DPProblem));
+    GroupRef* d_groups = (GroupRef*)E.groups.get(groups.size() * sizeof(GroupRef));
+    HIPCHECK(hipMemcpyAsync(d_probs, probs.data(), probs.size() * sizeof(DPProblem), hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(d_groups, groups.data(), groups.size() * sizeof(GroupRef), hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemsetAsync(flags, 0, flag_words * 4, st));
+    uint32_t* ctr = (uint32_t*)E.ctr.get(64);
+    HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));  // ctr[0] = dequeue counter, ctr[1] = error word
+    int grid = g_tuning.grid > 0 ? g_tuning.grid : E.num_cus;
+    grid = std::min<int>(grid, (int)groups.size());
+    HIPCHECK(hipEventRecord(E.ev0, st));
+    HIPCHECK(anyseq_launch_fill(R, NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fp, grid, st));
+    HIPCHECK(hipEventRecord(E.ev1, st));
+    HIPCHECK(hipEventSynchronize(E.ev1));
+    float ms = 0.f;
+    HIPCHECK(hipEventElapsedTime(&ms, E.ev0, E.ev1));
+    g_fill_ms += ms;
+    g_fill_launches += 1;
+    uint32_t err = 0;
+    HIPCHECK(hipMemcpy(&err, ctr + 1, 4, hipMemcpyDeviceToHost));
+    if (err) fail("fill kernel reported error %u (spin timeout)", err);
+}
+
+FillParams make_params(int kind, const anyseq_scoring& sc) {
+    FillParams fp;
+    memset(&fp, 0, sizeof fp);
+    fp.kind = kind;
+    fp.match = sc.match;
+    fp.mismatch = sc.mismatch;
+    fp.gap = sc.gap_extend;
+    fp.gap_open = sc.gap_open;
+    fp.gap_extend = sc.gap_extend;
+    fp.affine = sc.gap_open != 0;
+    return fp;
+}
+
+void check_scoring(int kind, const anyseq_scoring& sc) {
+    if (kind < 0 || kind > 2) fail("invalid alignment kind %d", kind);
+    if (sc.gap_extend >= 0) fail("gap_extend must be negative (got %d)", sc.gap_extend);
+    if (sc.gap_open > 0) fail("gap_open must be <= 0 (got %d)", sc.gap_open);
+    if (sc.gap_open != 0) fail("affine gaps are not available in this build yet");
+}
+
+// Score of an empty matrix (reference semantics with benchmark restored).
+int64_t empty_score(int kind, int n, int m, const anyseq_scoring& sc) {
+    if (kind == KIND_GLOBAL) return (int64_t)(n > 0 ? n : m) * sc.gap_extend;  // init(n-1) or init(m-1)
+    if (kind == KIND_SEMIGLOBAL) return 0;
+    return SCORE_MIN_VALUE;  // local: no slot is ever written
+}
+
+// Fill-based score on device-resident sequences (align.impala:218-235).
+int64_t score_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds, int m,
+                  hipStream_t st) {
+    if (n <= 0 || m <= 0) return empty_score(kind, n, m, sc);
+    const FillParams fp = make_params(kind, sc);
+    DPProblem P;
+    memset(&P, 0, sizeof P);
+    P.q = dq;
+    P.s = ds;
+    P.q_off = 0;
+    P.q_step = 1;
+    P.s_off = 0;
+    P.s_step = 1;
+    P.h = n;
+    P.w = m;
+    int32_t* res = (int32_t*)E.ctr.get(64) + 4;
+    if (kind != KIND_LOCAL) P.out_col = (int32_t*)E.outcol.get((size_t)n * 4);
+    if (kind == KIND_SEMIGLOBAL) P.out_row = (int32_t*)E.outrow.get((size_t)((m + 63) & ~63) * 4);
+    if (kind == KIND_LOCAL) {
+        P.best = res;
+        HIPCHECK(hipMemsetAsync(res, 0, 4, st));
+    }
+    std::vector<DPProblem> probs{P};
+    run_fill(E, probs, fp, st);
+    int32_t v = 0;
+    if (kind == KIND_GLOBAL) {
+        HIPCHECK(hipMemcpyAsync(&v, P.out_col + (n - 1), 4, hipMemcpyDeviceToHost, st));
+    } else if (kind == KIND_SEMIGLOBAL) {
+        HIPCHECK(hipMemsetAsync(res, 0, 4, st));
+        HIPCHECK(anyseq_launch_semiglobal_reduce(P.out_row, m, P.out_col, n, -sc.gap_extend, res, st));
+        HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, st));
+    } else {
+        HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHECK(hipStreamSynchronize(st));
+    return v;
+}
+
+int64_t score_host(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m) {
+    Engine& E = engine();
+    std::lock_guard<std::mutex> lk(E.mu);
+    if (n <= 0 || m <= 0) return empty_score(kind, n, m, sc);
+    uint8_t* dq = (uint8_t*)E.q.get((size_t)n);
+    uint8_t* ds = (uint8_t*)E.s.get((size_t)m);
+    HIPCHECK(hipMemcpyAsync(dq, q, (size_t)n, hipMemcpyHostToDevice, E.stream));
+    HIPCHECK(hipMemcpyAsync(ds, s, (size_t)m, hipMemcpyHostToDevice, E.stream));
+    return score_dev(E, kind, sc, dq, n, ds, m, E.stream);
+}
+
+// ------------------------------------------------------------- construct --
+int next_pow_2(int i) {  // utils.impala:19-28
+    if (i == 0) return 0;
+    int n = i - 1, r = 1;
+    while (n > 0) {
+        n >>= 1;
+        r <<= 1;
+    }
+    return r;
+}
+
+struct HostSplits {  // traceback_lintime.impala:1-42 (logical index -1 at storage 0)
+    std::vector<int32_t> v;
+    int nb = 0, bpp = 0;
+    int32_t at(int idx) const {
+        const int32_t x = v[idx + 1];
+        if (x == SPLIT_UNSET) fail("internal: split %d read before being set", idx);
+        return x;
+    }
+    void dims(int part, int& off, int& h) const {
+        const int start = part * bpp - 1;
+        const int end = std::min((part + 1) * bpp - 1, nb - 1);
+        off = at(start);
+        h = at(end) - off;
+    }
+};
+
+// Linear-space construct (traceback_lintime, align.impala:237-311) on the GPU.
+void construct_host(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m, char* alq,
+                    char* als) {
+    Engine& E = engine();
+    std::lock_guard<std::mutex> lk(E.mu);
+    hipStream_t st = E.stream;
+    const size_t L = (size_t)n + (size_t)m;
+    if (L == 0) return;
+    if (m <= 0) {  // no 128-column block: the reference writes only blanks
+        memset(alq, ' ', L);
+        memset(als, ' ', L);
+        return;
+    }
+    const FillParams fp = make_params(kind, sc);
+    uint8_t* dq = (uint8_t*)E.q.get((size_t)std::max(n, 1));
+    uint8_t* ds = (uint8_t*)E.s.get((size_t)m);
+    if (n > 0) HIPCHECK(hipMemcpyAsync(dq, q, (size_t)n, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(ds, s, (size_t)m, hipMemcpyHostToDevice, st));
+
+    HostSplits sp;
+    sp.nb = (m + MIN_PART_WIDTH_HB - 1) / MIN_PART_WIDTH_HB;
+    sp.v.assign((size_t)sp.nb + 1, SPLIT_UNSET);
+    int pw = next_pow_2(m);
+    sp.bpp = pw / MIN_PART_WIDTH_HB;
+    sp.v[0] = 0;
+    sp.v[sp.nb] = n;
+    int32_t* d_spl = (int32_t*)E.spl.get(sp.v.size() * 4);
+    HIPCHECK(hipMemcpyAsync(d_spl, sp.v.data(), sp.v.size() * 4, hipMemcpyHostToDevice, st));
+    int32_t* dL = (int32_t*)E.L.get((size_t)std::max(n, 1) * 4);
+    int32_t* dR = (int32_t*)E.R.get((size_t)std::max(n, 1) * 4);
+
+    while (pw > MIN_PART_WIDTH_HB) {  // traceback_lintime_step, align.impala:273-290
+        const int half = pw / 2;
+        const int parts = (m + half - 1) / pw;
+        std::vector<DPProblem> probs;
+        std::vector<PartInfo> pinfo;
+        for (int p = 0; p < parts; ++p) {
+            int hoi, hh;
+            sp.dims(p, hoi, hh);
+            const int hoj_l = p * pw, hoj_r = p * pw + half;
+            const int hw = std::min(half, m - hoj_r);
+            PartInfo pi;
+            pi.off = hoi;
+            pi.len = hh;
+            pi.rhw = hw;
+            pi.split_index = p * sp.bpp + sp.bpp / 2 - 1;
+            pinfo.push_back(pi);
+            if (hh <= 0) continue;
+            DPProblem P;
+            memset(&P, 0, sizeof P);
+            P.q = dq;
+            P.s = ds;
+            P.h = hh;
+            // left half: forward
+            P.q_off = hoi;
+            P.q_step = 1;
+            P.s_off = hoj_l;
+            P.s_step = 1;
+            P.w = half;
+            P.out_col = dL + hoi;
+            probs.push_back(P);
+            // right half: query rows and subject columns reversed (get_sequence_acc_half)
+            P.q_off = hoi + hh - 1;
+            P.q_step = -1;
+            P.s_off = hoj_r + hw - 1;
+            P.s_step = -1;
+            P.w = hw;
+            P.out_col = dR + hoi;
+            probs.push_back(P);
+        }
+        run_fill(E, probs, fp, st);
+        // hb_sum (traceback_lintime.impala:44-135), CPU BLOCK_WIDTH candidate order
+        const int bwh = std::min(CPU_BLOCK_WIDTH, half * 2);
+        const int bpp_h = half * 2 / bwh;
+        PartInfo* d_parts = (PartInfo*)E.parts.get(pinfo.size() * sizeof(PartInfo));
+        HIPCHECK(hipMemcpyAsync(d_parts, pinfo.data(), pinfo.size() * sizeof(PartInfo), hipMemcpyHostToDevice, st));
+        int32_t* d_bmax = (int32_t*)E.bmax.get((size_t)parts * bpp_h * 4);
+        int32_t* d_bind = (int32_t*)E.bind.get((size_t)parts * bpp_h * 4);
+        HIPCHECK(anyseq_launch_hb_sum(d_parts, parts, bpp_h, half, dL, dR, kind, sc.gap_extend, d_bmax, d_bind, d_spl,
+                                      st));
+        HIPCHECK(hipMemcpyAsync(sp.v.data(), d_spl, sp.v.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        pw /= 2;
+        sp.bpp /= 2;
+    }
+
+    // final level: blockwise predecessors + per-block walk (align.impala:292-311)
+    std::vector<BlockInfo> blocks((size_t)sp.nb);
+    int64_t pred_bytes = 0;
+    for (int b = 0; b < sp.nb; ++b) {
+        BlockInfo& bi = blocks[b];
+        sp.dims(b, bi.oi, bi.h);
+        bi.oj = b * MIN_PART_WIDTH_HB;
+        bi.w = std::min(MIN_PART_WIDTH_HB, m - bi.oj);
+        bi.pred_base = pred_bytes;
+        if (bi.h > 0) pred_bytes += (int64_t)(bi.h + 127) * 128;
+    }
+    BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
+    HIPCHECK(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, st));
+    uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
+    uint8_t* d_alq = (uint8_t*)E.alq.get(L);
+    uint8_t* d_als = (uint8_t*)E.als.get(L);
+    HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
+    HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
+    HIPCHECK(anyseq_launch_pred(d_blocks, sp.nb, dq, ds, d_pred, &fp, st));
+    HIPCHECK(anyseq_launch_walk(d_blocks, sp.nb, dq, ds, d_pred, kind, d_alq, d_als, st));
+    HIPCHECK(hipMemcpyAsync(alq, d_alq, L, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(als, d_als, L, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+}
+
+const anyseq_scoring kAbiScoring = {2, -1, 0, -1};  // linear_scoring_scheme(2,-1,-1)
+
+int64_t abi_score(int kind, const char* q, int n, const char* s, int m) {
+    try {
+        return score_host(kind, kAbiScoring, q, n, s, m);
+    } catch (const Failure& f) {
+        g_last_error = f.msg;
+        fprintf(stderr, "anyseq: %s\n", f.msg.c_str());
+        return INT64_MIN;
+    }
+}
+
+int64_t abi_construct(int kind, const char* q, int n, const char* s, int m, char* alq, char* als) {
+    try {
+        construct_host(kind, kAbiScoring, q, n, s, m, alq, als);
+        if (env_int("ANYSEQ_CONSTRUCT_TRUE_SCORE", 0)) return score_host(kind, kAbiScoring, q, n, s, m);
+        // the reference's literal return (scoring object never relaxed)
+        if (kind == KIND_GLOBAL) return (int64_t)n * kAbiScoring.gap_extend;
+        if (kind == KIND_SEMIGLOBAL) return 0;
+        return SCORE_MIN_VALUE;
+    } catch (const Failure& f) {
+        g_last_error = f.msg;
+        fprintf(stderr, "anyseq: %s\n", f.msg.c_str());
+        return INT64_MIN;
+    }
+}
+
+}  // namespace
+
+// ======================================================================= ABI
+extern "C" {
+
+int64_t global_alignment_score(const char* query, int lenq, const char* subject, int lens) {
+    return abi_score(KIND_GLOBAL, query, lenq, subject, lens);
+}
+int64_t semiglobal_alignment_score(const char* query, int lenq, const char* subject, int lens) {
+    return abi_score(KIND_SEMIGLOBAL, query, lenq, subject, lens);
+}
+int64_t local_alignment_score(const char* query, int lenq, const char* subject, int lens) {
+    return abi_score(KIND_LOCAL, query, lenq, subject, lens);
+}
+int64_t construct_global_alignment(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                   char* alSubject) {
+    return abi_construct(KIND_GLOBAL, query, lenq, subject, lens, alQuery, alSubject);
+}
+int64_t construct_semiglobal_alignment(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                       char* alSubject) {
+    return abi_construct(KIND_SEMIGLOBAL, query, lenq, subject, lens, alQuery, alSubject);
+}
+int64_t construct_local_alignment(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                  char* alSubject) {
+    return abi_construct(KIND_LOCAL, query, lenq, subject, lens, alQuery, alSubject);
+}
+
+int anyseq_score(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject, int lens,
+                 int64_t* score) {
+    try {
+        const anyseq_scoring s = sc ? *sc : kAbiScoring;
+        check_scoring(kind, s);
+        const int64_t v = score_host(kind, s, query, lenq, subject, lens);
+        if (score) *score = v;
+        return 0;
+    } catch (const Failure& f) {
+        g_last_error = f.msg;
+        return -1;
+    }
+}
+
+int anyseq_score_device(int kind, const anyseq_scoring* sc, const uint8_t* d_query, int lenq, const uint8_t* d_subject,
+                        int lens, void* stream, int64_t* score) {
+    try {
+        const anyseq_scoring s = sc ? *sc : kAbiScoring;
+        check_scoring(kind, s);
+        Engine& E = engine();
+        std::lock_guard<std::mutex> lk(E.mu);
+        hipStream_t st = stream ? (hipStream_t)stream : E.stream;
+        const int64_t v = score_dev(E, kind, s, d_query, lenq, d_subject, lens, st);
+        if (score) *score = v;
+        return 0;
+    } catch (const Failure& f) {
+        g_last_error = f.msg;
+        return -1;
+    }
+}
+
+int anyseq_construct(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject, int lens,
+                     char* alQuery, char* alSubject, int64_t* score) {
+    try {
+        const anyseq_scoring s = sc ? *sc : kAbiScoring;
+        check_scoring(kind, s);
+        construct_host(kind, s, query, lenq, subject, lens, alQuery, alSubject);
+        if (score) *score = score_host(kind, s, query, lenq, subject, lens);
+        return 0;
+    } catch (const Failure& f) {
+        g_last_error = f.msg;
+        return -1;
+    }
+}
+
+int anyseq_set_device(int device) {
+    std::lock_guard<std::mutex> lk(g_engines_mu);
+    g_device = device;
+    return 0;
+}
+
+int anyseq_get_device(void) { return g_device < 0 ? env_int("ANYSEQ_DEVICE", 0) : g_device; }
+
+const char* anyseq_last_error(void) { return g_last_error.c_str(); }
+
+void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid) {
+    std::lock_guard<std::mutex> lk(g_engines_mu);
+    g_tuning_init = true;
+    if (rows_per_lane > 0) g_tuning.R = rows_per_lane;
+    if (waves_per_group > 0) g_tuning.NW = waves_per_group;
+    if (grid >= 0) g_tuning.grid = grid;
+}
+
+void anyseq_last_fill_timing(double* ms, int* launches) {
+    if (ms) *ms = g_fill_ms;
+    if (launches) *launches = g_fill_launches;
+    g_fill_ms = 0.0;
+    g_fill_launches = 0;
+}
+
+void anyseq_main_random_pair(int64_t minlen, int64_t maxlen, char* query, int64_t* lenq, char* subject,
+                             int64_t* lens) {
+    // main.cpp:90-120 (uniform_ACGT_distribution, random_string) and :207-209
+    std::mt19937_64 urng;
+    auto gen = [&](char* out) -> int64_t {
+        const size_t len = std::uniform_int_distribution<size_t>{(size_t)minlen, (size_t)maxlen}(urng);
+        std::uniform_int_distribution<char> d{0, 3};
+        static const char acgt[4] = {'A', 'C', 'G', 'T'};
+        for (size_t i = 0; i < len; ++i) {
+            const int r = d(urng);
+            out[i] = (r >= 0 && r < 4) ? acgt[r] : '_';
+        }
+        return (int64_t)len;
+    };
+    *lenq = gen(query);
+    *lens = gen(subject);
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// anyseq_internal.h — shared types between the HIP kernels and the host engine.
+//
+// Value spaces used by the fill kernels:
+//   * linear global / semiglobal run in "G-space": G[r][c] = H[r][c] - (r+c+2)*gap,
+//     so the recurrence of align.impala:46-67 becomes G = max3(G_diag + w, G_left, G_up)
+//     with w = sub - 2*gap (4 for a match, 1 for a mismatch under (2,-1,-1));
+//   * linear local runs in "H-space": H = sat(max3(H_diag + sub - gap, H_left, H_up) + gap)
+//     (align.impala:69-79, the clamp at 0 folded into one saturating subtract).
+#pragma once
+#include <stdint.h>
+
+namespace anyseq {
+
+enum Kind : int32_t { KIND_GLOBAL = 0, KIND_SEMIGLOBAL = 1, KIND_LOCAL = 2 };
+
+// One rectangular DP sub-problem (a whole matrix, one Hirschberg half, ...).
+// Row r of the sub-problem reads query byte q[q_off + q_step*r]; column c reads
+// subject byte s[s_off + s_step*c] (q_step/s_step = +1 forward, -1 reversed:
+// get_sequence_acc_half, traceback_lintime.impala:137-148).  Borders are the
+// scheme's init relative to the sub-problem (scoring.impala:261-299).
+struct DPProblem {
+    const uint8_t* q;
+    const uint8_t* s;
+    int32_t q_off, q_step;
+    int32_t s_off, s_step;
+    int32_t h, w;
+    int32_t nbands;        // ceil(h / (64*R))
+    int32_t ngroups;       // ceil(nbands / NW)
+    int32_t wpad;          // row-buffer pitch (multiple of 64, >= w)
+    int32_t pad0;
+    int32_t* out_col;      // optional: H[r][w-1] for r in [0,h)
+    int32_t* out_row;      // optional: raw (kernel value space) bottom row, >= wpad ints
+    int32_t* rowbuf;       // (ngroups-1) * wpad ints: group -> group hand-off rows
+    uint32_t* flags;       // ngroups entries, chunk progress of each group's last band
+    int32_t* best;         // optional (local): atomicMax of every cell
+    int32_t* pad1;
+};
+
+struct GroupRef {
+    int32_t prob;
+    int32_t group;
+};
+
+struct FillParams {
+    int32_t kind;
+    int32_t match, mismatch, gap;     // linear (gap < 0)
+    int32_t gap_open, gap_extend;     // affine (gap_open <= 0, gap_extend < 0)
+    int32_t affine;
+    int32_t pad;
+};
+
+// Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).
+struct PartInfo {
+    int32_t off;          // first row of the part
+    int32_t len;          // rows of the part
+    int32_t rhw;          // right-half width
+    int32_t split_index;  // logical index into splits set by set_split_position
+};
+
+// One final-level 128-column block (iteration_*:121-173).
+struct BlockInfo {
+    int32_t oi, h;        // rows [oi, oi+h)
+    int32_t oj, w;        // cols [oj, oj+w)
+    int64_t pred_base;    // byte offset of the block's anti-diagonal-major predecessor slab
+};
+
+// Device-side error codes written to the error word.
+enum : uint32_t { ERR_NONE = 0, ERR_SPIN_TIMEOUT = 1 };
+
+}  // namespace anyseq

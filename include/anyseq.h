@@ -1,0 +1,99 @@
+/*
+ * anyseq.h — C-ABI of the MI355X-native AnySeq engine (libanyseq.so).
+ *
+ * The first block is exactly the reference's FFI for the hot path:
+ *   /root/reference/src/import.h:14-41 (+ datatypes.h:14 score_t = int64_t),
+ * defined there by export.impala:5-166.  The reference's own driver
+ * (src/main.cpp, sequence_io.cpp, alignment_io.cpp) compiles unchanged against
+ * this header and links against libanyseq.so.
+ *
+ * Fixed scoring for these six: match +2, mismatch -1, linear gap -1
+ * (linear_scoring_scheme(2,-1,-1), export.impala:14,33,70,89,126,145).
+ *
+ * Semantics (bit-exact with the reference CPU path, iteration_cpu/scoring_cpu,
+ * with `benchmark` running its body once — SURVEY.md §0.1):
+ *   *_score       optimal score: global H[n-1][m-1]; semiglobal max over the last
+ *                 row/column incl. the zero border; local max cell (an empty
+ *                 sequence gives -2147483647, the never-written slot value).
+ *   construct_*   alQuery/alSubject (caller-allocated, >= lenq+lens bytes each)
+ *                 receive the reference's sparse layout: [0, lenq+lens) first set
+ *                 to ' ', then each traceback step writes at i+j+1, gaps are '_'
+ *                 (traceback.impala:14-80), no NUL written.  The strings come from
+ *                 the reference's column-split Hirschberg (align.impala:237-311).
+ *                 Return value: the reference's literal value (-lenq / 0 /
+ *                 -2147483647) unless ANYSEQ_CONSTRUCT_TRUE_SCORE=1
+ *                 is set in the environment, in which case the optimal score.
+ * Errors: on an internal GPU failure these return INT64_MIN and print to stderr;
+ * anyseq_last_error() holds the message.
+ */
+#ifndef ANYSEQ_H_
+#define ANYSEQ_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- reference ABI: import.h:14-27 ---- */
+int64_t construct_global_alignment(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                   char* alSubject);
+int64_t construct_semiglobal_alignment(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                       char* alSubject);
+int64_t construct_local_alignment(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                  char* alSubject);
+
+/* ---- reference ABI: import.h:31-41 ---- */
+int64_t global_alignment_score(const char* query, int lenq, const char* subject, int lens);
+int64_t semiglobal_alignment_score(const char* query, int lenq, const char* subject, int lens);
+int64_t local_alignment_score(const char* query, int lenq, const char* subject, int lens);
+
+/* ---- extended API (build-defined; not part of the reference) ---- */
+enum { ANYSEQ_GLOBAL = 0, ANYSEQ_SEMIGLOBAL = 1, ANYSEQ_LOCAL = 2 };
+
+/* Scoring: substitution match/mismatch; a gap of length k costs gap_open + k*gap_extend.
+ * gap_open == 0 is the reference's linear scheme (gap = gap_extend).  Requires
+ * gap_extend < 0 and gap_open <= 0. */
+typedef struct {
+    int32_t match, mismatch, gap_open, gap_extend;
+} anyseq_scoring;
+
+/* Host buffers in, optimal score out.  Returns 0 on success, <0 on error. */
+int anyseq_score(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject, int lens,
+                 int64_t* score);
+
+/* Device-resident inputs (d_query/d_subject are device pointers of the current
+ * device); runs on `stream` (hipStream_t, NULL = the engine's own stream) and
+ * returns after the score has been copied back. */
+int anyseq_score_device(int kind, const anyseq_scoring* sc, const uint8_t* d_query, int lenq, const uint8_t* d_subject,
+                        int lens, void* stream, int64_t* score);
+
+/* Linear-space alignment with the reference's column-split Hirschberg, sparse
+ * i+j+1 layout as construct_*; *score (optional) receives the optimal score. */
+int anyseq_construct(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject, int lens,
+                     char* alQuery, char* alSubject, int64_t* score);
+
+/* Device selection (default: $ANYSEQ_DEVICE or 0) and diagnostics. */
+int anyseq_set_device(int device);
+int anyseq_get_device(void);
+const char* anyseq_last_error(void);
+
+/* Fill-kernel tuning: rows per lane (1,2,4), compute waves per workgroup (4,8),
+ * persistent grid size (0 = one workgroup per CU).  0 keeps the current value. */
+void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid);
+
+/* Timing of the most recent fill launch(es) of the calling thread, measured with
+ * HIP events on the engine stream: total kernel milliseconds and launch count. */
+void anyseq_last_fill_timing(double* ms, int* launches);
+
+/* main.cpp's random input generator (main.cpp:90-120, 200-210): mt19937_64 with the
+ * default seed, lengths uniform in [minlen, maxlen], bases uniform over ACGT.
+ * query/subject must hold maxlen bytes; lengths are returned. */
+void anyseq_main_random_pair(int64_t minlen, int64_t maxlen, char* query, int64_t* lenq, char* subject,
+                             int64_t* lens);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ANYSEQ_H_ */
