@@ -1,0 +1,62 @@
+"""GPU path against the committed golden fixtures (incl. the full 65536^2 configs[1]
+inputs: size-independent pinning by the oracle-generated scores)."""
+import json
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+KINDS = ("global", "semiglobal", "local")
+
+
+def load(name):
+    return json.load(open(os.path.join(GOLD, name)))
+
+
+def test_kat(anyseq):
+    for c in load("kat.json")["scores"]:
+        for k, v in c["score"].items():
+            assert getattr(anyseq, f"{k}_alignment_score")(c["q"], c["s"]) == v, (k, c)
+    for c in load("kat.json")["constructs"]:
+        r, aq, as_ = getattr(anyseq, f"construct_{c['kind']}_alignment")(c["q"], c["s"])
+        assert (r, aq.decode(), as_.decode()) == (c["ret"], c["alq"], c["als"]), c["kind"]
+
+
+def test_oracle_cases(anyseq):
+    for c in load("oracle_cases.json")["cases"]:
+        for k in KINDS:
+            assert getattr(anyseq, f"{k}_alignment_score")(c["q"], c["s"]) == c["score"][k]
+            r, aq, as_ = getattr(anyseq, f"construct_{k}_alignment")(c["q"], c["s"])
+            g = c["construct"][k]
+            assert (r, aq.decode(), as_.decode()) == (g["ret"], g["alq"], g["als"]), (k, len(c["q"]), len(c["s"]))
+
+
+def test_main_1024(anyseq):
+    g = load("main_1024.json")
+    q, s = anyseq.main_random_pair(1024, 1024)
+    for k in KINDS:
+        assert getattr(anyseq, f"{k}_alignment_score")(q, s) == g["score"][k]
+        r, aq, as_ = getattr(anyseq, f"construct_{k}_alignment")(q, s)
+        gc = g["construct"][k]
+        assert (r, aq.decode(), as_.decode()) == (gc["ret"], gc["alq"], gc["als"]), k
+
+
+def test_main_65536_scores(anyseq):
+    g = load("main_65536.json")
+    q, s = anyseq.main_random_pair(65536, 65536)
+    for k in KINDS:
+        assert getattr(anyseq, f"{k}_alignment_score")(q, s) == g["score"][k], k
+
+
+def test_main_65536_global_construct_properties(anyseq):
+    """Full-size construct: the sparse layout decodes to both input sequences and the
+    dense alignment's score equals the golden optimal score (size-independent check)."""
+    g = load("main_65536.json")
+    q, s = anyseq.main_random_pair(65536, 65536)
+    r, aq, as_ = anyseq.construct_global_alignment(q, s)
+    assert r == -len(q)
+    dq, ds = anyseq.dense(aq, as_)
+    assert dq.replace(b"_", b"") == q and ds.replace(b"_", b"") == s
+    sc = sum(-1 if (a == 95 or b == 95) else (2 if a == b else -1) for a, b in zip(dq, ds))
+    assert sc == g["score"]["global"]
