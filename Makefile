@@ -19,8 +19,14 @@ $(LIB): $(SRC)/anyseq_kernels.o $(SRC)/anyseq_engine.o
 oracle:
 	$(MAKE) -s -C oracle
 
+# diagnostic build with s_memtime stamps (tools only; never loaded by the product path)
+stamps: anyseq_amd/libanyseq_stamps.so
+anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.cpp $(SRC)/anyseq_internal.h
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_stamps.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o
+
 clean:
 	rm -f $(SRC)/*.o $(LIB)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean stamps

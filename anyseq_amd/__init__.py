@@ -21,7 +21,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libanyseq.so")
+# ANYSEQ_LIB selects a diagnostic build of the same library (e.g. the s_memtime
+# stamp build libanyseq_stamps.so); the product build is libanyseq.so.
+LIB_PATH = os.environ.get("ANYSEQ_LIB") or os.path.join(_HERE, "libanyseq.so")
 
 GLOBAL, SEMIGLOBAL, LOCAL = 0, 1, 2
 KINDS = {"global": GLOBAL, "semiglobal": SEMIGLOBAL, "local": LOCAL}
@@ -62,6 +64,8 @@ _lib.anyseq_construct.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int,
 _lib.anyseq_last_error.restype = _c_p
 _lib.anyseq_set_device.argtypes = [_c_int]
 _lib.anyseq_set_tuning.argtypes = [_c_int, _c_int, _c_int]
+_lib.anyseq_set_option.restype = _c_int
+_lib.anyseq_set_option.argtypes = [_c_p, _c_int]
 _lib.anyseq_last_fill_timing.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int)]
 _lib.anyseq_main_random_pair.argtypes = [_c_i64, _c_i64, _vp, ctypes.POINTER(_c_i64), _vp,
                                          ctypes.POINTER(_c_i64)]
@@ -172,6 +176,12 @@ def set_device(dev: int) -> None:
 
 def set_tuning(rows_per_lane: int = 0, waves_per_group: int = 0, grid: int = -1) -> None:
     _lib.anyseq_set_tuning(rows_per_lane, waves_per_group, grid)
+
+
+def set_option(name: str, value: int) -> None:
+    """Engine tuning: rows_per_lane, lane_skew_extra, waves_per_group, grid, fronts."""
+    if _lib.anyseq_set_option(name.encode(), int(value)) != 0:
+        raise AnySeqError(f"unknown option {name}")
 
 
 def last_fill_timing():

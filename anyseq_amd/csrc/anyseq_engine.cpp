@@ -21,10 +21,13 @@
 using namespace anyseq;
 
 extern "C" {
-hipError_t anyseq_launch_fill(int R, int NW, const DPProblem* probs, const GroupRef* groups, int ngroups,
+hipError_t anyseq_launch_fill(int R, int X, int NW, const DPProblem* probs, const GroupRef* groups, int ngroups,
                               uint32_t* dq, uint32_t* err, const FillParams* fp, int grid, hipStream_t st);
 hipError_t anyseq_launch_semiglobal_reduce(const int32_t* row_g, int m, const int32_t* col_h, int n, int ng,
                                            int32_t* out, hipStream_t st);
+hipError_t anyseq_launch_front_combine(int kind, const int32_t* rowF, int h1, const int32_t* rowB, int h2, int m,
+                                       int gap, const int32_t* colF, const int32_t* colB, int32_t* out,
+                                       hipStream_t st);
 hipError_t anyseq_launch_hb_sum(const void* parts, int nparts, int bpp, int half, const int32_t* L, const int32_t* R,
                                 int kind, int gap, int32_t* bmax, int32_t* bind, int32_t* splits, hipStream_t st);
 hipError_t anyseq_launch_pred(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
@@ -87,8 +90,10 @@ int env_int(const char* name, int dflt) {
 
 struct Tuning {
     int R = 1;
-    int NW = 8;
+    int X = 0;
+    int NW = 4;
     int grid = 0;
+    int fronts = 2;
 };
 
 struct Engine {
@@ -123,6 +128,7 @@ Engine& engine() {
     if (!g_tuning_init) {
         g_tuning.R = env_int("ANYSEQ_R", g_tuning.R);
         g_tuning.NW = env_int("ANYSEQ_NW", g_tuning.NW);
+        g_tuning.X = env_int("ANYSEQ_X", g_tuning.X);
         g_tuning.grid = env_int("ANYSEQ_GRID", g_tuning.grid);
         g_tuning_init = true;
     }
@@ -173,12 +179,20 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     HIPCHECK(hipMemcpyAsync(d_probs, probs.data(), probs.size() * sizeof(DPProblem), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(d_groups, groups.data(), groups.size() * sizeof(GroupRef), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemsetAsync(flags, 0, flag_words * 4, st));
-    uint32_t* ctr = (uint32_t*)E.ctr.get(64);
+    uint32_t* ctr = (uint32_t*)E.ctr.get(128);
     HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));  // ctr[0] = dequeue counter, ctr[1] = error word
     int grid = g_tuning.grid > 0 ? g_tuning.grid : E.num_cus;
     grid = std::min<int>(grid, (int)groups.size());
+    FillParams fpl = fp;
+    unsigned long long* dbg = nullptr;
+    if (getenv("ANYSEQ_STAMPS")) {
+        dbg = (unsigned long long*)E.ctr.get(64) + 4;   // ctr[8..] (bytes 32..95)
+        HIPCHECK(hipMemsetAsync(dbg, 0, 8 * 8, st));
+        fpl.dbg = dbg;
+    }
     HIPCHECK(hipEventRecord(E.ev0, st));
-    HIPCHECK(anyseq_launch_fill(R, NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fp, grid, st));
+    HIPCHECK(anyseq_launch_fill(R, g_tuning.X ? 1 : 0, NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fpl,
+                                grid, st));
     HIPCHECK(hipEventRecord(E.ev1, st));
     HIPCHECK(hipEventSynchronize(E.ev1));
     float ms = 0.f;
@@ -187,6 +201,15 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     g_fill_launches += 1;
     uint32_t err = 0;
     HIPCHECK(hipMemcpy(&err, ctr + 1, 4, hipMemcpyDeviceToHost));
+    if (dbg) {
+        unsigned long long h[8];
+        HIPCHECK(hipMemcpy(h, dbg, sizeof h, hipMemcpyDeviceToHost));
+        fprintf(stderr,
+                "anyseq stamps: %.3f ms R=%d NW=%d bands=%llu blocks=%llu | per band: total %.0f cyc, compute %.0f, "
+                "wait_in %.0f, wait_s %.0f, wait_out %.0f | compute/block %.1f cyc\n",
+                ms, R, NW, h[5], h[6], (double)h[0] / h[5], (double)h[1] / h[5], (double)h[2] / h[5],
+                (double)h[3] / h[5], (double)h[4] / h[5], (double)h[1] / std::max(1ull, h[6]));
+    }
     if (err) fail("fill kernel reported error %u (spin timeout)", err);
 }
 
@@ -200,6 +223,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.gap_open = sc.gap_open;
     fp.gap_extend = sc.gap_extend;
     fp.affine = sc.gap_open != 0;
+    fp.dbg = nullptr;
     return fp;
 }
 
@@ -218,39 +242,68 @@ int64_t empty_score(int kind, int n, int m, const anyseq_scoring& sc) {
 }
 
 // Fill-based score on device-resident sequences (align.impala:218-235).
+// Matrices with enough rows run as two fronts (top half forward, bottom half on
+// reversed sequences) in ONE launch and are combined by a row split
+// (front_combine_kernel): the pipeline depth of the band wavefront halves.
 int64_t score_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds, int m,
                   hipStream_t st) {
     if (n <= 0 || m <= 0) return empty_score(kind, n, m, sc);
     const FillParams fp = make_params(kind, sc);
+    const int wpad = (m + 63) & ~63;
+    int32_t* res = (int32_t*)E.ctr.get(128) + 4;
+    HIPCHECK(hipMemsetAsync(res, kind == KIND_LOCAL ? 0 : 0x80, 4, st));  // local: 0; else ~INT_MIN
+    const bool two_fronts = g_tuning.fronts > 1 && n >= 2 * 64 * rows_per_lane() * waves_per_group();
+    std::vector<DPProblem> probs;
     DPProblem P;
     memset(&P, 0, sizeof P);
     P.q = dq;
     P.s = ds;
-    P.q_off = 0;
     P.q_step = 1;
-    P.s_off = 0;
     P.s_step = 1;
-    P.h = n;
     P.w = m;
-    int32_t* res = (int32_t*)E.ctr.get(64) + 4;
-    if (kind != KIND_LOCAL) P.out_col = (int32_t*)E.outcol.get((size_t)n * 4);
-    if (kind == KIND_SEMIGLOBAL) P.out_row = (int32_t*)E.outrow.get((size_t)((m + 63) & ~63) * 4);
-    if (kind == KIND_LOCAL) {
-        P.best = res;
-        HIPCHECK(hipMemsetAsync(res, 0, 4, st));
+    if (!two_fronts) {
+        P.h = n;
+        if (kind != KIND_LOCAL) P.out_col = (int32_t*)E.outcol.get((size_t)n * 4);
+        if (kind == KIND_SEMIGLOBAL) P.out_row = (int32_t*)E.outrow.get((size_t)wpad * 4);
+        if (kind == KIND_LOCAL) P.best = res;
+        probs.push_back(P);
+        run_fill(E, probs, fp, st);
+        int32_t v = 0;
+        if (kind == KIND_GLOBAL) {
+            HIPCHECK(hipMemcpyAsync(&v, P.out_col + (n - 1), 4, hipMemcpyDeviceToHost, st));
+        } else if (kind == KIND_SEMIGLOBAL) {
+            HIPCHECK(hipMemsetAsync(res, 0, 4, st));
+            HIPCHECK(anyseq_launch_semiglobal_reduce(P.out_row, m, P.out_col, n, -sc.gap_extend, res, st));
+            HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, st));
+        } else {
+            HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, st));
+        }
+        HIPCHECK(hipStreamSynchronize(st));
+        return v;
     }
-    std::vector<DPProblem> probs{P};
+    const int h1 = n / 2, h2 = n - h1;
+    int32_t* rows = (int32_t*)E.outrow.get((size_t)2 * wpad * 4);
+    int32_t* cols = kind == KIND_SEMIGLOBAL ? (int32_t*)E.outcol.get((size_t)n * 4) : nullptr;
+    // top front: rows [0, h1) forward
+    P.h = h1;
+    P.out_row = rows;
+    P.out_col = cols;
+    if (kind == KIND_LOCAL) P.best = res;
+    probs.push_back(P);
+    // bottom front: rows [h1, n) with query and subject reversed
+    P.q_off = n - 1;
+    P.q_step = -1;
+    P.s_off = m - 1;
+    P.s_step = -1;
+    P.h = h2;
+    P.out_row = rows + wpad;
+    P.out_col = cols ? cols + h1 : nullptr;
+    probs.push_back(P);
     run_fill(E, probs, fp, st);
+    HIPCHECK(anyseq_launch_front_combine(kind, rows, h1, rows + wpad, h2, m, sc.gap_extend, cols,
+                                         cols ? cols + h1 : nullptr, res, st));
     int32_t v = 0;
-    if (kind == KIND_GLOBAL) {
-        HIPCHECK(hipMemcpyAsync(&v, P.out_col + (n - 1), 4, hipMemcpyDeviceToHost, st));
-    } else if (kind == KIND_SEMIGLOBAL) {
-        HIPCHECK(hipMemsetAsync(res, 0, 4, st));
-        HIPCHECK(anyseq_launch_semiglobal_reduce(P.out_row, m, P.out_col, n, -sc.gap_extend, res, st));
-        HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, st));
-    } else {
-        HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, st));
-    }
+    HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     return v;
 }
@@ -515,10 +568,34 @@ const char* anyseq_last_error(void) { return g_last_error.c_str(); }
 
 void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid) {
     std::lock_guard<std::mutex> lk(g_engines_mu);
+    if (!g_tuning_init) {
+        g_tuning.X = env_int("ANYSEQ_X", g_tuning.X);
+        g_tuning.fronts = env_int("ANYSEQ_FRONTS", g_tuning.fronts);
+    }
     g_tuning_init = true;
     if (rows_per_lane > 0) g_tuning.R = rows_per_lane;
     if (waves_per_group > 0) g_tuning.NW = waves_per_group;
     if (grid >= 0) g_tuning.grid = grid;
+}
+
+int anyseq_set_option(const char* name, int value) {
+    std::lock_guard<std::mutex> lk(g_engines_mu);
+    if (!g_tuning_init) {
+        g_tuning.R = env_int("ANYSEQ_R", g_tuning.R);
+        g_tuning.NW = env_int("ANYSEQ_NW", g_tuning.NW);
+        g_tuning.grid = env_int("ANYSEQ_GRID", g_tuning.grid);
+        g_tuning.X = env_int("ANYSEQ_X", g_tuning.X);
+        g_tuning.fronts = env_int("ANYSEQ_FRONTS", g_tuning.fronts);
+        g_tuning_init = true;
+    }
+    const std::string n = name ? name : "";
+    if (n == "rows_per_lane") g_tuning.R = value;
+    else if (n == "lane_skew_extra") g_tuning.X = value;
+    else if (n == "waves_per_group") g_tuning.NW = value;
+    else if (n == "grid") g_tuning.grid = value;
+    else if (n == "fronts") g_tuning.fronts = value;
+    else return -1;
+    return 0;
 }
 
 void anyseq_last_fill_timing(double* ms, int* launches) {

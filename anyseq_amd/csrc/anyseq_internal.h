@@ -47,6 +47,7 @@ struct FillParams {
     int32_t gap_open, gap_extend;     // affine (gap_open <= 0, gap_extend < 0)
     int32_t affine;
     int32_t pad;
+    unsigned long long* dbg;          // diagnostic build only (ANYSEQ_STAMPS): per-launch stamp sums
 };
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).

@@ -40,24 +40,31 @@ __device__ __forceinline__ bool err_set(uint32_t* err) {
 }
 
 __device__ __forceinline__ bool spin_lds_ge(uint32_t* p, uint32_t target, uint32_t* err) {
-    if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        return true;
+    }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+    uint32_t it = 0;
+    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err)) {
+        // the error word lives in HBM: look at it (and the clock) only every 256 polls
+        if ((++it & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
             atomicOr(err, ERR_SPIN_TIMEOUT);
             return false;
         }
     }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     return true;
 }
 
 __device__ __forceinline__ bool spin_glb_ge(uint32_t* p, uint32_t target, uint32_t* err) {
     if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t it = 0;
     while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err)) {
+        if ((++it & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
             atomicOr(err, ERR_SPIN_TIMEOUT);
             return false;
         }
@@ -80,18 +87,23 @@ __device__ __forceinline__ int to_h(int v, int r, int c, int ng) {
     return KIND == KIND_LOCAL ? v : v - (r + c + 2) * ng;
 }
 
-constexpr int kSlots = 16;    // in-ring depth in chunks
-constexpr int kSRing = 256;   // subject ring bytes per wave (+64 mirrored)
+constexpr int kSlots = 16;     // in-ring depth in chunks
+constexpr int kSRing = 4096;   // shared subject ring bytes per workgroup (+64 mirrored)
+constexpr int kMaxBack = 5 * 64 + 32;   // deepest look-back of a reader: D = 64(R+1) for R <= 4, + 1 chunk
 
 // LDS of one workgroup: NW compute waves + 1 I/O wave.  in_ring[w] feeds compute
 // wave w (written by wave w-1, or by the I/O wave for w = 0); in_ring[NW] is the
-// out-ring from the group's last compute wave to the I/O wave.
+// out-ring from the group's last compute wave to the I/O wave.  s_ring holds the
+// subject bytes of the group's columns, staged by the I/O wave ahead of wave 0
+// and recycled behind the trailing wave.
 template <int NW, int CH>
 struct FillShared {
     int32_t in_ring[NW + 1][kSlots * CH];
-    uint8_t s_ring[NW][kSRing + 64];
+    uint8_t s_ring[kSRing + 64];
     uint32_t prod[NW + 1];
     uint32_t cons[NW + 1];
+    uint32_t s_filled;   // subject chunks staged
+    uint32_t tail;       // blocks completed by the trailing compute wave
     int32_t group;
 };
 
@@ -101,42 +113,98 @@ struct CellK {
     int wm, wx, ng;
 };
 
+// LDS progress counters between waves of one workgroup.  The LDS executes one
+// wave's DS instructions in issue order, so a counter store issued after the
+// data stores is observed after them, and a data load issued after the counter
+// load returned reads the published data: relaxed DS accesses plus compiler
+// fences suffice.
 __device__ __forceinline__ uint32_t lds_ld(uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    return v;
 }
 __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// One step of the band wavefront: lane l processes column c = t - 1 - l.
-// MASK: some lanes are outside [0, w) in this step.  PARTIAL: rows >= h (dead
-// rows) pass the value from above through, so lane 63 always carries row h-1.
-template <int KIND, int R, bool MASK, bool PARTIAL>
-__device__ __forceinline__ void band_step(int t, int lane, int w, int topv, int sc, const int (&qv)[R],
-                                          const bool (&dead)[R], int (&cur)[R], int& dg, int& outv, int& best,
-                                          const CellK ck) {
-    int up = wave_shr1(topv, cur[R - 1]);
-    int diag = dg;
-    dg = up;
-    const bool act = MASK ? ((unsigned)(t - 1 - lane) < (unsigned)w) : true;
+// Global-memory views (address space 1): global_load/global_store count only
+// vmcnt, never lgkmcnt.
+#define GLOBAL_AS __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ GLOBAL_AS T* gmem(T* p) {
+    return (GLOBAL_AS T*)p;
+}
+
+// Diagnostic stamps (separate build with -DANYSEQ_STAMPS; never in the product build):
+// per-launch sums of wave cycles spent in compute blocks and in each kind of wait.
+#ifdef ANYSEQ_STAMPS
+#define STAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define STAMP_ADD(slot, v) acc[slot] += (v)
+#else
+#define STAMP(var)
+#define STAMP_ADD(slot, v)
+#endif
+enum { ST_TOTAL = 0, ST_COMPUTE, ST_WAIT_IN, ST_WAIT_S, ST_WAIT_OUT, ST_BANDS, ST_BLOCKS, ST_IO_TOTAL, ST_NSLOTS };
+
+// Band geometry.  Lane l owns rows r_k = rb + R*l + k (k < R) and at step t
+// row k processes column
+//     c_k(t) = t - BASE - S*l - k,   S = R + X,  BASE = 1 + X.
+// Consequences (derived in DESIGN.md §3.1):
+//  * rows k >= 1 read up = cur[k-1] and diag = prev[k-1] of their own lane, so
+//    the R cells of a step are independent (ILP = R);
+//  * row 0 reads lane l-1's row R-1 at the same column, produced 1 + X steps
+//    earlier and moved by one DPP wave_shr:1 (X = 1 issues it one step ahead,
+//    off the critical path, at the price of a 2-step lane skew);
+//  * lane 63's row R-1 produces column t - D, D = 64 (R + X), so bottom-row
+//    chunks stay CH-aligned.
+template <int R, int X>
+struct BandGeom {
+    static constexpr int S = R + X;             // lane skew (steps)
+    static constexpr int BASE = 1 + X;          // lane 0 / row 0 processes column t - BASE
+    static constexpr int D = 64 * R + 64 * X;   // lane 63 / row R-1 processes column t - D
+};
+
+// One step.  MASK: some rows are outside [0, w) in this step.  PARTIAL: rows
+// >= h pass the value from above through (so lane 63 carries row h-1).
+template <int KIND, int R, int X, bool MASK, bool PARTIAL>
+__device__ __forceinline__ void band_step(int t, int lane, int w, int topv, const int (&sc)[R], const int (&qv)[R],
+                                          const bool (&dead)[R], int (&cur)[R], int (&prev)[R], int& upc, int& dg,
+                                          int& outv, int& best, const CellK ck) {
+    constexpr int S = BandGeom<R, X>::S;
+    constexpr int BASE = BandGeom<R, X>::BASE;
+    // X = 1: DPP for the NEXT step (lane l-1's row R-1 at its start-of-step value);
+    // X = 0: DPP for this step.
+    const int up_dpp = wave_shr1(topv, cur[R - 1]);
+    if (X == 0) upc = up_dpp;
+    int nv[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        const int wgt = (qv[k] == sc) ? ck.wm : ck.wx;
+        const int up = k == 0 ? upc : cur[k - 1];
+        const int diag = k == 0 ? dg : prev[k - 1];
+        const int wgt = (qv[k] == sc[k]) ? ck.wm : ck.wx;
         int v = max(max(diag + wgt, cur[k]), up);
         if (KIND == KIND_LOCAL) v = (int)__builtin_elementwise_sub_sat((unsigned)v, (unsigned)ck.ng);
         if (PARTIAL && dead[k]) v = up;
-        diag = cur[k];
-        if (act) {
-            cur[k] = v;
-            if (KIND == KIND_LOCAL) best = max(best, v);
-        }
-        up = v;
+        nv[k] = v;
     }
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        prev[k] = cur[k];
+        const bool act = MASK ? ((unsigned)(t - BASE - S * lane - k) < (unsigned)w) : true;
+        if (act) {
+            cur[k] = nv[k];
+            if (KIND == KIND_LOCAL) best = max(best, nv[k]);
+        }
+    }
+    dg = upc;
+    if (X == 1) upc = up_dpp;
     outv = cur[R - 1];
 }
 
 struct WaveIO {
     bool in_border;            // band 0: inputs are the scheme's top border
+    bool trailing;             // last compute wave of the group: reports `tail`
     int32_t* my_ring;
     uint32_t* my_prod;
     uint32_t* my_cons;
@@ -144,89 +212,121 @@ struct WaveIO {
     int32_t* next_ring;
     uint32_t* next_prod;
     uint32_t* next_cons;
-    uint8_t* s_ring;
+    const uint8_t* s_ring;
+    uint32_t* s_filled;
+    uint32_t* tail;
 };
 
-template <int KIND, int R, int CH, bool MASK, bool PARTIAL>
+// CH steps t0 .. t0+CH-1.  top_first = top row at column t0-1 (read by the DPP
+// of step t0); ring_blk[u-1] = column t0+u-1.  s_blk[k][u] = subject byte of row k.
+template <int KIND, int R, int X, int CH, bool MASK, bool PARTIAL>
 __device__ __forceinline__ void band_block(int t0, int lane, int w, int top_first, const int32_t* ring_blk,
-                                           const uint8_t* s_blk, const int (&qv)[R], const bool (&dead)[R],
-                                           int (&cur)[R], int& dg, int (&outv)[CH], int& best, const CellK ck) {
+                                           const uint8_t* const (&s_blk)[R], const int (&qv)[R],
+                                           const bool (&dead)[R], int (&cur)[R], int (&prev)[R], int& upc, int& dg,
+                                           int (&outv)[CH], int& best, const CellK ck) {
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
         const int topv = u == 0 ? top_first : ring_blk[u - 1];
-        const int sc = s_blk[u];
-        band_step<KIND, R, MASK, PARTIAL>(t0 + u, lane, w, topv, sc, qv, dead, cur, dg, outv[u], best, ck);
+        int sc[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) sc[k] = s_blk[k][u];
+        band_step<KIND, R, X, MASK, PARTIAL>(t0 + u, lane, w, topv, sc, qv, dead, cur, prev, upc, dg, outv[u], best,
+                                             ck);
     }
 }
 
-template <int KIND, int R, int CH, bool PARTIAL>
-__device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& io, uint32_t* err, const CellK ck) {
+template <int KIND, int R, int X, int CH, bool PARTIAL>
+__device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& io, uint32_t* err, const CellK ck,
+                         unsigned long long* dbg) {
+#ifdef ANYSEQ_STAMPS
+    uint64_t acc[ST_NSLOTS] = {0};
+    STAMP(t_begin);
+#endif
     constexpr int IRM = kSlots * CH - 1;
-    constexpr int LAG = 64 / CH;      // blocks between computing and publishing a chunk
+    constexpr int S = BandGeom<R, X>::S;
+    constexpr int BASE = BandGeom<R, X>::BASE;
+    constexpr int D = BandGeom<R, X>::D;
+    constexpr int LAG = D / CH;      // blocks between computing and publishing a chunk
+    static_assert(D % CH == 0, "bottom-row chunks must stay aligned");
     const int h = P.h, w = P.w, ng = ck.ng;
     const int rb = band * 64 * R;
     const int row0 = rb + lane * R;
 
     int qv[R];
     bool dead[R];
-    int cur[R];
+    int cur[R], prev[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const int r = row0 + k;
         dead[k] = r >= h;
-        qv[k] = dead[k] ? 0x100 : (int)P.q[P.q_off + P.q_step * r];
+        qv[k] = dead[k] ? 0x100 : (int)gmem(P.q)[P.q_off + P.q_step * r];
         cur[k] = border_left<KIND>(r, ng);
+        prev[k] = cur[k];
     }
-    int dg = border_left<KIND>(row0 - 1, ng);
+    // settle the query loads here: no global load is in flight inside the block loop
+#pragma unroll
+    for (int k = 0; k < R; ++k) asm volatile("" : "+v"(qv[k]));
+    int dg = border_left<KIND>(row0 - 1, ng);   // diag of row 0 at its first column
+    int upc = 0;                                 // up of row 0 for the current step
     int outv[CH];
     int best = 0;
 
     const int nchunks = (w + CH - 1) / CH;
     const int nblocks = nchunks + LAG;
-    auto schar = [&](int c) -> uint8_t { return c < w ? P.s[P.s_off + P.s_step * c] : (uint8_t)0; };
-    auto sput = [&](int c, uint8_t v) {
-        const int p = c & (kSRing - 1);
-        io.s_ring[p] = v;
-        if (p < 64) io.s_ring[p + kSRing] = v;
-    };
-    // prologue: subject chars of block 0 into the ring, block 1 into registers
-    if (lane < CH) sput(lane, schar(lane));
-    uint8_t pf1 = lane < CH ? schar(CH + lane) : 0;
+    // last observed values of the LDS counters: most blocks need no LDS round trip
+    uint32_t seen_prod = 0, seen_sfill = 0, seen_cons = 0;
 
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
-        // ---- input chunk b (columns [t0, t0+CH))
+        // ---- input chunk b (columns [t0, t0+CH)) and its subject bytes
         if (b < nchunks) {
+            STAMP(ta);
             if (io.in_border) {
                 if (lane < CH) io.my_ring[(t0 + lane) & IRM] = border_top<KIND>(t0 + lane, ng);
-            } else {
+            } else if (seen_prod < (uint32_t)(b + 1)) {
                 if (!spin_lds_ge(io.my_prod, (uint32_t)(b + 1), err)) return;
+                seen_prod = __builtin_amdgcn_readfirstlane(lds_ld(io.my_prod));
             }
+            STAMP(tb);
+            if (seen_sfill < (uint32_t)(b + 1)) {
+                if (!spin_lds_ge(io.s_filled, (uint32_t)(b + 1), err)) return;
+                seen_sfill = __builtin_amdgcn_readfirstlane(lds_ld(io.s_filled));
+            }
+            STAMP(tc);
+            STAMP_ADD(ST_WAIT_IN, tb - ta);
+            STAMP_ADD(ST_WAIT_S, tc - tb);
         }
+        STAMP(t_comp0);
         const int top_first = b == 0 ? border_left<KIND>(rb - 1, ng) : io.my_ring[(t0 - 1) & IRM];
-        // ---- prefetch subject chars of block b+2
-        const uint8_t pf2 = lane < CH ? schar(t0 + 2 * CH + lane) : (uint8_t)0;
-
         const int32_t* ring_blk = io.my_ring + (t0 & IRM);
-        const uint8_t* s_blk = io.s_ring + ((t0 - 1 - lane) & (kSRing - 1));
-        const bool full = (t0 >= 64) && (t0 + CH <= w + 1);
+        const uint8_t* s_blk[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) s_blk[k] = io.s_ring + ((t0 - BASE - S * lane - k) & (kSRing - 1));
+        const bool full = (t0 >= D) && (t0 + CH <= w + BASE);
         if (full)
-            band_block<KIND, R, CH, false, PARTIAL>(t0, lane, w, top_first, ring_blk, s_blk, qv, dead, cur, dg, outv,
-                                                    best, ck);
+            band_block<KIND, R, X, CH, false, PARTIAL>(t0, lane, w, top_first, ring_blk, s_blk, qv, dead, cur, prev,
+                                                       upc, dg, outv, best, ck);
         else
-            band_block<KIND, R, CH, true, PARTIAL>(t0, lane, w, top_first, ring_blk, s_blk, qv, dead, cur, dg, outv,
-                                                   best, ck);
+            band_block<KIND, R, X, CH, true, PARTIAL>(t0, lane, w, top_first, ring_blk, s_blk, qv, dead, cur, prev,
+                                                      upc, dg, outv, best, ck);
+        STAMP(t_comp1);
+        STAMP_ADD(ST_COMPUTE, t_comp1 - t_comp0);
 
         // ---- release chunks < b (column t0+CH-1 of chunk b is still read by block b+1)
         if (!io.in_border) lds_st(io.my_cons, (uint32_t)b);
-        // ---- subject chars of block b+1 into the ring
-        if (lane < CH) sput(t0 + CH + lane, pf1);
-        pf1 = pf2;
+        if (io.trailing) lds_st(io.tail, (uint32_t)(b + 1));
 
         // ---- publish bottom-row chunk j = b - LAG (lane 63 holds it in outv)
         const int j = b - LAG;
         if (io.out_lds && j >= 0) {
-            if (!spin_lds_ge(io.next_cons, (uint32_t)max(0, j - kSlots + 1), err)) return;
+            const uint32_t need = (uint32_t)max(0, j - kSlots + 1);
+            STAMP(to0);
+            if (seen_cons < need) {
+                if (!spin_lds_ge(io.next_cons, need, err)) return;
+                seen_cons = __builtin_amdgcn_readfirstlane(lds_ld(io.next_cons));
+            }
+            STAMP(to1);
+            STAMP_ADD(ST_WAIT_OUT, to1 - to0);
             if (lane == 63) {
                 int4* dst = reinterpret_cast<int4*>(io.next_ring + ((j * CH) & IRM));
 #pragma unroll
@@ -237,13 +337,14 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         }
     }
     if (!io.in_border) lds_st(io.my_cons, (uint32_t)(nchunks + kSlots));
+    if (io.trailing) lds_st(io.tail, 0x7fffffffu);
 
     // ---- last column (H space) and local maximum
     if (P.out_col) {
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int r = row0 + k;
-            if (r < h) P.out_col[r] = to_h<KIND>(cur[k], r, w - 1, ng);
+            if (r < h) gmem(P.out_col)[r] = to_h<KIND>(cur[k], r, w - 1, ng);
         }
     }
     if (KIND == KIND_LOCAL && P.best) {
@@ -251,31 +352,88 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
         if (lane == 0) atomicMax(P.best, best);
     }
+#ifdef ANYSEQ_STAMPS
+    STAMP(t_end);
+    acc[ST_TOTAL] = t_end - t_begin;
+    acc[ST_BANDS] = 1;
+    acc[ST_BLOCKS] = nblocks;
+    if (dbg && lane == 0)
+        for (int i = 0; i < ST_NSLOTS; ++i) atomicAdd(dbg + i, (unsigned long long)acc[i]);
+#endif
 }
 
-// The I/O wave: copies the previous group's bottom row (HBM, sc1 loads behind a
-// relaxed progress flag) into compute wave 0's in-ring, and this group's bottom
-// row from the out-ring to HBM (sc1 stores, vmcnt(0), then the flag) — the
-// global hand-off latency never sits on a compute wave's critical path.
+// The I/O wave of a workgroup:
+//  * stages the subject bytes of the group's columns into the shared s_ring
+//    (ahead of wave 0, never overwriting bytes the trailing wave still reads);
+//  * copies the previous group's bottom row (HBM, sc1 loads behind a relaxed
+//    progress flag) into compute wave 0's in-ring;
+//  * copies this group's bottom row from the out-ring to HBM (sc1 stores,
+//    vmcnt(0), then the flag).
+// The HBM hand-off latency therefore never sits on a compute wave's critical path.
 template <int CH>
-__device__ void io_wave(int lane, int nchunks, const int32_t* g_in, uint32_t* g_in_flag, int32_t* ring0,
-                        uint32_t* prod0, uint32_t* cons0, int32_t* g_out, uint32_t* g_out_flag, int32_t* oring,
-                        uint32_t* oprod, uint32_t* ocons, uint32_t* err) {
+__device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* s_filled,
+                        uint32_t* tail, const int32_t* g_in, uint32_t* g_in_flag, int32_t* ring0, uint32_t* prod0,
+                        uint32_t* cons0, int32_t* g_out, uint32_t* g_out_flag, int32_t* oring, uint32_t* oprod,
+                        uint32_t* ocons, uint32_t* err) {
     constexpr int IRM = kSlots * CH - 1;
+    constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
+    const int nchunks = (w + CH - 1) / CH;
     const bool need_in = g_in != nullptr, need_out = g_out != nullptr;
-    int in_next = 0, out_next = 0;
-    uint32_t avail = 0;
+    const GLOBAL_AS uint8_t* sg = gmem(s);
+    int s_next = 0, in_next = 0, out_next = 0;
+    uint32_t avail = 0, idle = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    while ((need_in && in_next < nchunks) || (need_out && out_next < nchunks)) {
+    while (s_next < nchunks || (need_in && in_next < nchunks) || (need_out && out_next < nchunks)) {
         bool progress = false;
+        if (s_next < nchunks) {
+            const uint32_t tl = lds_ld(tail);
+            // the trailing wave in block `tl` still reads columns >= tl*CH - kMaxBack
+            int lim = (int)min((uint32_t)nchunks, tl >= 0x7fffffffu ? (uint32_t)nchunks
+                                                                     : tl + SCH - kMaxBack / CH - 1);
+            lim = min(lim, s_next + 1024 / CH);   // one batch: 16 loads in flight per lane
+            if (lim > s_next) {
+                const int c0 = s_next * CH;
+                uint8_t v[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int c = c0 + i * 64 + lane;
+                    v[i] = (c < w && c < lim * CH) ? sg[s_off + s_step * c] : (uint8_t)0;
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int c = c0 + i * 64 + lane;
+                    if (c < lim * CH) {
+                        const int p = c & (kSRing - 1);
+                        s_ring[p] = v[i];
+                        if (p < 64) s_ring[p + kSRing] = v[i];
+                    }
+                }
+                lds_st(s_filled, (uint32_t)lim);
+                s_next = lim;
+                progress = true;
+            }
+        }
         if (need_in && in_next < nchunks) {
             if ((int)avail <= in_next)
-                avail = __hip_atomic_load(g_in_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                avail = __hip_atomic_load(gmem(g_in_flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int lim = min(min((int)avail, (int)lds_ld(cons0) + kSlots), nchunks);
             if (lim > in_next) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (int col = in_next * CH + lane; col < lim * CH; col += 64)
-                    ring0[col & IRM] = __hip_atomic_load(g_in + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // all loads of the batch in flight before the first LDS write (<= kSlots*CH values)
+                constexpr int PER = kSlots * CH / 64;
+                int v[PER];
+                const int c0 = in_next * CH, c1 = lim * CH;
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int col = c0 + i * 64 + lane;
+                    v[i] = col < c1 ? __hip_atomic_load(gmem(g_in) + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0;
+                }
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int col = c0 + i * 64 + lane;
+                    if (col < c1) ring0[col & IRM] = v[i];
+                }
                 lds_st(prod0, (uint32_t)lim);
                 in_next = lim;
                 progress = true;
@@ -285,12 +443,14 @@ __device__ void io_wave(int lane, int nchunks, const int32_t* g_in, uint32_t* g_
             const int p = min((int)lds_ld(oprod), nchunks);
             if (p > out_next) {
                 for (int col = out_next * CH + lane; col < p * CH; col += 64)
-                    __hip_atomic_store(g_out + col, oring[col & IRM], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(gmem(g_out) + col, oring[col & IRM], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 lds_st(ocons, (uint32_t)p);
                 if (g_out_flag) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0)
-                        __hip_atomic_store(g_out_flag, (uint32_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(gmem(g_out_flag), (uint32_t)p, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
                 }
                 out_next = p;
                 progress = true;
@@ -298,16 +458,17 @@ __device__ void io_wave(int lane, int nchunks, const int32_t* g_in, uint32_t* g_
         }
         if (!progress) {
             __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t_start > SPIN_TICKS || err_set(err)) {
+            if ((++idle & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t_start > SPIN_TICKS || err_set(err))) {
                 atomicOr(err, ERR_SPIN_TIMEOUT);
                 lds_st(prod0, (uint32_t)nchunks);
+                lds_st(s_filled, (uint32_t)nchunks);
                 return;
             }
         }
     }
 }
 
-template <int KIND, int R, int NW, int CH>
+template <int KIND, int R, int X, int NW, int CH>
 __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __restrict__ probs,
                                                               const GroupRef* __restrict__ groups, int ngroups_total,
                                                               uint32_t* dq, uint32_t* err, FillParams fp) {
@@ -323,7 +484,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
         ck.wx = fp.mismatch - 2 * fp.gap;
     }
     for (;;) {
-        if (threadIdx.x == 0) sh.group = (int32_t)atomicAdd(dq, 1u);
+        if (threadIdx.x == 0) {
+            sh.group = (int32_t)atomicAdd(dq, 1u);
+            sh.s_filled = 0;
+            sh.tail = 0;
+        }
         if (threadIdx.x <= NW) {
             sh.prod[threadIdx.x] = 0;
             sh.cons[threadIdx.x] = 0;
@@ -345,20 +510,23 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
             g_out = P.out_row;
         }
         if (wave == NW) {
-            const int nchunks = (P.w + CH - 1) / CH;
             const int32_t* g_in = g.group > 0 ? P.rowbuf + (size_t)(g.group - 1) * P.wpad : nullptr;
             uint32_t* g_in_flag = g.group > 0 ? P.flags + (g.group - 1) : nullptr;
-            io_wave<CH>(lane, nchunks, g_in, g_in_flag, sh.in_ring[0], &sh.prod[0], &sh.cons[0], g_out, g_out_flag,
-                        sh.in_ring[NW], &sh.prod[NW], &sh.cons[NW], err);
+            io_wave<CH>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.s_filled, &sh.tail, g_in, g_in_flag,
+                        sh.in_ring[0], &sh.prod[0], &sh.cons[0], g_out, g_out_flag, sh.in_ring[NW], &sh.prod[NW],
+                        &sh.cons[NW], err);
         } else {
             const int band = first + wave;
             if (band <= last) {
                 WaveIO io;
                 io.in_border = band == 0;
+                io.trailing = band == last;
                 io.my_ring = sh.in_ring[wave];
                 io.my_prod = &sh.prod[wave];
                 io.my_cons = &sh.cons[wave];
-                io.s_ring = sh.s_ring[wave];
+                io.s_ring = sh.s_ring;
+                io.s_filled = &sh.s_filled;
+                io.tail = &sh.tail;
                 if (band < last) {
                     io.out_lds = true;
                     io.next_ring = sh.in_ring[wave + 1];
@@ -372,9 +540,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
                 }
                 const bool partial = (band + 1) * 64 * R > P.h;
                 if (partial)
-                    run_band<KIND, R, CH, true>(P, band, lane, io, err, ck);
+                    run_band<KIND, R, X, CH, true>(P, band, lane, io, err, ck, fp.dbg);
                 else
-                    run_band<KIND, R, CH, false>(P, band, lane, io, err, ck);
+                    run_band<KIND, R, X, CH, false>(P, band, lane, io, err, ck, fp.dbg);
             }
         }
         __syncthreads();
@@ -391,6 +559,37 @@ __global__ void semiglobal_reduce_kernel(const int32_t* __restrict__ row_g, int 
         best = max(best, row_g[j] - (n - 1 + j + 2) * ng);
     for (int i = threadIdx.x + blockIdx.x * blockDim.x; i < n; i += blockDim.x * gridDim.x)
         best = max(best, col_h[i]);
+    for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, best);
+}
+
+// Two-front score combine (Hirschberg row split at h1): the top front is the
+// forward DP of rows [0,h1), the bottom front the DP of rows [h1,n) with query
+// and subject reversed.  For every split column j in [-1, m-1]:
+//     F[j] + B[m-2-j]    (F = top bottom-row H, B = bottom-front bottom-row H,
+//                         index -1 = the scheme's border)
+// is the best path crossing rows h1-1 -> h1 after consuming s[0..j].  Semiglobal
+// adds paths ending on the right column in the top half (top out_col) and paths
+// starting on the left column in the bottom half (bottom out_col); local adds
+// the best cell of either front (already in *out via atomicMax).
+__global__ void front_combine_kernel(int kind, const int32_t* __restrict__ rowF, int h1, const int32_t* __restrict__ rowB,
+                                     int h2, int m, int gap, const int32_t* __restrict__ colF,
+                                     const int32_t* __restrict__ colB, int32_t* out) {
+    const int ng = -gap;
+    auto init = [&](int i) { return kind == KIND_GLOBAL ? (i + 1) * gap : 0; };
+    auto toh = [&](int v, int r, int c) { return kind == KIND_LOCAL ? v : v - (r + c + 2) * ng; };
+    // semiglobal: row[-1] = col[-1] = 0 borders are part of the reference's max (scoring.impala:51-63)
+    int best = kind == KIND_SEMIGLOBAL ? 0 : -2147483647;
+    for (int j = (int)(threadIdx.x + blockIdx.x * blockDim.x) - 1; j < m; j += blockDim.x * gridDim.x) {
+        const int F = j < 0 ? init(h1 - 1) : toh(rowF[j], h1 - 1, j);
+        const int jb = m - 2 - j;
+        const int B = jb < 0 ? init(h2 - 1) : toh(rowB[jb], h2 - 1, jb);
+        best = max(best, F + B);
+    }
+    if (kind == KIND_SEMIGLOBAL) {
+        for (int i = threadIdx.x + blockIdx.x * blockDim.x; i < h1; i += blockDim.x * gridDim.x) best = max(best, colF[i]);
+        for (int i = threadIdx.x + blockIdx.x * blockDim.x; i < h2; i += blockDim.x * gridDim.x) best = max(best, colB[i]);
+    }
     for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
     if ((threadIdx.x & 63) == 0) atomicMax(out, best);
 }
@@ -550,24 +749,34 @@ __global__ void walk_kernel(const BlockInfo* __restrict__ blocks, int nblocks, c
 }
 
 // --------------------------------------------------------------- launchers --
-template <int KIND, int R, int NW, int CH>
+template <int KIND, int R, int X, int NW, int CH>
 static hipError_t launch_fill_t(const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
                                 uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((fill_kernel<KIND, R, NW, CH>), dim3(grid), dim3(64 * (NW + 1)), 0, st, probs, groups,
+    hipLaunchKernelGGL((fill_kernel<KIND, R, X, NW, CH>), dim3(grid), dim3(64 * (NW + 1)), 0, st, probs, groups,
                        ngroups, dq, err, fp);
     return hipGetLastError();
 }
 
-template <int R, int NW, int CH>
+template <int R, int X, int NW, int CH>
 static hipError_t launch_fill_r(const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
                                 uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
     switch (fp.kind) {
         case KIND_GLOBAL:
-            return launch_fill_t<KIND_GLOBAL, R, NW, CH>(probs, groups, ngroups, dq, err, fp, grid, st);
+            return launch_fill_t<KIND_GLOBAL, R, X, NW, CH>(probs, groups, ngroups, dq, err, fp, grid, st);
         case KIND_SEMIGLOBAL:
-            return launch_fill_t<KIND_SEMIGLOBAL, R, NW, CH>(probs, groups, ngroups, dq, err, fp, grid, st);
+            return launch_fill_t<KIND_SEMIGLOBAL, R, X, NW, CH>(probs, groups, ngroups, dq, err, fp, grid, st);
         default:
-            return launch_fill_t<KIND_LOCAL, R, NW, CH>(probs, groups, ngroups, dq, err, fp, grid, st);
+            return launch_fill_t<KIND_LOCAL, R, X, NW, CH>(probs, groups, ngroups, dq, err, fp, grid, st);
+    }
+}
+
+template <int X, int NW>
+static hipError_t launch_fill_x(int R, const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
+                                uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
+    switch (R) {
+        case 1: return launch_fill_r<1, X, NW, 32>(probs, groups, ngroups, dq, err, fp, grid, st);
+        case 2: return launch_fill_r<2, X, NW, 32>(probs, groups, ngroups, dq, err, fp, grid, st);
+        default: return launch_fill_r<4, X, NW, 32>(probs, groups, ngroups, dq, err, fp, grid, st);
     }
 }
 
@@ -575,28 +784,30 @@ static hipError_t launch_fill_r(const DPProblem* probs, const GroupRef* groups, 
 
 extern "C" {
 
-// Fill launcher: R rows per lane in {1,2,4}; NW compute waves per workgroup in {4,8}; CH = 32.
-hipError_t anyseq_launch_fill(int R, int NW, const anyseq::DPProblem* probs, const anyseq::GroupRef* groups,
+// Fill launcher: R rows per lane in {1,2,4}; lane-skew extra X in {0,1};
+// NW compute waves per workgroup in {4,8}; CH = 32.
+hipError_t anyseq_launch_fill(int R, int X, int NW, const anyseq::DPProblem* probs, const anyseq::GroupRef* groups,
                               int ngroups, uint32_t* dq, uint32_t* err, const anyseq::FillParams* fp, int grid,
                               hipStream_t st) {
     using namespace anyseq;
-    if (NW == 4) {
-        switch (R) {
-            case 1: return launch_fill_r<1, 4, 32>(probs, groups, ngroups, dq, err, *fp, grid, st);
-            case 2: return launch_fill_r<2, 4, 32>(probs, groups, ngroups, dq, err, *fp, grid, st);
-            default: return launch_fill_r<4, 4, 32>(probs, groups, ngroups, dq, err, *fp, grid, st);
-        }
-    }
-    switch (R) {
-        case 1: return launch_fill_r<1, 8, 32>(probs, groups, ngroups, dq, err, *fp, grid, st);
-        case 2: return launch_fill_r<2, 8, 32>(probs, groups, ngroups, dq, err, *fp, grid, st);
-        default: return launch_fill_r<4, 8, 32>(probs, groups, ngroups, dq, err, *fp, grid, st);
-    }
+    if (NW == 4)
+        return X ? launch_fill_x<1, 4>(R, probs, groups, ngroups, dq, err, *fp, grid, st)
+                 : launch_fill_x<0, 4>(R, probs, groups, ngroups, dq, err, *fp, grid, st);
+    return X ? launch_fill_x<1, 8>(R, probs, groups, ngroups, dq, err, *fp, grid, st)
+             : launch_fill_x<0, 8>(R, probs, groups, ngroups, dq, err, *fp, grid, st);
 }
 
 hipError_t anyseq_launch_semiglobal_reduce(const int32_t* row_g, int m, const int32_t* col_h, int n, int ng,
                                            int32_t* out, hipStream_t st) {
     hipLaunchKernelGGL(anyseq::semiglobal_reduce_kernel, dim3(64), dim3(256), 0, st, row_g, m, col_h, n, ng, out);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_front_combine(int kind, const int32_t* rowF, int h1, const int32_t* rowB, int h2, int m,
+                                       int gap, const int32_t* colF, const int32_t* colB, int32_t* out,
+                                       hipStream_t st) {
+    hipLaunchKernelGGL(anyseq::front_combine_kernel, dim3(64), dim3(256), 0, st, kind, rowF, h1, rowB, h2, m, gap,
+                       colF, colB, out);
     return hipGetLastError();
 }
 

@@ -82,6 +82,11 @@ const char* anyseq_last_error(void);
  * persistent grid size (0 = one workgroup per CU).  0 keeps the current value. */
 void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid);
 
+/* Named tuning option: "rows_per_lane", "lane_skew_extra", "waves_per_group",
+ * "grid", "fronts" (1 or 2: score fill as one front or two meeting fronts).
+ * Returns 0, or -1 for an unknown name. */
+int anyseq_set_option(const char* name, int value);
+
 /* Timing of the most recent fill launch(es) of the calling thread, measured with
  * HIP events on the engine stream: total kernel milliseconds and launch count. */
 void anyseq_last_fill_timing(double* ms, int* launches);

@@ -102,4 +102,22 @@ def test_tuning_variants(anyseq, oracle, R, NW):
             q, s = rnd(rng, 1500), rnd(rng, 1300)
             assert abi_construct(anyseq, kind, q, s) == oracle.construct(kind, q, s), (R, NW, kind)
     finally:
-        anyseq.set_tuning(1, 8, 0)
+        anyseq.set_tuning(1, 4, 0)
+
+
+@pytest.mark.parametrize("fronts", [1, 2])
+@pytest.mark.parametrize("X", [0, 1])
+def test_fronts_and_skew(anyseq, oracle, fronts, X):
+    rng = random.Random(40 + fronts * 2 + X)
+    anyseq.set_option("fronts", fronts)
+    anyseq.set_option("lane_skew_extra", X)
+    try:
+        for kind in KINDS:
+            for n, m in [(513, 700), (2000, 1999), (4096, 64), (6001, 3000), (1024, 1)]:
+                q, s = rnd(rng, n), rnd(rng, m)
+                assert abi_score(anyseq, kind, q, s) == oracle.score(kind, q, s), (fronts, X, kind, n, m)
+            q, s = rnd(rng, 2500), rnd(rng, 1800)
+            assert abi_construct(anyseq, kind, q, s) == oracle.construct(kind, q, s), (fronts, X, kind)
+    finally:
+        anyseq.set_option("fronts", 2)
+        anyseq.set_option("lane_skew_extra", 0)
