@@ -21,7 +21,7 @@
 using namespace anyseq;
 
 extern "C" {
-hipError_t anyseq_launch_fill(int R, int X, int NW, const DPProblem* probs, const GroupRef* groups, int ngroups,
+hipError_t anyseq_launch_fill(int R, int CH, int NW, const DPProblem* probs, const GroupRef* groups, int ngroups,
                               uint32_t* dq, uint32_t* err, const FillParams* fp, int grid, hipStream_t st);
 hipError_t anyseq_launch_semiglobal_reduce(const int32_t* row_g, int m, const int32_t* col_h, int n, int ng,
                                            int32_t* out, hipStream_t st);
@@ -90,7 +90,7 @@ int env_int(const char* name, int dflt) {
 
 struct Tuning {
     int R = 1;
-    int X = 0;
+    int CH = 32;
     int NW = 4;
     int grid = 0;
     int fronts = 2;
@@ -128,7 +128,7 @@ Engine& engine() {
     if (!g_tuning_init) {
         g_tuning.R = env_int("ANYSEQ_R", g_tuning.R);
         g_tuning.NW = env_int("ANYSEQ_NW", g_tuning.NW);
-        g_tuning.X = env_int("ANYSEQ_X", g_tuning.X);
+        g_tuning.CH = env_int("ANYSEQ_CH", g_tuning.CH);
         g_tuning.grid = env_int("ANYSEQ_GRID", g_tuning.grid);
         g_tuning_init = true;
     }
@@ -143,7 +143,10 @@ Engine& engine() {
 }
 
 int rows_per_lane() { return g_tuning.R == 2 ? 2 : (g_tuning.R >= 4 ? 4 : 1); }
-int waves_per_group() { return g_tuning.NW == 4 ? 4 : 8; }
+int waves_per_group() {
+    const int nw = g_tuning.NW;
+    return (nw == 3 || nw == 4 || nw == 7) ? nw : 8;
+}
 
 // ---------------------------------------------------------------- fill --
 // Runs one batched fill launch over `probs` (host copies; device pointers set).
@@ -185,14 +188,15 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     grid = std::min<int>(grid, (int)groups.size());
     FillParams fpl = fp;
     unsigned long long* dbg = nullptr;
+    static DevBuf stamp_buf;
     if (getenv("ANYSEQ_STAMPS")) {
-        dbg = (unsigned long long*)E.ctr.get(64) + 4;   // ctr[8..] (bytes 32..95)
-        HIPCHECK(hipMemsetAsync(dbg, 0, 8 * 8, st));
+        dbg = (unsigned long long*)stamp_buf.get(8 * (16 + 4 * 4096));
+        HIPCHECK(hipMemsetAsync(dbg, 0, 8 * (16 + 4 * 4096), st));
         fpl.dbg = dbg;
     }
     HIPCHECK(hipEventRecord(E.ev0, st));
-    HIPCHECK(anyseq_launch_fill(R, g_tuning.X ? 1 : 0, NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fpl,
-                                grid, st));
+    HIPCHECK(anyseq_launch_fill(R, g_tuning.CH, NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fpl, grid,
+                                st));
     HIPCHECK(hipEventRecord(E.ev1, st));
     HIPCHECK(hipEventSynchronize(E.ev1));
     float ms = 0.f;
@@ -209,6 +213,20 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
                 "wait_in %.0f, wait_s %.0f, wait_out %.0f | compute/block %.1f cyc\n",
                 ms, R, NW, h[5], h[6], (double)h[0] / h[5], (double)h[1] / h[5], (double)h[2] / h[5],
                 (double)h[3] / h[5], (double)h[4] / h[5], (double)h[1] / std::max(1ull, h[6]));
+        if (const char* tl = getenv("ANYSEQ_TIMELINE")) {
+            std::vector<unsigned long long> t(4 * 4096);
+            HIPCHECK(hipMemcpy(t.data(), dbg + 16, t.size() * 8, hipMemcpyDeviceToHost));
+            FILE* f = fopen(tl, "a");
+            if (f) {
+                fprintf(f, "# launch %.3f ms R=%d NW=%d\n", ms, R, NW);
+                unsigned long long t0 = ~0ull;
+                for (size_t i = 0; i < t.size(); i += 4) if (t[i] && t[i] < t0) t0 = t[i];
+                for (size_t i = 0; i < t.size(); i += 4)
+                    if (t[i]) fprintf(f, "%zu %.2f %.2f %.2f\n", i / 4, (t[i] - t0) / 100.0,
+                                      t[i + 1] ? (t[i + 1] - t0) / 100.0 : -1.0, (t[i + 2] - t0) / 100.0);
+                fclose(f);
+            }
+        }
     }
     if (err) fail("fill kernel reported error %u (spin timeout)", err);
 }
@@ -569,7 +587,7 @@ const char* anyseq_last_error(void) { return g_last_error.c_str(); }
 void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid) {
     std::lock_guard<std::mutex> lk(g_engines_mu);
     if (!g_tuning_init) {
-        g_tuning.X = env_int("ANYSEQ_X", g_tuning.X);
+        g_tuning.CH = env_int("ANYSEQ_CH", g_tuning.CH);
         g_tuning.fronts = env_int("ANYSEQ_FRONTS", g_tuning.fronts);
     }
     g_tuning_init = true;
@@ -584,13 +602,13 @@ int anyseq_set_option(const char* name, int value) {
         g_tuning.R = env_int("ANYSEQ_R", g_tuning.R);
         g_tuning.NW = env_int("ANYSEQ_NW", g_tuning.NW);
         g_tuning.grid = env_int("ANYSEQ_GRID", g_tuning.grid);
-        g_tuning.X = env_int("ANYSEQ_X", g_tuning.X);
+        g_tuning.CH = env_int("ANYSEQ_CH", g_tuning.CH);
         g_tuning.fronts = env_int("ANYSEQ_FRONTS", g_tuning.fronts);
         g_tuning_init = true;
     }
     const std::string n = name ? name : "";
     if (n == "rows_per_lane") g_tuning.R = value;
-    else if (n == "lane_skew_extra") g_tuning.X = value;
+    else if (n == "chunk") g_tuning.CH = value == 16 ? 16 : 32;
     else if (n == "waves_per_group") g_tuning.NW = value;
     else if (n == "grid") g_tuning.grid = value;
     else if (n == "fronts") g_tuning.fronts = value;

@@ -39,23 +39,26 @@ __device__ __forceinline__ bool err_set(uint32_t* err) {
     return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 }
 
-__device__ __forceinline__ bool spin_lds_ge(uint32_t* p, uint32_t target, uint32_t* err) {
-    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
+// Waits until *p >= target; returns the observed value (wave-uniform), or 0 on timeout/error.
+__device__ __forceinline__ uint32_t spin_lds_ge(uint32_t* p, uint32_t target, uint32_t* err) {
+    uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (v >= target) {
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        return true;
+        return v;
     }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t it = 0;
-    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+    while ((v = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) < target) {
         __builtin_amdgcn_s_sleep(1);
         // the error word lives in HBM: look at it (and the clock) only every 256 polls
         if ((++it & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
             atomicOr(err, ERR_SPIN_TIMEOUT);
-            return false;
+            return 0;
         }
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    return true;
+    return v;
 }
 
 __device__ __forceinline__ bool spin_glb_ge(uint32_t* p, uint32_t target, uint32_t* err) {
@@ -86,6 +89,12 @@ template <int KIND>
 __device__ __forceinline__ int to_h(int v, int r, int c, int ng) {
     return KIND == KIND_LOCAL ? v : v - (r + c + 2) * ng;
 }
+
+// Diagnostic experiments (timing builds only, results are wrong): bit 0 skips the
+// in-ring reads, bit 1 the subject reads, bit 2 the bottom-row writes, bit 3 the DP.
+#ifndef ANYSEQ_EXP
+#define ANYSEQ_EXP 0
+#endif
 
 constexpr int kSlots = 16;     // in-ring depth in chunks
 constexpr int kSRing = 4096;   // shared subject ring bytes per workgroup (+64 mirrored)
@@ -217,22 +226,115 @@ struct WaveIO {
     uint32_t* tail;
 };
 
-// CH steps t0 .. t0+CH-1.  top_first = top row at column t0-1 (read by the DPP
-// of step t0); ring_blk[u-1] = column t0+u-1.  s_blk[k][u] = subject byte of row k.
+// CH steps t0 .. t0+CH-1 from registers: top_first = top row at column t0-1,
+// rv[u] = top row at column t0+u (only u < CH-1 is used here; rv[CH-1] becomes
+// the next block's top_first), sw[k][u/4] = subject bytes of row k, 4 per dword.
 template <int KIND, int R, int X, int CH, bool MASK, bool PARTIAL>
-__device__ __forceinline__ void band_block(int t0, int lane, int w, int top_first, const int32_t* ring_blk,
-                                           const uint8_t* const (&s_blk)[R], const int (&qv)[R],
+__device__ __forceinline__ void band_block(int t0, int lane, int w, int top_first, const int (&rv)[CH],
+                                           const uint32_t (&sw)[R][CH / 4], const int (&qv)[R],
                                            const bool (&dead)[R], int (&cur)[R], int (&prev)[R], int& upc, int& dg,
                                            int (&outv)[CH], int& best, const CellK ck) {
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
-        const int topv = u == 0 ? top_first : ring_blk[u - 1];
+        const int topv = u == 0 ? top_first : rv[u - 1];
         int sc[R];
 #pragma unroll
-        for (int k = 0; k < R; ++k) sc[k] = s_blk[k][u];
+        for (int k = 0; k < R; ++k) sc[k] = (int)((sw[k][u >> 2] >> (8 * (u & 3))) & 0xffu);
         band_step<KIND, R, X, MASK, PARTIAL>(t0 + u, lane, w, topv, sc, qv, dead, cur, prev, upc, dg, outv[u], best,
                                              ck);
     }
+}
+
+// ---- hand-scheduled steady-state block (R = 1, X = 0, CH = 32, all rows live) ----
+// One step is five VALU instructions, issued in the order
+//     C  v_cmp_eq_u32_sdwa vcc, q, s.byte      substitution test
+//     D  v_cndmask_b32     w, wx, wm, vcc     weight
+//     E  v_add_u32         a, dg, w           diag + weight (dg = previous step's up)
+//     A  v_mov_b32_dpp     up, cur wave_shr:1 lane l-1's cell; lane 0 keeps `up` = top row
+//     B  v_max3_i32        cur', a, cur, up
+// so the DPP always reads a `cur` written three instructions earlier (the
+// VALU->DPP hazard needs two) and the lane-to-lane chain B -> A -> B never stalls.
+// The DPP writes in place into the register holding the top-row value (its
+// `old` operand), which saves the copy the compiler emits for the builtin.
+// Local alignment adds a saturating `- ng` (H-space clamp at 0) and the running max.
+#define AQ_STEP_G(S, B, CUR, DG, TV, OV)                                      \
+    "v_cmp_eq_u32_sdwa vcc, %[q], " S " src0_sel:DWORD src1_sel:BYTE_" #B "\n" \
+    "v_cndmask_b32_e32 %[w], %[wx], %[wm], vcc\n"                              \
+    "v_add_u32_e32 %[a], " DG ", %[w]\n"                                       \
+    "v_mov_b32_dpp " TV ", " CUR " wave_shr:1 row_mask:0xf bank_mask:0xf\n"    \
+    "v_max3_i32 " OV ", %[a], " CUR ", " TV "\n"
+#define AQ_STEP_L(S, B, CUR, DG, TV, OV)                                      \
+    AQ_STEP_G(S, B, CUR, DG, TV, OV)                                           \
+    "v_sub_u32_e64 " OV ", " OV ", %[ng] clamp\n"                              \
+    "v_max_i32_e32 %[best], %[best], " OV "\n"
+#define AQ_8STEPS(STEP)                                            \
+    STEP("%[s0]", 0, "%[cur]", "%[dg]", "%[t0]", "%[o0]")          \
+    STEP("%[s0]", 1, "%[o0]", "%[t0]", "%[t1]", "%[o1]")           \
+    STEP("%[s0]", 2, "%[o1]", "%[t1]", "%[t2]", "%[o2]")           \
+    STEP("%[s0]", 3, "%[o2]", "%[t2]", "%[t3]", "%[o3]")           \
+    STEP("%[s1]", 0, "%[o3]", "%[t3]", "%[t4]", "%[o4]")           \
+    STEP("%[s1]", 1, "%[o4]", "%[t4]", "%[t5]", "%[o5]")           \
+    STEP("%[s1]", 2, "%[o5]", "%[t5]", "%[t6]", "%[o6]")           \
+    STEP("%[s1]", 3, "%[o6]", "%[t6]", "%[t7]", "%[o7]")
+#define AQ_OUTS(tv, ov)                                                                                       \
+    [o0] "=&v"(ov[0]), [o1] "=&v"(ov[1]), [o2] "=&v"(ov[2]), [o3] "=&v"(ov[3]), [o4] "=&v"(ov[4]),          \
+        [o5] "=&v"(ov[5]), [o6] "=&v"(ov[6]), [o7] "=&v"(ov[7]), [t0] "+v"(tv[0]), [t1] "+v"(tv[1]),          \
+        [t2] "+v"(tv[2]), [t3] "+v"(tv[3]), [t4] "+v"(tv[4]), [t5] "+v"(tv[5]), [t6] "+v"(tv[6]),             \
+        [t7] "+v"(tv[7]), [w] "=&v"(w), [a] "=&v"(a)
+
+// Eight steps: tv[i] holds the top-row value lane 0 uses at step i (destroyed:
+// it becomes the step's up value); ov[i] receives the cell value after step i.
+template <int KIND>
+__device__ __forceinline__ void steps8_asm(int& cur, int& dg, int (&tv)[8], uint32_t s0, uint32_t s1, int q,
+                                           const CellK& ck, int (&ov)[8], int& best) {
+    int w, a;
+    if (KIND == KIND_LOCAL) {
+        asm volatile(AQ_8STEPS(AQ_STEP_L)
+                     : AQ_OUTS(tv, ov), [best] "+v"(best)
+                     : [cur] "v"(cur), [dg] "v"(dg), [s0] "v"(s0), [s1] "v"(s1), [q] "v"(q), [wm] "v"(ck.wm),
+                       [wx] "v"(ck.wx), [ng] "v"(ck.ng)
+                     : "vcc");
+    } else {
+        asm volatile(AQ_8STEPS(AQ_STEP_G)
+                     : AQ_OUTS(tv, ov)
+                     : [cur] "v"(cur), [dg] "v"(dg), [s0] "v"(s0), [s1] "v"(s1), [q] "v"(q), [wm] "v"(ck.wm),
+                       [wx] "v"(ck.wx)
+                     : "vcc");
+    }
+    cur = ov[7];
+    dg = tv[7];
+}
+
+// A full 32-step block (t0 >= D, t0 + 32 <= w + BASE, no dead rows): four
+// 8-step chunks.  rv[0..30] are consumed (destroyed), rv[31] is kept for the
+// next block's top_first.
+template <int KIND>
+__device__ __forceinline__ void band_block_asm(int top_first, int (&rv)[32], const uint32_t (&sw)[8], int q,
+                                               int& cur, int& dg, int (&outv)[32], int& best, const CellK& ck) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        int tv[8], ov[8];
+        tv[0] = c == 0 ? top_first : rv[8 * c - 1];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) tv[i] = rv[8 * c + i - 1];
+        steps8_asm<KIND>(cur, dg, tv, sw[2 * c], sw[2 * c + 1], q, ck, ov, best);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) outv[8 * c + i] = ov[i];
+    }
+}
+
+// 32 subject bytes starting at ring position p (any alignment) -> 8 dwords:
+// 9 aligned ds_read_b32 + 8 v_alignbit (unaligned b64/b128 LDS reads replay).
+template <int CH>
+__device__ __forceinline__ void load_sbytes(const uint8_t* s_ring, int p, uint32_t (&out)[CH / 4]) {
+    const int pa = p & ~3;
+    const uint32_t sh = (uint32_t)(p & 3) * 8u;
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(s_ring + pa);
+    uint32_t d[CH / 4 + 1];
+#pragma unroll
+    for (int i = 0; i <= CH / 4; ++i) d[i] = base[i];
+#pragma unroll
+    for (int i = 0; i < CH / 4; ++i) out[i] = __builtin_amdgcn_alignbit(d[i + 1], d[i], sh);
 }
 
 template <int KIND, int R, int X, int CH, bool PARTIAL>
@@ -275,45 +377,80 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
     const int nblocks = nchunks + LAG;
     // last observed values of the LDS counters: most blocks need no LDS round trip
     uint32_t seen_prod = 0, seen_sfill = 0, seen_cons = 0;
+    int rv[CH];
+    uint32_t sw[R][CH / 4];
 
-    for (int b = 0; b < nblocks; ++b) {
-        const int t0 = b * CH;
-        // ---- input chunk b (columns [t0, t0+CH)) and its subject bytes
-        if (b < nchunks) {
+    // Acquire block bb's inputs into registers: the top-row chunk bb (in-ring) and
+    // the subject bytes of every row.  Returns false on timeout.
+    auto acquire = [&](int bb) -> bool {
+        const int tb = bb * CH;
+        if (bb < nchunks) {
             STAMP(ta);
             if (io.in_border) {
-                if (lane < CH) io.my_ring[(t0 + lane) & IRM] = border_top<KIND>(t0 + lane, ng);
-            } else if (seen_prod < (uint32_t)(b + 1)) {
-                if (!spin_lds_ge(io.my_prod, (uint32_t)(b + 1), err)) return;
-                seen_prod = __builtin_amdgcn_readfirstlane(lds_ld(io.my_prod));
+                if (lane < CH) io.my_ring[(tb + lane) & IRM] = border_top<KIND>(tb + lane, ng);
+            } else if (seen_prod < (uint32_t)(bb + 1)) {
+                if (!(seen_prod = spin_lds_ge(io.my_prod, (uint32_t)(bb + 1), err))) return false;
             }
-            STAMP(tb);
-            if (seen_sfill < (uint32_t)(b + 1)) {
-                if (!spin_lds_ge(io.s_filled, (uint32_t)(b + 1), err)) return;
-                seen_sfill = __builtin_amdgcn_readfirstlane(lds_ld(io.s_filled));
+            STAMP(tb2);
+            if (seen_sfill < (uint32_t)(bb + 1)) {
+                if (!(seen_sfill = spin_lds_ge(io.s_filled, (uint32_t)(bb + 1), err))) return false;
             }
             STAMP(tc);
-            STAMP_ADD(ST_WAIT_IN, tb - ta);
-            STAMP_ADD(ST_WAIT_S, tc - tb);
-        }
-        STAMP(t_comp0);
-        const int top_first = b == 0 ? border_left<KIND>(rb - 1, ng) : io.my_ring[(t0 - 1) & IRM];
-        const int32_t* ring_blk = io.my_ring + (t0 & IRM);
-        const uint8_t* s_blk[R];
+            STAMP_ADD(ST_WAIT_IN, tb2 - ta);
+            STAMP_ADD(ST_WAIT_S, tc - tb2);
+            const int4* src = reinterpret_cast<const int4*>(io.my_ring + (tb & IRM));
+            if (ANYSEQ_EXP & 1) {
 #pragma unroll
-        for (int k = 0; k < R; ++k) s_blk[k] = io.s_ring + ((t0 - BASE - S * lane - k) & (kSRing - 1));
+                for (int q = 0; q < CH; ++q) rv[q] = tb + q;
+            } else
+#pragma unroll
+            for (int q = 0; q < CH / 4; ++q) {
+                const int4 v = src[q];
+                rv[4 * q] = v.x;
+                rv[4 * q + 1] = v.y;
+                rv[4 * q + 2] = v.z;
+                rv[4 * q + 3] = v.w;
+            }
+            // chunk bb is in registers now: the producer may reuse its slot
+            if (!io.in_border) lds_st(io.my_cons, (uint32_t)(bb + 1));
+        }
+        if (ANYSEQ_EXP & 2) {
+#pragma unroll
+            for (int k = 0; k < R; ++k)
+#pragma unroll
+                for (int q = 0; q < CH / 4; ++q) sw[k][q] = (uint32_t)(tb * 0x01010101 + lane + k + q);
+            return true;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+            load_sbytes<CH>(io.s_ring, (tb - BASE - S * lane - k) & (kSRing - 1), sw[k]);
+        return true;
+    };
+
+    if (!acquire(0)) return;
+    int top_first = border_left<KIND>(rb - 1, ng);
+    for (int b = 0; b < nblocks; ++b) {
+        const int t0 = b * CH;
+        STAMP(t_comp0);
+#ifdef ANYSEQ_STAMPS
+        if (b == 0 && dbg && lane == 0 && band < 2048) dbg[16 + 4 * (band + (P.q_step < 0 ? 2048 : 0))] = __builtin_amdgcn_s_memrealtime();
+#endif
         const bool full = (t0 >= D) && (t0 + CH <= w + BASE);
-        if (full)
-            band_block<KIND, R, X, CH, false, PARTIAL>(t0, lane, w, top_first, ring_blk, s_blk, qv, dead, cur, prev,
-                                                       upc, dg, outv, best, ck);
-        else
-            band_block<KIND, R, X, CH, true, PARTIAL>(t0, lane, w, top_first, ring_blk, s_blk, qv, dead, cur, prev,
-                                                      upc, dg, outv, best, ck);
+        if (ANYSEQ_EXP & 8) {
+#pragma unroll
+            for (int u = 0; u < CH; ++u) outv[u] = rv[u] + (int)sw[0][u / 4];
+        } else if (full) {
+            if constexpr (R == 1 && X == 0 && CH == 32 && !PARTIAL && !(ANYSEQ_EXP & 16))
+                band_block_asm<KIND>(top_first, rv, sw[0], qv[0], cur[0], dg, outv, best, ck);
+            else
+                band_block<KIND, R, X, CH, false, PARTIAL>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev, upc,
+                                                           dg, outv, best, ck);
+        } else
+            band_block<KIND, R, X, CH, true, PARTIAL>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev, upc, dg,
+                                                      outv, best, ck);
         STAMP(t_comp1);
         STAMP_ADD(ST_COMPUTE, t_comp1 - t_comp0);
-
-        // ---- release chunks < b (column t0+CH-1 of chunk b is still read by block b+1)
-        if (!io.in_border) lds_st(io.my_cons, (uint32_t)b);
+        top_first = rv[CH - 1];
         if (io.trailing) lds_st(io.tail, (uint32_t)(b + 1));
 
         // ---- publish bottom-row chunk j = b - LAG (lane 63 holds it in outv)
@@ -322,19 +459,23 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
             const uint32_t need = (uint32_t)max(0, j - kSlots + 1);
             STAMP(to0);
             if (seen_cons < need) {
-                if (!spin_lds_ge(io.next_cons, need, err)) return;
-                seen_cons = __builtin_amdgcn_readfirstlane(lds_ld(io.next_cons));
+                if (!(seen_cons = spin_lds_ge(io.next_cons, need, err))) return;
             }
             STAMP(to1);
             STAMP_ADD(ST_WAIT_OUT, to1 - to0);
-            if (lane == 63) {
+            if (lane == 63 && !(ANYSEQ_EXP & 4)) {
                 int4* dst = reinterpret_cast<int4*>(io.next_ring + ((j * CH) & IRM));
 #pragma unroll
                 for (int q = 0; q < CH / 4; ++q)
                     dst[q] = make_int4(outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]);
             }
             lds_st(io.next_prod, (uint32_t)(j + 1));
+#ifdef ANYSEQ_STAMPS
+            if (j == 0 && dbg && lane == 0 && band < 2048) dbg[16 + 4 * (band + (P.q_step < 0 ? 2048 : 0)) + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
         }
+        // ---- inputs of the next block into registers
+        if (b + 1 < nblocks && !acquire(b + 1)) return;
     }
     if (!io.in_border) lds_st(io.my_cons, (uint32_t)(nchunks + kSlots));
     if (io.trailing) lds_st(io.tail, 0x7fffffffu);
@@ -353,6 +494,7 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         if (lane == 0) atomicMax(P.best, best);
     }
 #ifdef ANYSEQ_STAMPS
+    if (dbg && lane == 0 && band < 2048) dbg[16 + 4 * (band + (P.q_step < 0 ? 2048 : 0)) + 2] = __builtin_amdgcn_s_memrealtime();
     STAMP(t_end);
     acc[ST_TOTAL] = t_end - t_begin;
     acc[ST_BANDS] = 1;
@@ -473,7 +615,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
                                                               const GroupRef* __restrict__ groups, int ngroups_total,
                                                               uint32_t* dq, uint32_t* err, FillParams fp) {
     __shared__ __attribute__((aligned(16))) FillShared<NW, CH> sh;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave index via readfirstlane: everything derived from it is provably wave-uniform (SGPRs,
+    // scalar branches instead of exec-mask flow)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     CellK ck;
     ck.ng = -fp.gap;
     if (KIND == KIND_LOCAL) {
@@ -494,7 +638,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
             sh.cons[threadIdx.x] = 0;
         }
         __syncthreads();
-        const int gi = sh.group;
+        const int gi = __builtin_amdgcn_readfirstlane(sh.group);
         if (gi >= ngroups_total || err_set(err)) break;
         const GroupRef g = groups[gi];
         const DPProblem P = probs[g.prob];
@@ -749,6 +893,7 @@ __global__ void walk_kernel(const BlockInfo* __restrict__ blocks, int nblocks, c
 }
 
 // --------------------------------------------------------------- launchers --
+#ifndef ANYSEQ_MICRO   // tools/micro includes the kernels without the launchers
 template <int KIND, int R, int X, int NW, int CH>
 static hipError_t launch_fill_t(const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
                                 uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
@@ -770,31 +915,41 @@ static hipError_t launch_fill_r(const DPProblem* probs, const GroupRef* groups, 
     }
 }
 
-template <int X, int NW>
-static hipError_t launch_fill_x(int R, const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
+template <int NW, int CH>
+static hipError_t launch_fill_n(int R, const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
                                 uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
     switch (R) {
-        case 1: return launch_fill_r<1, X, NW, 32>(probs, groups, ngroups, dq, err, fp, grid, st);
-        case 2: return launch_fill_r<2, X, NW, 32>(probs, groups, ngroups, dq, err, fp, grid, st);
-        default: return launch_fill_r<4, X, NW, 32>(probs, groups, ngroups, dq, err, fp, grid, st);
+        case 1: return launch_fill_r<1, 0, NW, CH>(probs, groups, ngroups, dq, err, fp, grid, st);
+        case 2: return launch_fill_r<2, 0, NW, CH>(probs, groups, ngroups, dq, err, fp, grid, st);
+        default: return launch_fill_r<4, 0, NW, CH>(probs, groups, ngroups, dq, err, fp, grid, st);
     }
 }
 
+template <int CH>
+static hipError_t launch_fill_c(int R, int NW, const DPProblem* probs, const GroupRef* groups, int ngroups,
+                                uint32_t* dq, uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
+    switch (NW) {
+        case 3: return launch_fill_n<3, CH>(R, probs, groups, ngroups, dq, err, fp, grid, st);
+        case 4: return launch_fill_n<4, CH>(R, probs, groups, ngroups, dq, err, fp, grid, st);
+        case 7: return launch_fill_n<7, CH>(R, probs, groups, ngroups, dq, err, fp, grid, st);
+        default: return launch_fill_n<8, CH>(R, probs, groups, ngroups, dq, err, fp, grid, st);
+    }
+}
+
+#endif  // ANYSEQ_MICRO
 }  // namespace anyseq
 
+#ifndef ANYSEQ_MICRO
 extern "C" {
 
-// Fill launcher: R rows per lane in {1,2,4}; lane-skew extra X in {0,1};
-// NW compute waves per workgroup in {4,8}; CH = 32.
-hipError_t anyseq_launch_fill(int R, int X, int NW, const anyseq::DPProblem* probs, const anyseq::GroupRef* groups,
+// Fill launcher: R rows per lane in {1,2,4}; NW compute waves per workgroup in
+// {3,4,7,8} (+1 I/O wave); CH (steps per block = hand-off chunk) in {16,32}.
+hipError_t anyseq_launch_fill(int R, int CH, int NW, const anyseq::DPProblem* probs, const anyseq::GroupRef* groups,
                               int ngroups, uint32_t* dq, uint32_t* err, const anyseq::FillParams* fp, int grid,
                               hipStream_t st) {
     using namespace anyseq;
-    if (NW == 4)
-        return X ? launch_fill_x<1, 4>(R, probs, groups, ngroups, dq, err, *fp, grid, st)
-                 : launch_fill_x<0, 4>(R, probs, groups, ngroups, dq, err, *fp, grid, st);
-    return X ? launch_fill_x<1, 8>(R, probs, groups, ngroups, dq, err, *fp, grid, st)
-             : launch_fill_x<0, 8>(R, probs, groups, ngroups, dq, err, *fp, grid, st);
+    if (CH == 16) return launch_fill_c<16>(R, NW, probs, groups, ngroups, dq, err, *fp, grid, st);
+    return launch_fill_c<32>(R, NW, probs, groups, ngroups, dq, err, *fp, grid, st);
 }
 
 hipError_t anyseq_launch_semiglobal_reduce(const int32_t* row_g, int m, const int32_t* col_h, int n, int ng,
@@ -841,3 +996,4 @@ hipError_t anyseq_launch_walk(const void* blocks, int nblocks, const uint8_t* Q,
 }
 
 }  // extern "C"
+#endif  // ANYSEQ_MICRO

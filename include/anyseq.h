@@ -78,12 +78,13 @@ int anyseq_set_device(int device);
 int anyseq_get_device(void);
 const char* anyseq_last_error(void);
 
-/* Fill-kernel tuning: rows per lane (1,2,4), compute waves per workgroup (4,8),
+/* Fill-kernel tuning: rows per lane (1,2,4), compute waves per workgroup (3,4,7,8),
  * persistent grid size (0 = one workgroup per CU).  0 keeps the current value. */
 void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid);
 
-/* Named tuning option: "rows_per_lane", "lane_skew_extra", "waves_per_group",
- * "grid", "fronts" (1 or 2: score fill as one front or two meeting fronts).
+/* Named tuning option: "rows_per_lane" (1,2,4), "chunk" (16,32 steps per block),
+ * "waves_per_group" (3,4,7,8), "grid", "fronts" (1 or 2: score fill as one
+ * front or two meeting fronts).
  * Returns 0, or -1 for an unknown name. */
 int anyseq_set_option(const char* name, int value);
 

@@ -90,7 +90,7 @@ def test_construct_random_shapes(anyseq, oracle, kind):
         assert got == exp, (kind, n, m)
 
 
-@pytest.mark.parametrize("R,NW", [(1, 4), (1, 8), (2, 8), (4, 8), (2, 4), (4, 4)])
+@pytest.mark.parametrize("R,NW", [(1, 3), (1, 4), (1, 7), (1, 8), (2, 8), (4, 8), (2, 4), (4, 3)])
 def test_tuning_variants(anyseq, oracle, R, NW):
     rng = random.Random(30 + R * 10 + NW)
     anyseq.set_tuning(R, NW, 0)
@@ -106,11 +106,11 @@ def test_tuning_variants(anyseq, oracle, R, NW):
 
 
 @pytest.mark.parametrize("fronts", [1, 2])
-@pytest.mark.parametrize("X", [0, 1])
-def test_fronts_and_skew(anyseq, oracle, fronts, X):
-    rng = random.Random(40 + fronts * 2 + X)
+@pytest.mark.parametrize("CH", [16, 32])
+def test_fronts_and_chunk(anyseq, oracle, fronts, CH):
+    rng = random.Random(40 + fronts * 2 + CH)
     anyseq.set_option("fronts", fronts)
-    anyseq.set_option("lane_skew_extra", X)
+    anyseq.set_option("chunk", CH)
     try:
         for kind in KINDS:
             for n, m in [(513, 700), (2000, 1999), (4096, 64), (6001, 3000), (1024, 1)]:
@@ -120,4 +120,4 @@ def test_fronts_and_skew(anyseq, oracle, fronts, X):
             assert abi_construct(anyseq, kind, q, s) == oracle.construct(kind, q, s), (fronts, X, kind)
     finally:
         anyseq.set_option("fronts", 2)
-        anyseq.set_option("lane_skew_extra", 0)
+        anyseq.set_option("chunk", 32)
