@@ -7,7 +7,7 @@ LIB := anyseq_amd/libanyseq.so
 
 all: $(LIB) oracle
 
-$(SRC)/anyseq_kernels.o: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_internal.h
+$(SRC)/anyseq_kernels.o: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_internal.h $(SRC)/anyseq_block_asm.inc
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -c $< -o $@
 
 $(SRC)/anyseq_engine.o: $(SRC)/anyseq_engine.cpp $(SRC)/anyseq_internal.h include/anyseq.h
@@ -21,7 +21,7 @@ oracle:
 
 # diagnostic build with s_memtime stamps (tools only; never loaded by the product path)
 stamps: anyseq_amd/libanyseq_stamps.so
-anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_internal.h
+anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_internal.h $(SRC)/anyseq_block_asm.inc
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_stamps.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o
 

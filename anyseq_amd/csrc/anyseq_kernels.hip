@@ -90,14 +90,15 @@ __device__ __forceinline__ int to_h(int v, int r, int c, int ng) {
     return KIND == KIND_LOCAL ? v : v - (r + c + 2) * ng;
 }
 
-// Diagnostic experiments (timing builds only, results are wrong): bit 0 skips the
-// in-ring reads, bit 1 the subject reads, bit 2 the bottom-row writes, bit 3 the DP.
+// Diagnostic experiments (timing builds only, results are wrong): bit 1 skips the
+// subject reads, bit 2 the bottom-row writes, bit 4 the hand-scheduled block.
 #ifndef ANYSEQ_EXP
 #define ANYSEQ_EXP 0
 #endif
 
 constexpr int kSlots = 16;     // in-ring depth in chunks
 constexpr int kSRing = 4096;   // shared subject ring bytes per workgroup (+64 mirrored)
+constexpr int kSkewBlocks = 32;   // pre-skewed subject blocks held per workgroup (R = 1, X = 0, CH = 32)
 constexpr int kMaxBack = 5 * 64 + 32;   // deepest look-back of a reader: D = 64(R+1) for R <= 4, + 1 chunk
 
 // LDS of one workgroup: NW compute waves + 1 I/O wave.  in_ring[w] feeds compute
@@ -111,6 +112,11 @@ struct FillShared {
     uint8_t s_ring[kSRing + 64];
     uint32_t prod[NW + 1];
     uint32_t cons[NW + 1];
+    int32_t dummy[NW][64];   // per-wave sink of the block asm's non-publishing lanes
+    // Pre-skewed subject (R = 1, X = 0, CH = 32 only): skew[b % kSkewBlocks][i][l] =
+    // the 4 subject bytes lane l needs at steps 32b + 4i .. 32b + 4i + 3, i.e.
+    // s[32b + 4i - 1 - l ..] -- one conflict-free ds_read_b32 per dword, no realignment.
+    uint32_t skew[kSkewBlocks][8][64];
     uint32_t s_filled;   // subject chunks staged
     uint32_t tail;       // blocks completed by the trailing compute wave
     int32_t group;
@@ -140,6 +146,7 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
 // Global-memory views (address space 1): global_load/global_store count only
 // vmcnt, never lgkmcnt.
 #define GLOBAL_AS __attribute__((address_space(1)))
+#define LDS_AS __attribute__((address_space(3)))
 template <typename T>
 __device__ __forceinline__ GLOBAL_AS T* gmem(T* p) {
     return (GLOBAL_AS T*)p;
@@ -154,7 +161,7 @@ __device__ __forceinline__ GLOBAL_AS T* gmem(T* p) {
 #define STAMP(var)
 #define STAMP_ADD(slot, v)
 #endif
-enum { ST_TOTAL = 0, ST_COMPUTE, ST_WAIT_IN, ST_WAIT_S, ST_WAIT_OUT, ST_BANDS, ST_BLOCKS, ST_IO_TOTAL, ST_NSLOTS };
+enum { ST_TOTAL = 0, ST_COMPUTE, ST_WAIT_IN, ST_WAIT_S, ST_WAIT_OUT, ST_BANDS, ST_BLOCKS, ST_IO_TOTAL, ST_ACQ, ST_PUB, ST_NSLOTS };
 
 // Band geometry.  Lane l owns rows r_k = rb + R*l + k (k < R) and at step t
 // row k processes column
@@ -176,7 +183,7 @@ struct BandGeom {
 
 // One step.  MASK: some rows are outside [0, w) in this step.  PARTIAL: rows
 // >= h pass the value from above through (so lane 63 carries row h-1).
-template <int KIND, int R, int X, bool MASK, bool PARTIAL>
+template <int KIND, int R, int X, bool MASK, bool PARTIAL, bool VIRT = false>
 __device__ __forceinline__ void band_step(int t, int lane, int w, int topv, const int (&sc)[R], const int (&qv)[R],
                                           const bool (&dead)[R], int (&cur)[R], int (&prev)[R], int& upc, int& dg,
                                           int& outv, int& best, const CellK ck) {
@@ -200,7 +207,9 @@ __device__ __forceinline__ void band_step(int t, int lane, int w, int topv, cons
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         prev[k] = cur[k];
-        const bool act = MASK ? ((unsigned)(t - BASE - S * lane - k) < (unsigned)w) : true;
+        // VIRT: columns < 0 are virtual (see run_band) and computed like real ones
+        const bool act = MASK ? (VIRT ? (t - BASE - S * lane - k < w) : ((unsigned)(t - BASE - S * lane - k) < (unsigned)w))
+                              : true;
         if (act) {
             cur[k] = nv[k];
             if (KIND == KIND_LOCAL) best = max(best, nv[k]);
@@ -224,12 +233,14 @@ struct WaveIO {
     const uint8_t* s_ring;
     uint32_t* s_filled;
     uint32_t* tail;
+    int32_t* dummy;            // 64 ints of this wave's scratch
+    const uint32_t* skew;      // pre-skewed subject blocks (FillShared::skew)
 };
 
 // CH steps t0 .. t0+CH-1 from registers: top_first = top row at column t0-1,
 // rv[u] = top row at column t0+u (only u < CH-1 is used here; rv[CH-1] becomes
 // the next block's top_first), sw[k][u/4] = subject bytes of row k, 4 per dword.
-template <int KIND, int R, int X, int CH, bool MASK, bool PARTIAL>
+template <int KIND, int R, int X, int CH, bool MASK, bool PARTIAL, bool VIRT = false>
 __device__ __forceinline__ void band_block(int t0, int lane, int w, int top_first, const int (&rv)[CH],
                                            const uint32_t (&sw)[R][CH / 4], const int (&qv)[R],
                                            const bool (&dead)[R], int (&cur)[R], int (&prev)[R], int& upc, int& dg,
@@ -240,87 +251,98 @@ __device__ __forceinline__ void band_block(int t0, int lane, int w, int top_firs
         int sc[R];
 #pragma unroll
         for (int k = 0; k < R; ++k) sc[k] = (int)((sw[k][u >> 2] >> (8 * (u & 3))) & 0xffu);
-        band_step<KIND, R, X, MASK, PARTIAL>(t0 + u, lane, w, topv, sc, qv, dead, cur, prev, upc, dg, outv[u], best,
-                                             ck);
+        band_step<KIND, R, X, MASK, PARTIAL, VIRT>(t0 + u, lane, w, topv, sc, qv, dead, cur, prev, upc, dg, outv[u],
+                                                   best, ck);
     }
 }
 
-// ---- hand-scheduled steady-state block (R = 1, X = 0, CH = 32, all rows live) ----
-// One step is five VALU instructions, issued in the order
-//     C  v_cmp_eq_u32_sdwa vcc, q, s.byte      substitution test
-//     D  v_cndmask_b32     w, wx, wm, vcc     weight
-//     E  v_add_u32         a, dg, w           diag + weight (dg = previous step's up)
-//     A  v_mov_b32_dpp     up, cur wave_shr:1 lane l-1's cell; lane 0 keeps `up` = top row
-//     B  v_max3_i32        cur', a, cur, up
-// so the DPP always reads a `cur` written three instructions earlier (the
-// VALU->DPP hazard needs two) and the lane-to-lane chain B -> A -> B never stalls.
-// The DPP writes in place into the register holding the top-row value (its
-// `old` operand), which saves the copy the compiler emits for the builtin.
-// Local alignment adds a saturating `- ng` (H-space clamp at 0) and the running max.
-#define AQ_STEP_G(S, B, CUR, DG, TV, OV)                                      \
-    "v_cmp_eq_u32_sdwa vcc, %[q], " S " src0_sel:DWORD src1_sel:BYTE_" #B "\n" \
-    "v_cndmask_b32_e32 %[w], %[wx], %[wm], vcc\n"                              \
-    "v_add_u32_e32 %[a], " DG ", %[w]\n"                                       \
-    "v_mov_b32_dpp " TV ", " CUR " wave_shr:1 row_mask:0xf bank_mask:0xf\n"    \
-    "v_max3_i32 " OV ", %[a], " CUR ", " TV "\n"
-#define AQ_STEP_L(S, B, CUR, DG, TV, OV)                                      \
-    AQ_STEP_G(S, B, CUR, DG, TV, OV)                                           \
-    "v_sub_u32_e64 " OV ", " OV ", %[ng] clamp\n"                              \
-    "v_max_i32_e32 %[best], %[best], " OV "\n"
-#define AQ_8STEPS(STEP)                                            \
-    STEP("%[s0]", 0, "%[cur]", "%[dg]", "%[t0]", "%[o0]")          \
-    STEP("%[s0]", 1, "%[o0]", "%[t0]", "%[t1]", "%[o1]")           \
-    STEP("%[s0]", 2, "%[o1]", "%[t1]", "%[t2]", "%[o2]")           \
-    STEP("%[s0]", 3, "%[o2]", "%[t2]", "%[t3]", "%[o3]")           \
-    STEP("%[s1]", 0, "%[o3]", "%[t3]", "%[t4]", "%[o4]")           \
-    STEP("%[s1]", 1, "%[o4]", "%[t4]", "%[t5]", "%[o5]")           \
-    STEP("%[s1]", 2, "%[o5]", "%[t5]", "%[t6]", "%[o6]")           \
-    STEP("%[s1]", 3, "%[o6]", "%[t6]", "%[t7]", "%[o7]")
-#define AQ_OUTS(tv, ov)                                                                                       \
-    [o0] "=&v"(ov[0]), [o1] "=&v"(ov[1]), [o2] "=&v"(ov[2]), [o3] "=&v"(ov[3]), [o4] "=&v"(ov[4]),          \
-        [o5] "=&v"(ov[5]), [o6] "=&v"(ov[6]), [o7] "=&v"(ov[7]), [t0] "+v"(tv[0]), [t1] "+v"(tv[1]),          \
-        [t2] "+v"(tv[2]), [t3] "+v"(tv[3]), [t4] "+v"(tv[4]), [t5] "+v"(tv[5]), [t6] "+v"(tv[6]),             \
-        [t7] "+v"(tv[7]), [w] "=&v"(w), [a] "=&v"(a)
+#include "anyseq_block_asm.inc"
 
-// Eight steps: tv[i] holds the top-row value lane 0 uses at step i (destroyed:
-// it becomes the step's up value); ov[i] receives the cell value after step i.
+// A full 32-step block (all 64 lanes inside [0, w) or on virtual columns, no dead
+// rows) as ONE asm statement (tools/gen_block_asm.py): ra = LDS byte address of
+// the block's 32 top-row values, tf = top row at column t0 - 1 (on return: the
+// block's last top-row value, the next tf); lane 63 stores the block's 32 bottom
+// cells through a DPP shift register: one ds_write_b32 at the per-lane LDS byte
+// address pa (lanes 32..63: the 32 consecutive slots of the chunk; lanes 0..31 and
+// non-publishing blocks: the wave's dummy area).
 template <int KIND>
-__device__ __forceinline__ void steps8_asm(int& cur, int& dg, int (&tv)[8], uint32_t s0, uint32_t s1, int q,
-                                           const CellK& ck, int (&ov)[8], int& best) {
-    int w, a;
-    if (KIND == KIND_LOCAL) {
-        asm volatile(AQ_8STEPS(AQ_STEP_L)
-                     : AQ_OUTS(tv, ov), [best] "+v"(best)
-                     : [cur] "v"(cur), [dg] "v"(dg), [s0] "v"(s0), [s1] "v"(s1), [q] "v"(q), [wm] "v"(ck.wm),
-                       [wx] "v"(ck.wx), [ng] "v"(ck.ng)
-                     : "vcc");
+__device__ __forceinline__ void band_block_asm(int& tf, uint32_t ra, uint32_t pa, uint64_t pm,
+                                               const uint32_t (&sw)[8], int q, int& cur, int& dg, int& best,
+                                               const CellK& ck) {
+    uint64_t sv;
+    if constexpr (KIND == KIND_LOCAL) {
+        asm volatile(ANYSEQ_BLOCK_ASM_L
+                     : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [best] "+v"(best), [sv] "=&s"(sv)
+                     : [ra] "v"(ra), [pa] "v"(pa), [pm] "s"(pm), [s0] "v"(sw[0]), [s1] "v"(sw[1]), [s2] "v"(sw[2]),
+                       [s3] "v"(sw[3]), [s4] "v"(sw[4]), [s5] "v"(sw[5]), [s6] "v"(sw[6]), [s7] "v"(sw[7]),
+                       [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [ng] "v"(ck.ng)
+                     : ANYSEQ_BLOCK_ASM_CLOBBERS, "memory");
     } else {
-        asm volatile(AQ_8STEPS(AQ_STEP_G)
-                     : AQ_OUTS(tv, ov)
-                     : [cur] "v"(cur), [dg] "v"(dg), [s0] "v"(s0), [s1] "v"(s1), [q] "v"(q), [wm] "v"(ck.wm),
-                       [wx] "v"(ck.wx)
-                     : "vcc");
+        asm volatile(ANYSEQ_BLOCK_ASM_G
+                     : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [sv] "=&s"(sv)
+                     : [ra] "v"(ra), [pa] "v"(pa), [pm] "s"(pm), [s0] "v"(sw[0]), [s1] "v"(sw[1]), [s2] "v"(sw[2]),
+                       [s3] "v"(sw[3]), [s4] "v"(sw[4]), [s5] "v"(sw[5]), [s6] "v"(sw[6]), [s7] "v"(sw[7]),
+                       [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx)
+                     : ANYSEQ_BLOCK_ASM_CLOBBERS, "memory");
     }
-    cur = ov[7];
-    dg = tv[7];
 }
 
-// A full 32-step block (t0 >= D, t0 + 32 <= w + BASE, no dead rows): four
-// 8-step chunks.  rv[0..30] are consumed (destroyed), rv[31] is kept for the
-// next block's top_first.
+// Addresses and flags of one band's steady-state loop (ANYSEQ_LOOP_ASM_*).
+struct LoopArgs {
+    uint32_t rb, nb;                        // LDS byte address of my in-ring / the next ring
+    uint32_t apr, acn, anp, anc, asf, atl;  // LDS byte addresses: my prod/cons, next prod/cons, s_filled, tail
+    uint32_t skb;                           // skew base + 4*lane
+    uint32_t lo;                            // 4*(lane-32) (publishing lanes 32..63)
+    uint32_t lid4;                          // 4*lane
+    uint32_t bvb;                           // border value of column `lane` (band 0)
+    uint32_t bvs;                           // border value step per column (band 0)
+    uint32_t fl;                            // bit0 in_border, bit1 trailing, bit2 publishes
+};
+
+// Blocks b .. be-1 of a band (all full) in one asm statement (tools/gen_block_asm.py,
+// gen_loop).  Returns 0, or 1 on a spin timeout.  b is advanced to be on success.
 template <int KIND>
-__device__ __forceinline__ void band_block_asm(int top_first, int (&rv)[32], const uint32_t (&sw)[8], int q,
-                                               int& cur, int& dg, int (&outv)[32], int& best, const CellK& ck) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        int tv[8], ov[8];
-        tv[0] = c == 0 ? top_first : rv[8 * c - 1];
-#pragma unroll
-        for (int i = 1; i < 8; ++i) tv[i] = rv[8 * c + i - 1];
-        steps8_asm<KIND>(cur, dg, tv, sw[2 * c], sw[2 * c + 1], q, ck, ov, best);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) outv[8 * c + i] = ov[i];
+__device__ __forceinline__ uint32_t band_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
+                                                  const LoopArgs& la, int q, int& cur, int& dg, int& tf, int& best,
+                                                  const CellK& ck) {
+    uint32_t st, x0, x1, x2, x3, x4;
+    const uint64_t hm = 0xffffffff00000000ull;
+    // "s" operands must be provably uniform SGPR values
+#define RFL(x) __builtin_amdgcn_readfirstlane(x)
+    b = RFL(b);
+    sp = RFL(sp);
+    sf = RFL(sf);
+    sc = RFL(sc);
+    be = RFL(be);
+    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), fl = RFL(la.fl);
+#undef RFL
+    if constexpr (KIND == KIND_LOCAL) {
+        asm volatile(ANYSEQ_LOOP_ASM_L
+                     : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [best] "+v"(best), [b] "+s"(b), [sp] "+s"(sp),
+                       [sf] "+s"(sf), [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2),
+                       [x3] "=&s"(x3), [x4] "=&s"(x4)
+                     : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [ng] "v"(ck.ng), [rb] "s"(rb),
+                       [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc),
+                       [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4),
+                       [bvb] "v"(la.bvb), [bvs] "s"(bvs), [fl] "s"(fl), [hm] "s"(hm)
+                     : ANYSEQ_LOOP_ASM_CLOBBERS, "memory");
+    } else {
+        asm volatile(ANYSEQ_LOOP_ASM_G
+                     : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf),
+                       [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3),
+                       [x4] "=&s"(x4)
+                     : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [rb] "s"(rb), [nb] "s"(nb),
+                       [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc), [asf] "v"(la.asf),
+                       [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4), [bvb] "v"(la.bvb),
+                       [bvs] "s"(bvs), [fl] "s"(fl), [hm] "s"(hm)
+                     : ANYSEQ_LOOP_ASM_CLOBBERS, "memory");
     }
+    return st;
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(T* p) {
+    return (uint32_t)(size_t)(LDS_AS T*)p;
 }
 
 // 32 subject bytes starting at ring position p (any alignment) -> 8 dwords:
@@ -354,6 +376,13 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
     const int rb = band * 64 * R;
     const int row0 = rb + lane * R;
 
+    // VIRT: the prologue needs no masking.  Lanes left of column 0 compute virtual
+    // cells: every cell of columns <= -2 starts at kVirtNeg (and stays far below any
+    // real value), so column -1 computes max3(neg, neg, up) = the cell above = 0,
+    // which is the left border of global (G space) and local (H space).  Semiglobal's
+    // left border grows with the row in G space and keeps the masked prologue.
+    constexpr bool VIRT = KIND != KIND_SEMIGLOBAL && R == 1 && X == 0 && !PARTIAL;
+    constexpr int kVirtNeg = -(1 << 29);
     int qv[R];
     bool dead[R];
     int cur[R], prev[R];
@@ -362,13 +391,13 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         const int r = row0 + k;
         dead[k] = r >= h;
         qv[k] = dead[k] ? 0x100 : (int)gmem(P.q)[P.q_off + P.q_step * r];
-        cur[k] = border_left<KIND>(r, ng);
+        cur[k] = VIRT ? kVirtNeg : border_left<KIND>(r, ng);
         prev[k] = cur[k];
     }
     // settle the query loads here: no global load is in flight inside the block loop
 #pragma unroll
     for (int k = 0; k < R; ++k) asm volatile("" : "+v"(qv[k]));
-    int dg = border_left<KIND>(row0 - 1, ng);   // diag of row 0 at its first column
+    int dg = VIRT ? kVirtNeg : border_left<KIND>(row0 - 1, ng);   // diag of row 0 at its first column
     int upc = 0;                                 // up of row 0 for the current step
     int outv[CH];
     int best = 0;
@@ -380,82 +409,119 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
     int rv[CH];
     uint32_t sw[R][CH / 4];
 
-    // Acquire block bb's inputs into registers: the top-row chunk bb (in-ring) and
-    // the subject bytes of every row.  Returns false on timeout.
-    auto acquire = [&](int bb) -> bool {
+    // the hand-scheduled steady-state block reads its top-row values itself
+    constexpr bool ASM = R == 1 && X == 0 && CH == 32 && !PARTIAL && !(ANYSEQ_EXP & 16);
+
+    // Acquire block bb's inputs: wait for the top-row chunk bb (in-ring) and the
+    // subject bytes, load the subject bytes of every row and (unless the asm block
+    // reads them itself) the top-row chunk.  Returns false on timeout.
+    auto acquire = [&](int bb, bool asm_blk) -> bool {
         const int tb = bb * CH;
+        STAMP(ta);
+        if (bb < nchunks && seen_sfill < (uint32_t)(bb + 1)) {
+            if (!(seen_sfill = spin_lds_ge(io.s_filled, (uint32_t)(bb + 1), err))) return false;
+        }
+        STAMP(tb2);
+        STAMP_ADD(ST_WAIT_S, tb2 - ta);
+        // subject words first: their latency overlaps the wait for the top row
+        if constexpr (ASM) {
+            if (asm_blk) {
+                const uint32_t* src = io.skew + (bb % kSkewBlocks) * 8 * 64 + lane;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) sw[0][i] = src[64 * i];
+            }
+        }
+        if (!asm_blk) {
+            if (ANYSEQ_EXP & 2) {
+#pragma unroll
+                for (int k = 0; k < R; ++k)
+#pragma unroll
+                    for (int q = 0; q < CH / 4; ++q) sw[k][q] = (uint32_t)(tb * 0x01010101 + lane + k + q);
+            } else {
+#pragma unroll
+                for (int k = 0; k < R; ++k)
+                    load_sbytes<CH>(io.s_ring, (tb - BASE - S * lane - k) & (kSRing - 1), sw[k]);
+            }
+        }
         if (bb < nchunks) {
-            STAMP(ta);
             if (io.in_border) {
                 if (lane < CH) io.my_ring[(tb + lane) & IRM] = border_top<KIND>(tb + lane, ng);
             } else if (seen_prod < (uint32_t)(bb + 1)) {
                 if (!(seen_prod = spin_lds_ge(io.my_prod, (uint32_t)(bb + 1), err))) return false;
             }
-            STAMP(tb2);
-            if (seen_sfill < (uint32_t)(bb + 1)) {
-                if (!(seen_sfill = spin_lds_ge(io.s_filled, (uint32_t)(bb + 1), err))) return false;
-            }
             STAMP(tc);
-            STAMP_ADD(ST_WAIT_IN, tb2 - ta);
-            STAMP_ADD(ST_WAIT_S, tc - tb2);
-            const int4* src = reinterpret_cast<const int4*>(io.my_ring + (tb & IRM));
-            if (ANYSEQ_EXP & 1) {
+            STAMP_ADD(ST_WAIT_IN, tc - tb2);
+            if (!asm_blk) {
+                const int4* src = reinterpret_cast<const int4*>(io.my_ring + (tb & IRM));
 #pragma unroll
-                for (int q = 0; q < CH; ++q) rv[q] = tb + q;
-            } else
-#pragma unroll
-            for (int q = 0; q < CH / 4; ++q) {
-                const int4 v = src[q];
-                rv[4 * q] = v.x;
-                rv[4 * q + 1] = v.y;
-                rv[4 * q + 2] = v.z;
-                rv[4 * q + 3] = v.w;
+                for (int q = 0; q < CH / 4; ++q) {
+                    const int4 v = src[q];
+                    rv[4 * q] = v.x;
+                    rv[4 * q + 1] = v.y;
+                    rv[4 * q + 2] = v.z;
+                    rv[4 * q + 3] = v.w;
+                }
             }
-            // chunk bb is in registers now: the producer may reuse its slot
-            if (!io.in_border) lds_st(io.my_cons, (uint32_t)(bb + 1));
         }
-        if (ANYSEQ_EXP & 2) {
-#pragma unroll
-            for (int k = 0; k < R; ++k)
-#pragma unroll
-                for (int q = 0; q < CH / 4; ++q) sw[k][q] = (uint32_t)(tb * 0x01010101 + lane + k + q);
-            return true;
-        }
-#pragma unroll
-        for (int k = 0; k < R; ++k)
-            load_sbytes<CH>(io.s_ring, (tb - BASE - S * lane - k) & (kSRing - 1), sw[k]);
         return true;
     };
 
-    if (!acquire(0)) return;
     int top_first = border_left<KIND>(rb - 1, ng);
+    // full blocks [fb, fe): all lanes inside the matrix (or on virtual columns)
+    const int fb = VIRT ? 0 : D / CH;
+    const int fe = w + BASE >= CH ? (w + BASE - CH) / CH + 1 : 0;
+    LoopArgs la;
+    if constexpr (ASM) {
+        la.rb = lds_addr(io.my_ring);
+        la.nb = io.out_lds ? lds_addr(io.next_ring) : 0u;
+        la.apr = lds_addr(io.my_prod);
+        la.acn = lds_addr(io.my_cons);
+        la.anp = io.out_lds ? lds_addr(io.next_prod) : 0u;
+        la.anc = io.out_lds ? lds_addr(io.next_cons) : 0u;
+        la.asf = lds_addr(io.s_filled);
+        la.atl = lds_addr(io.tail);
+        la.skb = lds_addr(io.skew) + 4u * lane;
+        la.lo = 4u * (lane - 32);
+        la.lid4 = 4u * lane;
+        la.bvb = (uint32_t)border_top<KIND>(lane, ng);
+        la.bvs = (uint32_t)(border_top<KIND>(1, ng) - border_top<KIND>(0, ng));
+        la.fl = (io.in_border ? 1u : 0u) | (io.trailing ? 2u : 0u) | (io.out_lds && !(ANYSEQ_EXP & 4) ? 4u : 0u);
+    }
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
+        const bool full = (VIRT || t0 >= D) && (t0 + CH <= w + BASE);
+        if constexpr (ASM) {
+            if (full && !(ANYSEQ_EXP & 32)) {
+#ifdef ANYSEQ_STAMPS
+                if (b == 0 && dbg && lane == 0 && band < 2048) dbg[16 + 4 * (band + (P.q_step < 0 ? 2048 : 0))] = __builtin_amdgcn_s_memrealtime();
+                STAMP(tl0);
+#endif
+                uint32_t bb = (uint32_t)b;
+                if (band_loop_asm<KIND>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, qv[0], cur[0], dg,
+                                        top_first, best, ck)) {
+                    atomicOr(err, ERR_SPIN_TIMEOUT);
+                    return;
+                }
+#ifdef ANYSEQ_STAMPS
+                STAMP(tl1);
+                STAMP_ADD(ST_COMPUTE, tl1 - tl0);
+#endif
+                b = (int)bb - 1;   // ++b of the for
+                continue;
+            }
+        }
+        // inputs of this block (rv/sw live only inside one iteration)
+        STAMP(t_acq0);
+        if (!acquire(b, ASM && full)) return;
         STAMP(t_comp0);
+        STAMP_ADD(ST_ACQ, t_comp0 - t_acq0);
 #ifdef ANYSEQ_STAMPS
         if (b == 0 && dbg && lane == 0 && band < 2048) dbg[16 + 4 * (band + (P.q_step < 0 ? 2048 : 0))] = __builtin_amdgcn_s_memrealtime();
 #endif
-        const bool full = (t0 >= D) && (t0 + CH <= w + BASE);
-        if (ANYSEQ_EXP & 8) {
-#pragma unroll
-            for (int u = 0; u < CH; ++u) outv[u] = rv[u] + (int)sw[0][u / 4];
-        } else if (full) {
-            if constexpr (R == 1 && X == 0 && CH == 32 && !PARTIAL && !(ANYSEQ_EXP & 16))
-                band_block_asm<KIND>(top_first, rv, sw[0], qv[0], cur[0], dg, outv, best, ck);
-            else
-                band_block<KIND, R, X, CH, false, PARTIAL>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev, upc,
-                                                           dg, outv, best, ck);
-        } else
-            band_block<KIND, R, X, CH, true, PARTIAL>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev, upc, dg,
-                                                      outv, best, ck);
-        STAMP(t_comp1);
-        STAMP_ADD(ST_COMPUTE, t_comp1 - t_comp0);
-        top_first = rv[CH - 1];
-        if (io.trailing) lds_st(io.tail, (uint32_t)(b + 1));
-
-        // ---- publish bottom-row chunk j = b - LAG (lane 63 holds it in outv)
+        // bottom-row chunk j = b - LAG is complete after this block: make room for it
         const int j = b - LAG;
-        if (io.out_lds && j >= 0) {
+        const bool pub = io.out_lds && j >= 0;
+        if (pub) {
             const uint32_t need = (uint32_t)max(0, j - kSlots + 1);
             STAMP(to0);
             if (seen_cons < need) {
@@ -463,19 +529,42 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
             }
             STAMP(to1);
             STAMP_ADD(ST_WAIT_OUT, to1 - to0);
-            if (lane == 63 && !(ANYSEQ_EXP & 4)) {
+        }
+        if (ASM && full) {
+            if constexpr (ASM) {
+                const bool st = pub && !(ANYSEQ_EXP & 4);
+                const uint32_t pa = st && lane >= 32 ? lds_addr(io.next_ring + ((j * CH) & IRM) + (lane - 32))
+                                                     : lds_addr(io.dummy + lane);
+                const uint64_t pm = 0;
+                band_block_asm<KIND>(top_first, lds_addr(io.my_ring + (t0 & IRM)), pa, pm, sw[0], qv[0], cur[0], dg,
+                                     best, ck);
+            }
+        } else {
+            if (full)
+                band_block<KIND, R, X, CH, false, PARTIAL>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev, upc,
+                                                           dg, outv, best, ck);
+            else
+                band_block<KIND, R, X, CH, true, PARTIAL, VIRT>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev,
+                                                                upc, dg, outv, best, ck);
+            top_first = rv[CH - 1];
+            if (pub && lane == 63 && !(ANYSEQ_EXP & 4)) {
                 int4* dst = reinterpret_cast<int4*>(io.next_ring + ((j * CH) & IRM));
 #pragma unroll
                 for (int q = 0; q < CH / 4; ++q)
                     dst[q] = make_int4(outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]);
             }
+        }
+        STAMP(t_comp1);
+        STAMP_ADD(ST_COMPUTE, t_comp1 - t_comp0);
+        // chunk b has been read: the producer may reuse its slot
+        if (!io.in_border && b < nchunks) lds_st(io.my_cons, (uint32_t)(b + 1));
+        if (io.trailing) lds_st(io.tail, (uint32_t)(b + 1));
+        if (pub) {
             lds_st(io.next_prod, (uint32_t)(j + 1));
 #ifdef ANYSEQ_STAMPS
             if (j == 0 && dbg && lane == 0 && band < 2048) dbg[16 + 4 * (band + (P.q_step < 0 ? 2048 : 0)) + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
         }
-        // ---- inputs of the next block into registers
-        if (b + 1 < nblocks && !acquire(b + 1)) return;
     }
     if (!io.in_border) lds_st(io.my_cons, (uint32_t)(nchunks + kSlots));
     if (io.trailing) lds_st(io.tail, 0x7fffffffu);
@@ -512,8 +601,9 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
 //  * copies this group's bottom row from the out-ring to HBM (sc1 stores,
 //    vmcnt(0), then the flag).
 // The HBM hand-off latency therefore never sits on a compute wave's critical path.
-template <int CH>
-__device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* s_filled,
+template <int CH, bool SKEW>
+__device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
+                        uint32_t* s_filled,
                         uint32_t* tail, const int32_t* g_in, uint32_t* g_in_flag, int32_t* ring0, uint32_t* prod0,
                         uint32_t* cons0, int32_t* g_out, uint32_t* g_out_flag, int32_t* oring, uint32_t* oprod,
                         uint32_t* ocons, uint32_t* err) {
@@ -522,10 +612,11 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
     const int nchunks = (w + CH - 1) / CH;
     const bool need_in = g_in != nullptr, need_out = g_out != nullptr;
     const GLOBAL_AS uint8_t* sg = gmem(s);
-    int s_next = 0, in_next = 0, out_next = 0;
+    int s_next = 0, sk_next = 0, in_next = 0, out_next = 0;
     uint32_t avail = 0, idle = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    while (s_next < nchunks || (need_in && in_next < nchunks) || (need_out && out_next < nchunks)) {
+    while (s_next < nchunks || (SKEW && sk_next < nchunks) || (need_in && in_next < nchunks) ||
+           (need_out && out_next < nchunks)) {
         bool progress = false;
         if (s_next < nchunks) {
             const uint32_t tl = lds_ld(tail);
@@ -550,8 +641,27 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                         if (p < 64) s_ring[p + kSRing] = v[i];
                     }
                 }
-                lds_st(s_filled, (uint32_t)lim);
+                if (!SKEW) lds_st(s_filled, (uint32_t)lim);
                 s_next = lim;
+                progress = true;
+            }
+        }
+        if (SKEW && sk_next < s_next) {
+            // skewed copy of block b needs raw columns 32b-64 .. 32b+31 (staged: b < s_next)
+            // and a free slot: the trailing wave has finished block b - kSkewBlocks
+            const uint32_t tl = lds_ld(tail);
+            int lim = min(s_next, tl >= 0x7fffffffu ? nchunks : (int)tl + kSkewBlocks);
+            lim = min(lim, sk_next + 8);
+            for (int b = sk_next; b < lim; ++b) {
+                uint32_t d[8];
+                load_sbytes<32>(s_ring, (32 * b - 1 - lane) & (kSRing - 1), d);
+                uint32_t* dst = skew + (b % kSkewBlocks) * 8 * 64 + lane;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) dst[64 * i] = d[i];
+            }
+            if (lim > sk_next) {
+                lds_st(s_filled, (uint32_t)lim);
+                sk_next = lim;
                 progress = true;
             }
         }
@@ -656,7 +766,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
         if (wave == NW) {
             const int32_t* g_in = g.group > 0 ? P.rowbuf + (size_t)(g.group - 1) * P.wpad : nullptr;
             uint32_t* g_in_flag = g.group > 0 ? P.flags + (g.group - 1) : nullptr;
-            io_wave<CH>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.s_filled, &sh.tail, g_in, g_in_flag,
+            io_wave<CH, R == 1 && X == 0 && CH == 32>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0],
+                                                      &sh.s_filled, &sh.tail, g_in, g_in_flag,
                         sh.in_ring[0], &sh.prod[0], &sh.cons[0], g_out, g_out_flag, sh.in_ring[NW], &sh.prod[NW],
                         &sh.cons[NW], err);
         } else {
@@ -671,6 +782,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
                 io.s_ring = sh.s_ring;
                 io.s_filled = &sh.s_filled;
                 io.tail = &sh.tail;
+                io.dummy = sh.dummy[wave];
+                io.skew = &sh.skew[0][0][0];
                 if (band < last) {
                     io.out_lds = true;
                     io.next_ring = sh.in_ring[wave + 1];

@@ -1,0 +1,295 @@
+#!/usr/bin/env python3
+"""Generate anyseq_amd/csrc/anyseq_block_asm.inc: the hand-scheduled 32-step
+steady-state block of the fill kernel (R = 1, X = 0, CH = 32) as inline-asm
+strings, one per value space (G: global/semiglobal, L: local).
+
+Per step (all lanes live):  C v_cmp_eq_u32_sdwa vcc, q, s.byte   substitution test
+                            D v_cndmask_b32     w, wx, wm, vcc   weight
+                            E v_add_u32         a, dg, w         diag + weight
+                            A v_mov_b32_dpp     T, cur wave_shr:1  up (lane 0 keeps T = top row)
+                            B v_max3_i32        O, a, cur, T     cell
+(L adds  v_sub_u32 O, O, ng clamp  and  v_max_i32 best, best, O.)
+The DPP reads `cur` written >= 3 instructions earlier (the VALU->DPP hazard needs
+2), and writes in place into the register holding the top-row value, so a step is
+five VALU with no copies and no stalls.
+
+Registers: the 32 top-row values T0..T31 and the 32 cell values O0..O31 of the
+block live in fixed VGPRs (clobbered); the top row comes in with eight broadcast
+ds_read_b128.  Lane 63's bottom row leaves through a DPP shift register: once
+O(u-1) is dead (after step u), `v_mov_b32_dpp O(u-1), O(u-2) wave_shl:1` moves
+the register down one lane while lane 63 keeps its own cell, so after the block
+lanes 32..63 of O31 hold lane 63's 32 cells in column order and ONE ds_write_b32
+(per-lane address `pa`, lanes 0..31 into a dummy slot) publishes them.  A wide
+store from a single lane would cost ~29 issue cycles per ds_write_b128 plus exec
+switches; the shift costs one VALU per step off the critical path.
+"""
+import os
+
+T0, O0, W, A = 64, 96, 128, 129   # fixed VGPRs: T 64..95, O 96..127, w, a (<= 170 VGPRs: 3 waves/SIMD)
+
+
+def v(n):
+    return f"v{n}"
+
+
+def gen(kind, reads=True, stores=True, store_mode="shift"):
+    L = kind == "L"
+    out = []
+    e = out.append
+    # top row of this block: T0..T31 = ring[ra + 0 .. 124]
+    for i in range(8):
+        if reads:
+            e(f"ds_read_b128 v[{T0 + 4 * i}:{T0 + 4 * i + 3}], %[ra] offset:{16 * i}")
+    if reads:
+        e("s_waitcnt lgkmcnt(6)")          # T0..T7 landed
+    cur = "%[cur]"
+    dg = "%[dg]"
+    for u in range(32):
+        c = u // 8
+        if u % 8 == 0 and c >= 1 and stores and store_mode != "shift":
+            # lane 63 publishes chunk c-1's eight cells (two b128 stores) before the
+            # first step of chunk c; exec is restored >= 5 instructions before the next DPP
+            o = O0 + 8 * (c - 1)
+            if store_mode == "exec":
+                e("s_mov_b64 %[sv], exec")
+                e("s_mov_b64 exec, %[pm]")
+            if store_mode != "exec_only":
+                e(f"ds_write_b128 %[pa], v[{o}:{o + 3}] offset:{32 * (c - 1)}")
+                e(f"ds_write_b128 %[pa], v[{o + 4}:{o + 7}] offset:{32 * (c - 1) + 16}")
+            if store_mode in ("exec", "exec_only"):
+                if store_mode == "exec_only":
+                    e("s_mov_b64 %[sv], exec")
+                    e("s_mov_b64 exec, %[pm]")
+                e("s_mov_b64 exec, %[sv]")
+                e("s_nop 1")
+        if u % 8 == 0 and c >= 1 and reads:
+            # chunk c reads T(8c-1)..T(8c+6), i.e. b128 reads up to r = (8c+6)//4; the
+            # 7-r younger reads and the 2c stores issued so far may stay in flight
+            r = (8 * c + 6) // 4
+            e(f"s_waitcnt lgkmcnt({7 - r + (2 * c if stores and store_mode != 'shift' else 0)})")
+        s = f"%[s{u // 4}]"
+        b = u % 4
+        tv = "%[tf]" if u == 0 else v(T0 + u - 1)
+        ov = v(O0 + u)
+        e(f"v_cmp_eq_u32_sdwa vcc, %[q], {s} src0_sel:DWORD src1_sel:BYTE_{b}")
+        e(f"v_cndmask_b32_e32 v{W}, %[wx], %[wm], vcc")
+        e(f"v_add_u32_e32 v{A}, {dg}, v{W}")
+        e(f"v_mov_b32_dpp {tv}, {cur} wave_shr:1 row_mask:0xf bank_mask:0xf")
+        e(f"v_max3_i32 {ov}, v{A}, {cur}, {tv}")
+        if L:
+            e(f"v_sub_u32_e64 {ov}, {ov}, %[ng] clamp")
+            e(f"v_max_i32_e32 %[best], %[best], {ov}")
+        if stores and store_mode == "shift" and u >= 2:
+            # O(u-1) is dead now: shift register step (lane 63 keeps its cell)
+            e(f"v_mov_b32_dpp {v(O0 + u - 1)}, {v(O0 + u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+        cur = ov
+        dg = tv
+    # last chunk's cells, then the block outputs
+    o = O0 + 24
+    if stores and store_mode == "shift":
+        e(f"v_mov_b32_e32 %[cur], v{O0 + 31}")
+        e(f"v_mov_b32_e32 %[dg], v{T0 + 30}")
+        e(f"v_mov_b32_dpp {v(O0 + 31)}, {v(O0 + 30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+        e(f"v_mov_b32_e32 %[tf], v{T0 + 31}")
+        e("s_nop 1")
+        e(f"ds_write_b32 %[pa], {v(O0 + 31)}")
+        return out
+    if stores:
+        if store_mode in ("exec", "exec_only"):
+            e("s_mov_b64 %[sv], exec")
+            e("s_mov_b64 exec, %[pm]")
+        if store_mode != "exec_only":
+            e(f"ds_write_b128 %[pa], v[{o}:{o + 3}] offset:96")
+            e(f"ds_write_b128 %[pa], v[{o + 4}:{o + 7}] offset:112")
+        if store_mode in ("exec", "exec_only"):
+            e("s_mov_b64 exec, %[sv]")
+    e(f"v_mov_b32_e32 %[cur], v{O0 + 31}")
+    e(f"v_mov_b32_e32 %[dg], v{T0 + 30}")
+    e(f"v_mov_b32_e32 %[tf], v{T0 + 31}")
+    return out
+
+SK0, VT, VT2, VA, VB = 130, 138, 139, 140, 141   # subject words, temps, LDS addresses
+TA, TB = 96, 98                                   # fixed SGPR pairs for s_memrealtime
+
+
+def wait(e, name, seen, target, addr):
+    """Spin until seen >= target, refreshing `seen` from the LDS word at `addr`
+    (wave-uniform), with s_sleep between polls and a 10 s s_memrealtime limit
+    checked every 256 polls (-> L_timeout)."""
+    e(f"s_cmp_ge_u32 {seen}, {target}")
+    e(f"s_cbranch_scc1 L_{name}_ok_%=")
+    e(f"s_memrealtime s[{TA}:{TA + 1}]")
+    e("s_mov_b32 %[x3], 0")
+    e(f"L_{name}_loop_%=:")
+    e(f"ds_read_b32 v{VT2}, {addr}")
+    e("s_waitcnt lgkmcnt(0)")
+    e(f"v_readfirstlane_b32 {seen}, v{VT2}")
+    e(f"s_cmp_ge_u32 {seen}, {target}")
+    e(f"s_cbranch_scc1 L_{name}_ok_%=")
+    e("s_sleep 1")
+    e("s_add_u32 %[x3], %[x3], 1")
+    e("s_and_b32 %[x2], %[x3], 255")
+    e(f"s_cbranch_scc1 L_{name}_loop_%=")
+    e(f"s_memrealtime s[{TB}:{TB + 1}]")
+    e("s_waitcnt lgkmcnt(0)")
+    e(f"s_sub_u32 s{TB}, s{TB}, s{TA}")
+    e(f"s_subb_u32 s{TB + 1}, s{TB + 1}, s{TA + 1}")
+    e(f"s_cmp_lg_u32 s{TB + 1}, 0")
+    e("s_cbranch_scc1 L_timeout_%=")
+    e(f"s_cmp_gt_u32 s{TB}, 1000000000")
+    e("s_cbranch_scc1 L_timeout_%=")
+    e(f"s_branch L_{name}_loop_%=")
+    e(f"L_{name}_ok_%=:")
+
+
+def gen_loop(kind):
+    """The whole steady state of a band: blocks b .. be-1 (all full) in one
+    asm statement.  Per block: wait for the subject block (s_filled) and the
+    top-row chunk (prod, or write the border for band 0), read 4 x read2st64
+    subject words + 8 x b128 top values, 32 steps, then publish lane 63's chunk
+    b-2 (one ds_write_b32 from lanes 32..63) and bump cons / tail / next_prod.
+    flags: bit0 in_border, bit1 trailing (reports tail), bit2 publishes."""
+    L = kind == "L"
+    out = []
+    e = out.append
+    e("L_top_%=:")
+    e("s_lshl_b32 %[x0], %[b], 5")              # tb
+    e("s_add_u32 %[x1], %[b], 1")               # b + 1
+    wait(e, "sf", "%[sf]", "%[x1]", "%[asf]")
+    # subject words of block b: skew[(b & 31)][i][lane]
+    e("s_and_b32 %[x2], %[b], 31")
+    e("s_lshl_b32 %[x2], %[x2], 11")
+    e(f"v_add_u32_e32 v{VA}, %[x2], %[skb]")
+    for i in range(4):
+        e(f"ds_read2st64_b32 v[{SK0 + 2 * i}:{SK0 + 2 * i + 1}], v{VA} offset0:{2 * i} offset1:{2 * i + 1}")
+    # top row: band 0 writes the scheme's border, others wait for the producer
+    e("s_bitcmp1_b32 %[fl], 0")
+    e("s_cbranch_scc0 L_notborder_%=")
+    e("s_mul_i32 %[x2], %[x0], %[bvs]")
+    e(f"v_add_u32_e32 v{VT}, %[x2], %[bvb]")
+    e("s_lshl_b32 %[x2], %[x0], 2")
+    e(f"v_add_u32_e32 v{VT2}, %[x2], %[lid4]")
+    e(f"v_and_b32_e32 v{VT2}, 0x7ff, v{VT2}")
+    e(f"v_add_u32_e32 v{VT2}, %[rb], v{VT2}")
+    e(f"ds_write_b32 v{VT2}, v{VT}")
+    e("s_branch L_havetop_%=")
+    e("L_notborder_%=:")
+    wait(e, "pr", "%[sp]", "%[x1]", "%[apr]")
+    e("L_havetop_%=:")
+    # back-pressure: chunk b-2 goes to slot (b-2) & 15, free once the consumer is at >= b-17
+    e("s_bitcmp1_b32 %[fl], 2")
+    e("s_cbranch_scc0 L_nobp_%=")
+    e("s_cmp_lt_u32 %[b], 17")
+    e("s_cbranch_scc1 L_nobp_%=")
+    e("s_sub_u32 %[x4], %[b], 17")
+    wait(e, "bp", "%[sc]", "%[x4]", "%[anc]")
+    e("L_nobp_%=:")
+    # the 32 top values of chunk b
+    e("s_and_b32 %[x2], %[x0], 511")
+    e("s_lshl_b32 %[x2], %[x2], 2")
+    e("s_add_u32 %[x2], %[x2], %[rb]")
+    e(f"v_mov_b32_e32 v{VB}, %[x2]")
+    for i in range(8):
+        e(f"ds_read_b128 v[{T0 + 4 * i}:{T0 + 4 * i + 3}], v{VB} offset:{16 * i}")
+    # ops in flight: 4 subject reads, then 8 top reads
+    cur = "%[cur]"
+    dg = "%[dg]"
+    for u in range(32):
+        c = u // 8
+        if u % 8 == 0:
+            r = (8 * c + 6) // 4          # last top read chunk c needs
+            e(f"s_waitcnt lgkmcnt({7 - r})")
+        sw = v(SK0 + u // 4)
+        b = u % 4
+        tv = "%[tf]" if u == 0 else v(T0 + u - 1)
+        ov = v(O0 + u)
+        e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{b}")
+        e(f"v_cndmask_b32_e32 v{W}, %[wx], %[wm], vcc")
+        e(f"v_add_u32_e32 v{A}, {dg}, v{W}")
+        e(f"v_mov_b32_dpp {tv}, {cur} wave_shr:1 row_mask:0xf bank_mask:0xf")
+        e(f"v_max3_i32 {ov}, v{A}, {cur}, {tv}")
+        if L:
+            e(f"v_sub_u32_e64 {ov}, {ov}, %[ng] clamp")
+            e(f"v_max_i32_e32 %[best], %[best], {ov}")
+        if u >= 2:
+            e(f"v_mov_b32_dpp {v(O0 + u - 1)}, {v(O0 + u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+        cur = ov
+        dg = tv
+    e(f"v_mov_b32_e32 %[cur], v{O0 + 31}")
+    e(f"v_mov_b32_e32 %[dg], v{T0 + 30}")
+    e(f"v_mov_b32_dpp {v(O0 + 31)}, {v(O0 + 30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    e(f"v_mov_b32_e32 %[tf], v{T0 + 31}")
+    # publish chunk j = b - 2 (lanes 32..63 of O31 hold it in column order)
+    e("s_bitcmp1_b32 %[fl], 2")
+    e("s_cbranch_scc0 L_nopub_%=")
+    e("s_cmp_lt_u32 %[b], 2")
+    e("s_cbranch_scc1 L_nopub_%=")
+    e("s_sub_u32 %[x2], %[b], 2")
+    e("s_lshl_b32 %[x2], %[x2], 7")
+    e("s_and_b32 %[x2], %[x2], 2047")
+    e("s_add_u32 %[x2], %[x2], %[nb]")
+    e(f"v_add_u32_e32 v{VT}, %[x2], %[lo]")
+    e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
+    e("s_mov_b64 exec, %[hm]")
+    e(f"ds_write_b32 v{VT}, v{O0 + 31}")
+    e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
+    e("s_sub_u32 %[x2], %[b], 1")
+    e(f"v_mov_b32_e32 v{VT2}, %[x2]")
+    e(f"ds_write_b32 %[anp], v{VT2}")
+    e("L_nopub_%=:")
+    # release the in-ring slot / report the trailing wave's progress
+    e(f"v_mov_b32_e32 v{VT2}, %[x1]")
+    e("s_bitcmp1_b32 %[fl], 0")
+    e("s_cbranch_scc1 L_nocons_%=")
+    e(f"ds_write_b32 %[acn], v{VT2}")
+    e("L_nocons_%=:")
+    e("s_bitcmp1_b32 %[fl], 1")
+    e("s_cbranch_scc0 L_notail_%=")
+    e(f"ds_write_b32 %[atl], v{VT2}")
+    e("L_notail_%=:")
+    e("s_mov_b32 %[b], %[x1]")
+    e("s_cmp_lt_u32 %[b], %[be]")
+    e("s_cbranch_scc1 L_top_%=")
+    e("s_mov_b32 %[st], 0")
+    e("s_branch L_end_%=")
+    e("L_timeout_%=:")
+    e("s_mov_b32 %[st], 1")
+    e("L_end_%=:")
+    return out
+
+
+def main():
+    here = os.path.dirname(os.path.abspath(__file__))
+    dst = os.path.join(here, "..", "anyseq_amd", "csrc", "anyseq_block_asm.inc")
+    lines = ["// GENERATED by tools/gen_block_asm.py -- do not edit.", ""]
+    variants = [("G", "G", {}), ("L", "L", {}),
+                # timing variants for tools/micro/block_micro.hip
+                ("G_NOST", "G", {"stores": False}), ("G_NORD", "G", {"reads": False}),
+                ("G_NONE", "G", {"stores": False, "reads": False}),
+                ("G_ALLST", "G", {"reads": False, "store_mode": "all"}),
+                ("G_EXONLY", "G", {"reads": False, "store_mode": "exec_only"}),
+                ("G_EXEC", "G", {"store_mode": "exec"})]
+    for name, kind, kw in variants:
+        body = gen(kind, **kw)
+        lines.append(f"#define ANYSEQ_BLOCK_ASM_{name} \\")
+        for ln in body:
+            lines.append(f'    "{ln}\\n" \\')
+        lines.append("")
+    for name, kind in (("G", "G"), ("L", "L")):
+        lines.append(f"#define ANYSEQ_LOOP_ASM_{name} \\")
+        for ln in gen_loop(kind):
+            lines.append(f'    "{ln}\\n" \\')
+        lines.append("")
+    clob = ", ".join(f'"v{n}"' for n in range(T0, A + 1))
+    lines.append(f"#define ANYSEQ_BLOCK_ASM_CLOBBERS {clob}, \"vcc\"")
+    clob = ", ".join(f'"v{n}"' for n in range(T0, VB + 1))
+    sclob = ", ".join(f'"s{n}"' for n in range(TA, TB + 2))
+    lines.append(f"#define ANYSEQ_LOOP_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
+    lines.append("")
+    with open(dst, "w") as f:
+        f.write("\n".join(lines))
+    print("wrote", dst)
+
+
+if __name__ == "__main__":
+    main()

@@ -11,7 +11,7 @@
 using namespace anyseq;
 
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void chain(const uint8_t* q, int w, uint32_t* err, unsigned long long* out, int32_t* col) {
+__global__ __launch_bounds__(64 * NW) void chain(const uint8_t* q, int w, uint32_t* err, unsigned long long* out, int32_t* col, unsigned long long* dbg) {
     constexpr int CH = 32;
     __shared__ __attribute__((aligned(16))) FillShared<NW, CH> sh;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -34,12 +34,14 @@ __global__ __launch_bounds__(64 * NW) void chain(const uint8_t* q, int w, uint32
     io.s_ring = sh.s_ring;
     io.s_filled = &sh.s_filled;
     io.tail = &sh.tail;
+    io.dummy = sh.dummy[wave];
+    io.skew = &sh.skew[0][0][0];
     io.out_lds = wave < NW - 1;
     io.next_ring = sh.in_ring[wave + 1];
     io.next_prod = &sh.prod[wave + 1];
     io.next_cons = &sh.cons[wave + 1];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    run_band<KIND_GLOBAL, 1, 0, CH, false>(P, wave, lane, io, err, ck, nullptr);
+    run_band<KIND_GLOBAL, 1, 0, CH, false>(P, wave, lane, io, err, ck, dbg);
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) { out[2 * (blockIdx.x * NW + wave)] = t0; out[2 * (blockIdx.x * NW + wave) + 1] = t1; }
 }
@@ -51,11 +53,12 @@ void run(int grid, int w) {
     hipMalloc(&err, 4); hipMemset(err, 0, 4);
     hipMalloc(&out, 16 * grid * NW);
     int32_t* col; hipMalloc(&col, 4 * 64 * NW * grid);
-    hipLaunchKernelGGL(chain<NW>, dim3(grid), dim3(64 * NW), 0, 0, q, w, err, out, col);
+    unsigned long long* dbg; hipMalloc(&dbg, 8 * 64); hipMemset(dbg, 0, 8 * 64);
+    hipLaunchKernelGGL(chain<NW>, dim3(grid), dim3(64 * NW), 0, 0, q, w, err, out, col, nullptr);
     hipDeviceSynchronize();
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     hipEventRecord(e0);
-    hipLaunchKernelGGL(chain<NW>, dim3(grid), dim3(64 * NW), 0, 0, q, w, err, out, col);
+    hipLaunchKernelGGL(chain<NW>, dim3(grid), dim3(64 * NW), 0, 0, q, w, err, out, col, dbg);
     hipEventRecord(e1); hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
     std::vector<unsigned long long> h(2 * grid * NW);
@@ -65,7 +68,17 @@ void run(int grid, int w) {
     printf("NW=%d grid=%d w=%d: kernel %.3f ms | wave0 %.1f ns/block | last wave %.1f ns/block, start lag %.2f us/band | err %u\n",
            NW, grid, w, ms, (h[1] - h[0]) * 10.0 / nb, (h[2 * NW - 1] - h[2 * NW - 2]) * 10.0 / nb,
            (h[2 * NW - 2] - h[0]) / 100.0 / (NW > 1 ? NW - 1 : 1), e);
-    hipFree(q); hipFree(err); hipFree(out); hipFree(col);
+#ifdef ANYSEQ_STAMPS
+    unsigned long long hd[16];
+    hipMemcpy(hd, dbg, 128, hipMemcpyDeviceToHost);
+    const double bands = hd[ST_BANDS] ? (double)hd[ST_BANDS] : 1.0, blocks = hd[ST_BLOCKS] ? (double)hd[ST_BLOCKS] : 1.0;
+    printf("    stamps per block (cycles): total %.0f | acquire %.0f (wait_in %.0f wait_s %.0f) | compute %.0f | "
+           "publish %.0f (wait_out %.0f)\n",
+           hd[ST_TOTAL] / blocks, hd[ST_ACQ] / blocks, hd[ST_WAIT_IN] / blocks, hd[ST_WAIT_S] / blocks,
+           hd[ST_COMPUTE] / blocks, hd[ST_PUB] / blocks, hd[ST_WAIT_OUT] / blocks);
+    (void)bands;
+#endif
+    hipFree(q); hipFree(err); hipFree(out); hipFree(col); hipFree(dbg);
 }
 
 int main(int argc, char** argv) {
