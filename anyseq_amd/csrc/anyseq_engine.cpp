@@ -182,6 +182,8 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     HIPCHECK(hipMemcpyAsync(d_probs, probs.data(), probs.size() * sizeof(DPProblem), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(d_groups, groups.data(), groups.size() * sizeof(GroupRef), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemsetAsync(flags, 0, flag_words * 4, st));
+    // group -> group hand-off rows start as the sentinel -1 (the consumer polls the data)
+    if (rowbuf_ints) HIPCHECK(hipMemsetAsync(rowbuf, 0xff, rowbuf_ints * 4, st));
     uint32_t* ctr = (uint32_t*)E.ctr.get(128);
     HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));  // ctr[0] = dequeue counter, ctr[1] = error word
     int grid = g_tuning.grid > 0 ? g_tuning.grid : E.num_cus;
@@ -206,13 +208,15 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     uint32_t err = 0;
     HIPCHECK(hipMemcpy(&err, ctr + 1, 4, hipMemcpyDeviceToHost));
     if (dbg) {
-        unsigned long long h[8];
+        unsigned long long h[16];
         HIPCHECK(hipMemcpy(h, dbg, sizeof h, hipMemcpyDeviceToHost));
+        const double nb = (double)std::max(1ull, h[6]);
         fprintf(stderr,
                 "anyseq stamps: %.3f ms R=%d NW=%d bands=%llu blocks=%llu | per band: total %.0f cyc, compute %.0f, "
-                "wait_in %.0f, wait_s %.0f, wait_out %.0f | compute/block %.1f cyc\n",
+                "wait_in %.0f, wait_s %.0f, wait_out %.0f | compute/block %.1f cyc | polls/block: subject %.2f "
+                "in %.2f out %.2f\n",
                 ms, R, NW, h[5], h[6], (double)h[0] / h[5], (double)h[1] / h[5], (double)h[2] / h[5],
-                (double)h[3] / h[5], (double)h[4] / h[5], (double)h[1] / std::max(1ull, h[6]));
+                (double)h[3] / h[5], (double)h[4] / h[5], (double)h[1] / nb, h[10] / nb, h[11] / nb, h[12] / nb);
         if (const char* tl = getenv("ANYSEQ_TIMELINE")) {
             std::vector<unsigned long long> t(4 * 4096);
             HIPCHECK(hipMemcpy(t.data(), dbg + 16, t.size() * 8, hipMemcpyDeviceToHost));

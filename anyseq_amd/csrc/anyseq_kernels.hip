@@ -161,7 +161,7 @@ __device__ __forceinline__ GLOBAL_AS T* gmem(T* p) {
 #define STAMP(var)
 #define STAMP_ADD(slot, v)
 #endif
-enum { ST_TOTAL = 0, ST_COMPUTE, ST_WAIT_IN, ST_WAIT_S, ST_WAIT_OUT, ST_BANDS, ST_BLOCKS, ST_IO_TOTAL, ST_ACQ, ST_PUB, ST_NSLOTS };
+enum { ST_TOTAL = 0, ST_COMPUTE, ST_WAIT_IN, ST_WAIT_S, ST_WAIT_OUT, ST_BANDS, ST_BLOCKS, ST_IO_TOTAL, ST_ACQ, ST_PUB, ST_POLL_S, ST_POLL_IN, ST_POLL_OUT, ST_NSLOTS };
 
 // Band geometry.  Lane l owns rows r_k = rb + R*l + k (k < R) and at step t
 // row k processes column
@@ -235,6 +235,7 @@ struct WaveIO {
     uint32_t* tail;
     int32_t* dummy;            // 64 ints of this wave's scratch
     const uint32_t* skew;      // pre-skewed subject blocks (FillShared::skew)
+    int32_t* gout;             // last band of a group: global destination of the bottom row (or null)
 };
 
 // CH steps t0 .. t0+CH-1 from registers: top_first = top row at column t0-1,
@@ -296,15 +297,25 @@ struct LoopArgs {
     uint32_t lid4;                          // 4*lane
     uint32_t bvb;                           // border value of column `lane` (band 0)
     uint32_t bvs;                           // border value step per column (band 0)
-    uint32_t fl;                            // bit0 in_border, bit1 trailing, bit2 publishes
+    uint32_t fl;                            // bit0 in_border, bit1 trailing, bit2 publishes (LDS), bit3 (global)
+    uint64_t gp;                            // global bottom-row destination (bit 3)
 };
 
 // Blocks b .. be-1 of a band (all full) in one asm statement (tools/gen_block_asm.py,
 // gen_loop).  Returns 0, or 1 on a spin timeout.  b is advanced to be on success.
+#ifdef ANYSEQ_STAMPS   // diagnostic build: the loop also returns the time block 0's inputs were ready
+#define AQ_LOOP_G ANYSEQ_LOOP_ASM_G_TS
+#define AQ_LOOP_L ANYSEQ_LOOP_ASM_L_TS
+#define AQ_TS_OUT , [ts] "+s"(tsv), [nsf] "+s"(npoll[0]), [npr] "+s"(npoll[1]), [nbp] "+s"(npoll[2])
+#else
+#define AQ_LOOP_G ANYSEQ_LOOP_ASM_G
+#define AQ_LOOP_L ANYSEQ_LOOP_ASM_L
+#define AQ_TS_OUT
+#endif
 template <int KIND>
 __device__ __forceinline__ uint32_t band_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                   const LoopArgs& la, int q, int& cur, int& dg, int& tf, int& best,
-                                                  const CellK& ck) {
+                                                  const CellK& ck, uint64_t& tsv, uint32_t (&npoll)[3]) {
     uint32_t st, x0, x1, x2, x3, x4;
     const uint64_t hm = 0xffffffff00000000ull;
     // "s" operands must be provably uniform SGPR values
@@ -315,26 +326,28 @@ __device__ __forceinline__ uint32_t band_loop_asm(uint32_t& b, uint32_t be, uint
     sc = RFL(sc);
     be = RFL(be);
     const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), fl = RFL(la.fl);
+    // (readfirstlane returns int: widen through uint32_t, or bit 31 sign-extends into the high half)
+    const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
 #undef RFL
     if constexpr (KIND == KIND_LOCAL) {
-        asm volatile(ANYSEQ_LOOP_ASM_L
+        asm volatile(AQ_LOOP_L
                      : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [best] "+v"(best), [b] "+s"(b), [sp] "+s"(sp),
                        [sf] "+s"(sf), [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2),
-                       [x3] "=&s"(x3), [x4] "=&s"(x4)
+                       [x3] "=&s"(x3), [x4] "=&s"(x4) AQ_TS_OUT
                      : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [ng] "v"(ck.ng), [rb] "s"(rb),
                        [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc),
                        [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4),
-                       [bvb] "v"(la.bvb), [bvs] "s"(bvs), [fl] "s"(fl), [hm] "s"(hm)
+                       [bvb] "v"(la.bvb), [bvs] "s"(bvs), [fl] "s"(fl), [hm] "s"(hm), [gp] "s"(gp)
                      : ANYSEQ_LOOP_ASM_CLOBBERS, "memory");
     } else {
-        asm volatile(ANYSEQ_LOOP_ASM_G
+        asm volatile(AQ_LOOP_G
                      : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf),
                        [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3),
-                       [x4] "=&s"(x4)
+                       [x4] "=&s"(x4) AQ_TS_OUT
                      : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [rb] "s"(rb), [nb] "s"(nb),
                        [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc), [asf] "v"(la.asf),
                        [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4), [bvb] "v"(la.bvb),
-                       [bvs] "s"(bvs), [fl] "s"(fl), [hm] "s"(hm)
+                       [bvs] "s"(bvs), [fl] "s"(fl), [hm] "s"(hm), [gp] "s"(gp)
                      : ANYSEQ_LOOP_ASM_CLOBBERS, "memory");
     }
     return st;
@@ -467,8 +480,7 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
     };
 
     int top_first = border_left<KIND>(rb - 1, ng);
-    // full blocks [fb, fe): all lanes inside the matrix (or on virtual columns)
-    const int fb = VIRT ? 0 : D / CH;
+    // full blocks end at fe (they start at 0 for VIRT, at D / CH otherwise)
     const int fe = w + BASE >= CH ? (w + BASE - CH) / CH + 1 : 0;
     LoopArgs la;
     if constexpr (ASM) {
@@ -485,7 +497,9 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         la.lid4 = 4u * lane;
         la.bvb = (uint32_t)border_top<KIND>(lane, ng);
         la.bvs = (uint32_t)(border_top<KIND>(1, ng) - border_top<KIND>(0, ng));
-        la.fl = (io.in_border ? 1u : 0u) | (io.trailing ? 2u : 0u) | (io.out_lds && !(ANYSEQ_EXP & 4) ? 4u : 0u);
+        la.fl = (io.in_border ? 1u : 0u) | (io.trailing ? 2u : 0u) | (io.out_lds && !(ANYSEQ_EXP & 4) ? 4u : 0u) |
+                (io.gout ? 8u : 0u);
+        la.gp = (uint64_t)(size_t)io.gout;
     }
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
@@ -497,14 +511,20 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
                 STAMP(tl0);
 #endif
                 uint32_t bb = (uint32_t)b;
+                uint64_t tsv = 0;
+                uint32_t npoll[3] = {0, 0, 0};
                 if (band_loop_asm<KIND>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, qv[0], cur[0], dg,
-                                        top_first, best, ck)) {
+                                        top_first, best, ck, tsv, npoll)) {
                     atomicOr(err, ERR_SPIN_TIMEOUT);
                     return;
                 }
 #ifdef ANYSEQ_STAMPS
                 STAMP(tl1);
                 STAMP_ADD(ST_COMPUTE, tl1 - tl0);
+                if (b == 0 && dbg && lane == 0 && band < 2048) dbg[16 + 4 * (band + (P.q_step < 0 ? 2048 : 0))] = tsv;
+                acc[ST_POLL_S] += npoll[0];
+                acc[ST_POLL_IN] += npoll[1];
+                acc[ST_POLL_OUT] += npoll[2];
 #endif
                 b = (int)bb - 1;   // ++b of the for
                 continue;
@@ -552,6 +572,13 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
 #pragma unroll
                 for (int q = 0; q < CH / 4; ++q)
                     dst[q] = make_int4(outv[4 * q], outv[4 * q + 1], outv[4 * q + 2], outv[4 * q + 3]);
+            }
+            if (io.gout && j >= 0 && lane == 63) {
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+                    if (j * CH + u < w)
+                        __hip_atomic_store(gmem(io.gout) + j * CH + u, outv[u], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         STAMP(t_comp1);
@@ -603,20 +630,17 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
 // The HBM hand-off latency therefore never sits on a compute wave's critical path.
 template <int CH, bool SKEW>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
-                        uint32_t* s_filled,
-                        uint32_t* tail, const int32_t* g_in, uint32_t* g_in_flag, int32_t* ring0, uint32_t* prod0,
-                        uint32_t* cons0, int32_t* g_out, uint32_t* g_out_flag, int32_t* oring, uint32_t* oprod,
-                        uint32_t* ocons, uint32_t* err) {
+                        uint32_t* s_filled, uint32_t* tail, const int32_t* g_in, int32_t* ring0, uint32_t* prod0,
+                        uint32_t* cons0, uint32_t* err) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
     const int nchunks = (w + CH - 1) / CH;
-    const bool need_in = g_in != nullptr, need_out = g_out != nullptr;
+    const bool need_in = g_in != nullptr;
     const GLOBAL_AS uint8_t* sg = gmem(s);
-    int s_next = 0, sk_next = 0, in_next = 0, out_next = 0;
-    uint32_t avail = 0, idle = 0;
+    int s_next = 0, sk_next = 0, in_next = 0;
+    uint32_t idle = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    while (s_next < nchunks || (SKEW && sk_next < nchunks) || (need_in && in_next < nchunks) ||
-           (need_out && out_next < nchunks)) {
+    while (s_next < nchunks || (SKEW && sk_next < nchunks) || (need_in && in_next < nchunks)) {
         bool progress = false;
         if (s_next < nchunks) {
             const uint32_t tl = lds_ld(tail);
@@ -666,46 +690,42 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             }
         }
         if (need_in && in_next < nchunks) {
-            if ((int)avail <= in_next)
-                avail = __hip_atomic_load(gmem(g_in_flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int lim = min(min((int)avail, (int)lds_ld(cons0) + kSlots), nchunks);
+            // The previous group's last band stores its bottom row straight into g_in
+            // (sc1), which the host filled with the sentinel -1 (never a kernel value:
+            // G >= 0 and local H >= 0).  Poll the data itself: a chunk is ready when
+            // none of its columns < w still holds -1.
+            const int lim = min((int)lds_ld(cons0) + kSlots, nchunks);
             if (lim > in_next) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                // all loads of the batch in flight before the first LDS write (<= kSlots*CH values)
-                constexpr int PER = kSlots * CH / 64;
+                constexpr int PER = kSlots * CH / 64;   // 2 chunks per load row
                 int v[PER];
                 const int c0 = in_next * CH, c1 = lim * CH;
 #pragma unroll
                 for (int i = 0; i < PER; ++i) {
                     const int col = c0 + i * 64 + lane;
-                    v[i] = col < c1 ? __hip_atomic_load(gmem(g_in) + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                    : 0;
+                    v[i] = col < c1 && col < w
+                               ? __hip_atomic_load(gmem(g_in) + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0;
                 }
+                // leading run of complete chunks
+                int ready = 0;
+                bool stop = false;
 #pragma unroll
                 for (int i = 0; i < PER; ++i) {
-                    const int col = c0 + i * 64 + lane;
-                    if (col < c1) ring0[col & IRM] = v[i];
+                    const uint64_t bad = __ballot(v[i] == -1);
+                    if (!stop && in_next + 2 * i < lim && (uint32_t)bad == 0u) ++ready; else stop = true;
+                    if (!stop && in_next + 2 * i + 1 < lim && (uint32_t)(bad >> 32) == 0u) ++ready; else stop = true;
                 }
-                lds_st(prod0, (uint32_t)lim);
-                in_next = lim;
-                progress = true;
-            }
-        }
-        if (need_out && out_next < nchunks) {
-            const int p = min((int)lds_ld(oprod), nchunks);
-            if (p > out_next) {
-                for (int col = out_next * CH + lane; col < p * CH; col += 64)
-                    __hip_atomic_store(gmem(g_out) + col, oring[col & IRM], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                lds_st(ocons, (uint32_t)p);
-                if (g_out_flag) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0)
-                        __hip_atomic_store(gmem(g_out_flag), (uint32_t)p, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                if (ready > 0) {
+                    const int c2 = (in_next + ready) * CH;
+#pragma unroll
+                    for (int i = 0; i < PER; ++i) {
+                        const int col = c0 + i * 64 + lane;
+                        if (col < c2) ring0[col & IRM] = v[i];
+                    }
+                    lds_st(prod0, (uint32_t)(in_next + ready));
+                    in_next += ready;
+                    progress = true;
                 }
-                out_next = p;
-                progress = true;
             }
         }
         if (!progress) {
@@ -754,22 +774,19 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
         const DPProblem P = probs[g.prob];
         const int first = g.group * NW;
         const int last = min(P.nbands, first + NW) - 1;   // last band of this group
-        // where the group's bottom row goes: the next group, the problem's out_row, or nowhere
+        // where the group's bottom row goes: the next group's input row (rowbuf, pre-filled
+        // with the sentinel -1), the problem's out_row, or nowhere.  The group's last band
+        // stores it there itself.
         int32_t* g_out = nullptr;
-        uint32_t* g_out_flag = nullptr;
-        if (last < P.nbands - 1) {
+        if (last < P.nbands - 1)
             g_out = P.rowbuf + (size_t)g.group * P.wpad;
-            g_out_flag = P.flags + g.group;
-        } else if (P.out_row) {
+        else if (P.out_row)
             g_out = P.out_row;
-        }
         if (wave == NW) {
             const int32_t* g_in = g.group > 0 ? P.rowbuf + (size_t)(g.group - 1) * P.wpad : nullptr;
-            uint32_t* g_in_flag = g.group > 0 ? P.flags + (g.group - 1) : nullptr;
             io_wave<CH, R == 1 && X == 0 && CH == 32>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0],
-                                                      &sh.s_filled, &sh.tail, g_in, g_in_flag,
-                        sh.in_ring[0], &sh.prod[0], &sh.cons[0], g_out, g_out_flag, sh.in_ring[NW], &sh.prod[NW],
-                        &sh.cons[NW], err);
+                                                      &sh.s_filled, &sh.tail, g_in, sh.in_ring[0], &sh.prod[0],
+                                                      &sh.cons[0], err);
         } else {
             const int band = first + wave;
             if (band <= last) {
@@ -784,16 +801,18 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
                 io.tail = &sh.tail;
                 io.dummy = sh.dummy[wave];
                 io.skew = &sh.skew[0][0][0];
+                io.gout = nullptr;
                 if (band < last) {
                     io.out_lds = true;
                     io.next_ring = sh.in_ring[wave + 1];
                     io.next_prod = &sh.prod[wave + 1];
                     io.next_cons = &sh.cons[wave + 1];
                 } else {
-                    io.out_lds = g_out != nullptr;
-                    io.next_ring = sh.in_ring[NW];
-                    io.next_prod = &sh.prod[NW];
-                    io.next_cons = &sh.cons[NW];
+                    io.out_lds = false;
+                    io.gout = g_out;
+                    io.next_ring = nullptr;
+                    io.next_prod = nullptr;
+                    io.next_cons = nullptr;
                 }
                 const bool partial = (band + 1) * 64 * R > P.h;
                 if (partial)

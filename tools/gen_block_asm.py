@@ -112,7 +112,7 @@ SK0, VT, VT2, VA, VB = 130, 138, 139, 140, 141   # subject words, temps, LDS add
 TA, TB = 96, 98                                   # fixed SGPR pairs for s_memrealtime
 
 
-def wait(e, name, seen, target, addr):
+def wait(e, name, seen, target, addr, count=None):
     """Spin until seen >= target, refreshing `seen` from the LDS word at `addr`
     (wave-uniform), with s_sleep between polls and a 10 s s_memrealtime limit
     checked every 256 polls (-> L_timeout)."""
@@ -126,6 +126,8 @@ def wait(e, name, seen, target, addr):
     e(f"v_readfirstlane_b32 {seen}, v{VT2}")
     e(f"s_cmp_ge_u32 {seen}, {target}")
     e(f"s_cbranch_scc1 L_{name}_ok_%=")
+    if count:
+        e(f"s_add_u32 {count}, {count}, 1")
     e("s_sleep 1")
     e("s_add_u32 %[x3], %[x3], 1")
     e("s_and_b32 %[x2], %[x3], 255")
@@ -142,7 +144,7 @@ def wait(e, name, seen, target, addr):
     e(f"L_{name}_ok_%=:")
 
 
-def gen_loop(kind):
+def gen_loop(kind, ts=False):
     """The whole steady state of a band: blocks b .. be-1 (all full) in one
     asm statement.  Per block: wait for the subject block (s_filled) and the
     top-row chunk (prod, or write the border for band 0), read 4 x read2st64
@@ -155,7 +157,7 @@ def gen_loop(kind):
     e("L_top_%=:")
     e("s_lshl_b32 %[x0], %[b], 5")              # tb
     e("s_add_u32 %[x1], %[b], 1")               # b + 1
-    wait(e, "sf", "%[sf]", "%[x1]", "%[asf]")
+    wait(e, "sf", "%[sf]", "%[x1]", "%[asf]", "%[nsf]" if ts else None)
     # subject words of block b: skew[(b & 31)][i][lane]
     e("s_and_b32 %[x2], %[b], 31")
     e("s_lshl_b32 %[x2], %[x2], 11")
@@ -174,15 +176,22 @@ def gen_loop(kind):
     e(f"ds_write_b32 v{VT2}, v{VT}")
     e("s_branch L_havetop_%=")
     e("L_notborder_%=:")
-    wait(e, "pr", "%[sp]", "%[x1]", "%[apr]")
+    wait(e, "pr", "%[sp]", "%[x1]", "%[apr]", "%[npr]" if ts else None)
     e("L_havetop_%=:")
+    if ts:
+        # diagnostic builds: s_memrealtime when block 0's inputs are ready (-> %[ts])
+        e("s_cmp_lg_u32 %[b], 0")
+        e("s_cbranch_scc1 L_nots_%=")
+        e("s_memrealtime %[ts]")
+        e("s_waitcnt lgkmcnt(0)")
+        e("L_nots_%=:")
     # back-pressure: chunk b-2 goes to slot (b-2) & 15, free once the consumer is at >= b-17
     e("s_bitcmp1_b32 %[fl], 2")
     e("s_cbranch_scc0 L_nobp_%=")
     e("s_cmp_lt_u32 %[b], 17")
     e("s_cbranch_scc1 L_nobp_%=")
     e("s_sub_u32 %[x4], %[b], 17")
-    wait(e, "bp", "%[sc]", "%[x4]", "%[anc]")
+    wait(e, "bp", "%[sc]", "%[x4]", "%[anc]", "%[nbp]" if ts else None)
     e("L_nobp_%=:")
     # the 32 top values of chunk b
     e("s_and_b32 %[x2], %[x0], 511")
@@ -237,6 +246,19 @@ def gen_loop(kind):
     e(f"v_mov_b32_e32 v{VT2}, %[x2]")
     e(f"ds_write_b32 %[anp], v{VT2}")
     e("L_nopub_%=:")
+    # the group's last band: chunk j = b - 2 straight to global memory (sc1, lanes 32..63)
+    e("s_bitcmp1_b32 %[fl], 3")
+    e("s_cbranch_scc0 L_nogpub_%=")
+    e("s_cmp_lt_u32 %[b], 2")
+    e("s_cbranch_scc1 L_nogpub_%=")
+    e("s_sub_u32 %[x2], %[b], 2")
+    e("s_lshl_b32 %[x2], %[x2], 7")
+    e(f"v_add_u32_e32 v{VT}, %[x2], %[lo]")
+    e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
+    e("s_mov_b64 exec, %[hm]")
+    e(f"global_store_dword v{VT}, v{O0 + 31}, %[gp] sc1")
+    e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
+    e("L_nogpub_%=:")
     # release the in-ring slot / report the trailing wave's progress
     e(f"v_mov_b32_e32 v{VT2}, %[x1]")
     e("s_bitcmp1_b32 %[fl], 0")
@@ -275,9 +297,9 @@ def main():
         for ln in body:
             lines.append(f'    "{ln}\\n" \\')
         lines.append("")
-    for name, kind in (("G", "G"), ("L", "L")):
+    for name, kind, ts in (("G", "G", False), ("L", "L", False), ("G_TS", "G", True), ("L_TS", "L", True)):
         lines.append(f"#define ANYSEQ_LOOP_ASM_{name} \\")
-        for ln in gen_loop(kind):
+        for ln in gen_loop(kind, ts):
             lines.append(f'    "{ln}\\n" \\')
         lines.append("")
     clob = ", ".join(f'"v{n}"' for n in range(T0, A + 1))

@@ -36,6 +36,7 @@ __global__ __launch_bounds__(64 * NW) void chain(const uint8_t* q, int w, uint32
     io.tail = &sh.tail;
     io.dummy = sh.dummy[wave];
     io.skew = &sh.skew[0][0][0];
+    io.gout = nullptr;
     io.out_lds = wave < NW - 1;
     io.next_ring = sh.in_ring[wave + 1];
     io.next_prod = &sh.prod[wave + 1];
