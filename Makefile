@@ -7,6 +7,10 @@ LIB := anyseq_amd/libanyseq.so
 
 all: $(LIB) oracle
 
+# the steady-state loop of the fill kernel is generated asm (tools/gen_block_asm.py)
+$(SRC)/anyseq_block_asm.inc: tools/gen_block_asm.py
+	python3 tools/gen_block_asm.py > /dev/null
+
 $(SRC)/anyseq_kernels.o: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_internal.h $(SRC)/anyseq_block_asm.inc
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -c $< -o $@
 

@@ -302,17 +302,37 @@ struct LoopArgs {
 };
 
 // Blocks b .. be-1 of a band (all full) in one asm statement (tools/gen_block_asm.py,
-// gen_loop).  Returns 0, or 1 on a spin timeout.  b is advanced to be on success.
-#ifdef ANYSEQ_STAMPS   // diagnostic build: the loop also returns the time block 0's inputs were ready
-#define AQ_LOOP_G ANYSEQ_LOOP_ASM_G_TS
-#define AQ_LOOP_L ANYSEQ_LOOP_ASM_L_TS
+// gen_loop2), specialised by the band's role: BORDER (band 0 writes the top border)
+// and PUB (0: no bottom row, 1: LDS ring of the next band, 2: HBM row of the next
+// group / out_row).  Returns 0, or 1 on a spin timeout; b is advanced to be.
+#ifdef ANYSEQ_STAMPS   // diagnostic build: also block 0's ready time and poll counts
+#define AQ_NAME(K, B, P) ANYSEQ_LOOP2_##K##_##B##_##P##_TS
 #define AQ_TS_OUT , [ts] "+s"(tsv), [nsf] "+s"(npoll[0]), [npr] "+s"(npoll[1]), [nbp] "+s"(npoll[2])
 #else
-#define AQ_LOOP_G ANYSEQ_LOOP_ASM_G
-#define AQ_LOOP_L ANYSEQ_LOOP_ASM_L
+#define AQ_NAME(K, B, P) ANYSEQ_LOOP2_##K##_##B##_##P
 #define AQ_TS_OUT
 #endif
-template <int KIND>
+#define AQ_ASM_G(NAME)                                                                                          \
+    asm volatile(NAME                                                                                          \
+                 : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf),     \
+                   [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3), \
+                   [x4] "=&s"(x4) AQ_TS_OUT                                                                    \
+                 : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [rb] "s"(rb), [nb] "s"(nb),       \
+                   [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc), [asf] "v"(la.asf), \
+                   [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4), [bvb] "v"(la.bvb), \
+                   [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp)                                                  \
+                 : ANYSEQ_LOOP2_ASM_CLOBBERS, "memory")
+#define AQ_ASM_L(NAME)                                                                                          \
+    asm volatile(NAME                                                                                          \
+                 : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [best] "+v"(best), [b] "+s"(b), [sp] "+s"(sp), \
+                   [sf] "+s"(sf), [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), \
+                   [x3] "=&s"(x3), [x4] "=&s"(x4) AQ_TS_OUT                                                    \
+                 : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [ng] "v"(ck.ng), [rb] "s"(rb),   \
+                   [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc),     \
+                   [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4), \
+                   [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp)                               \
+                 : ANYSEQ_LOOP2_ASM_CLOBBERS, "memory")
+template <int KIND, bool BORDER, int PUB>
 __device__ __forceinline__ uint32_t band_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                   const LoopArgs& la, int q, int& cur, int& dg, int& tf, int& best,
                                                   const CellK& ck, uint64_t& tsv, uint32_t (&npoll)[3]) {
@@ -325,30 +345,24 @@ __device__ __forceinline__ uint32_t band_loop_asm(uint32_t& b, uint32_t be, uint
     sf = RFL(sf);
     sc = RFL(sc);
     be = RFL(be);
-    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), fl = RFL(la.fl);
+    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs);
     // (readfirstlane returns int: widen through uint32_t, or bit 31 sign-extends into the high half)
     const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
 #undef RFL
     if constexpr (KIND == KIND_LOCAL) {
-        asm volatile(AQ_LOOP_L
-                     : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [best] "+v"(best), [b] "+s"(b), [sp] "+s"(sp),
-                       [sf] "+s"(sf), [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2),
-                       [x3] "=&s"(x3), [x4] "=&s"(x4) AQ_TS_OUT
-                     : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [ng] "v"(ck.ng), [rb] "s"(rb),
-                       [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc),
-                       [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4),
-                       [bvb] "v"(la.bvb), [bvs] "s"(bvs), [fl] "s"(fl), [hm] "s"(hm), [gp] "s"(gp)
-                     : ANYSEQ_LOOP_ASM_CLOBBERS, "memory");
+        if constexpr (BORDER && PUB == 0) AQ_ASM_L(AQ_NAME(L, B1, NONE));
+        if constexpr (BORDER && PUB == 1) AQ_ASM_L(AQ_NAME(L, B1, LDS));
+        if constexpr (BORDER && PUB == 2) AQ_ASM_L(AQ_NAME(L, B1, GLOB));
+        if constexpr (!BORDER && PUB == 0) AQ_ASM_L(AQ_NAME(L, B0, NONE));
+        if constexpr (!BORDER && PUB == 1) AQ_ASM_L(AQ_NAME(L, B0, LDS));
+        if constexpr (!BORDER && PUB == 2) AQ_ASM_L(AQ_NAME(L, B0, GLOB));
     } else {
-        asm volatile(AQ_LOOP_G
-                     : [cur] "+v"(cur), [dg] "+v"(dg), [tf] "+v"(tf), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf),
-                       [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3),
-                       [x4] "=&s"(x4) AQ_TS_OUT
-                     : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [rb] "s"(rb), [nb] "s"(nb),
-                       [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc), [asf] "v"(la.asf),
-                       [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4), [bvb] "v"(la.bvb),
-                       [bvs] "s"(bvs), [fl] "s"(fl), [hm] "s"(hm), [gp] "s"(gp)
-                     : ANYSEQ_LOOP_ASM_CLOBBERS, "memory");
+        if constexpr (BORDER && PUB == 0) AQ_ASM_G(AQ_NAME(G, B1, NONE));
+        if constexpr (BORDER && PUB == 1) AQ_ASM_G(AQ_NAME(G, B1, LDS));
+        if constexpr (BORDER && PUB == 2) AQ_ASM_G(AQ_NAME(G, B1, GLOB));
+        if constexpr (!BORDER && PUB == 0) AQ_ASM_G(AQ_NAME(G, B0, NONE));
+        if constexpr (!BORDER && PUB == 1) AQ_ASM_G(AQ_NAME(G, B0, LDS));
+        if constexpr (!BORDER && PUB == 2) AQ_ASM_G(AQ_NAME(G, B0, GLOB));
     }
     return st;
 }
@@ -513,8 +527,21 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
                 uint32_t bb = (uint32_t)b;
                 uint64_t tsv = 0;
                 uint32_t npoll[3] = {0, 0, 0};
-                if (band_loop_asm<KIND>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, qv[0], cur[0], dg,
-                                        top_first, best, ck, tsv, npoll)) {
+                const int role = (io.in_border ? 3 : 0) + (io.out_lds ? 1 : (io.gout ? 2 : 0));
+                uint32_t st = 0;
+#define AQ_CALL(BD, PB)                                                                                          \
+    st = band_loop_asm<KIND, BD, PB>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, qv[0], cur[0], dg,   \
+                                     top_first, best, ck, tsv, npoll)
+                switch (role) {
+                    case 0: AQ_CALL(false, 0); break;
+                    case 1: AQ_CALL(false, 1); break;
+                    case 2: AQ_CALL(false, 2); break;
+                    case 3: AQ_CALL(true, 0); break;
+                    case 4: AQ_CALL(true, 1); break;
+                    default: AQ_CALL(true, 2); break;
+                }
+#undef AQ_CALL
+                if (st) {
                     atomicOr(err, ERR_SPIN_TIMEOUT);
                     return;
                 }

@@ -144,134 +144,137 @@ def wait(e, name, seen, target, addr, count=None):
     e(f"L_{name}_ok_%=:")
 
 
-def gen_loop(kind, ts=False):
-    """The whole steady state of a band: blocks b .. be-1 (all full) in one
-    asm statement.  Per block: wait for the subject block (s_filled) and the
-    top-row chunk (prod, or write the border for band 0), read 4 x read2st64
-    subject words + 8 x b128 top values, 32 steps, then publish lane 63's chunk
-    b-2 (one ds_write_b32 from lanes 32..63) and bump cons / tail / next_prod.
-    flags: bit0 in_border, bit1 trailing (reports tail), bit2 publishes."""
+SKB_ = 142   # second subject-word set (double buffer): v142..v149
+
+
+def gen_loop2(kind, border, pub, ts=False):
+    """Steady-state loop specialised by role (no per-block flag tests):
+    border: band 0 writes the scheme's top border into its own ring;
+    pub: "lds" (next band of the group), "glob" (the group's last band: the
+    next group's row buffer or out_row, plus the tail counter) or "none" (last
+    band of the problem without an output row; reports tail).
+    The subject words of block b+1 are prefetched during block b into the other
+    of two register sets (the body is unrolled twice)."""
     L = kind == "L"
+    trailing = pub != "lds"
     out = []
     e = out.append
-    e("L_top_%=:")
-    e("s_lshl_b32 %[x0], %[b], 5")              # tb
-    e("s_add_u32 %[x1], %[b], 1")               # b + 1
-    wait(e, "sf", "%[sf]", "%[x1]", "%[asf]", "%[nsf]" if ts else None)
-    # subject words of block b: skew[(b & 31)][i][lane]
+    sets = (SK0, SKB_)
+
+    def body(k):
+        cs, ns = sets[k], sets[1 - k]
+        e("s_add_u32 %[x1], %[b], 1")
+        # prefetch the next block's subject words
+        e("s_cmp_ge_u32 %[x1], %[be]")
+        e(f"s_cbranch_scc1 L_nopf{k}_%=")
+        e("s_add_u32 %[x4], %[b], 2")
+        wait(e, f"sf{k}", "%[sf]", "%[x4]", "%[asf]", "%[nsf]" if ts else None)
+        e("s_and_b32 %[x2], %[x1], 31")
+        e("s_lshl_b32 %[x2], %[x2], 11")
+        e(f"v_add_u32_e32 v{VA}, %[x2], %[skb]")
+        for i in range(4):
+            e(f"ds_read2st64_b32 v[{ns + 2 * i}:{ns + 2 * i + 1}], v{VA} offset0:{2 * i} offset1:{2 * i + 1}")
+        e(f"L_nopf{k}_%=:")
+        # top row of block b
+        if border:
+            e("s_lshl_b32 %[x0], %[b], 5")
+            e("s_mul_i32 %[x2], %[x0], %[bvs]")
+            e(f"v_add_u32_e32 v{VT}, %[x2], %[bvb]")
+            e("s_lshl_b32 %[x2], %[x0], 2")
+            e(f"v_add_u32_e32 v{VT2}, %[x2], %[lid4]")
+            e(f"v_and_b32_e32 v{VT2}, 0x7ff, v{VT2}")
+            e(f"v_add_u32_e32 v{VT2}, %[rb], v{VT2}")
+            e(f"ds_write_b32 v{VT2}, v{VT}")
+        else:
+            wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", "%[npr]" if ts else None)
+        if ts:
+            e("s_cmp_lg_u32 %[b], 0")
+            e(f"s_cbranch_scc1 L_nots{k}_%=")
+            e("s_memrealtime %[ts]")
+            e("s_waitcnt lgkmcnt(0)")
+            e(f"L_nots{k}_%=:")
+        if pub == "lds":
+            # chunk b-2 goes to slot (b-2) & 15: free once the consumer is at >= b-17
+            e("s_cmp_lt_u32 %[b], 17")
+            e(f"s_cbranch_scc1 L_nobp{k}_%=")
+            e("s_sub_u32 %[x4], %[b], 17")
+            wait(e, f"bp{k}", "%[sc]", "%[x4]", "%[anc]", "%[nbp]" if ts else None)
+            e(f"L_nobp{k}_%=:")
+        e("s_lshl_b32 %[x2], %[b], 7")
+        e("s_and_b32 %[x2], %[x2], 2047")
+        e("s_add_u32 %[x2], %[x2], %[rb]")
+        e(f"v_mov_b32_e32 v{VB}, %[x2]")
+        for i in range(8):
+            e(f"ds_read_b128 v[{T0 + 4 * i}:{T0 + 4 * i + 3}], v{VB} offset:{16 * i}")
+        cur, dg = "%[cur]", "%[dg]"
+        for u in range(32):
+            c = u // 8
+            if u % 8 == 0:
+                r = (8 * c + 6) // 4
+                e(f"s_waitcnt lgkmcnt({7 - r})")
+            sw = v(cs + u // 4)
+            tv = "%[tf]" if u == 0 else v(T0 + u - 1)
+            ov = v(O0 + u)
+            e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+            e(f"v_cndmask_b32_e32 v{W}, %[wx], %[wm], vcc")
+            e(f"v_add_u32_e32 v{A}, {dg}, v{W}")
+            e(f"v_mov_b32_dpp {tv}, {cur} wave_shr:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_max3_i32 {ov}, v{A}, {cur}, {tv}")
+            if L:
+                e(f"v_sub_u32_e64 {ov}, {ov}, %[ng] clamp")
+                e(f"v_max_i32_e32 %[best], %[best], {ov}")
+            if u >= 2 and pub != "none":
+                e(f"v_mov_b32_dpp {v(O0 + u - 1)}, {v(O0 + u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            cur, dg = ov, tv
+        e(f"v_mov_b32_e32 %[cur], v{O0 + 31}")
+        e(f"v_mov_b32_e32 %[dg], v{T0 + 30}")
+        if pub != "none":
+            e(f"v_mov_b32_dpp {v(O0 + 31)}, {v(O0 + 30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+        e(f"v_mov_b32_e32 %[tf], v{T0 + 31}")
+        if pub != "none":
+            e("s_cmp_lt_u32 %[b], 2")
+            e(f"s_cbranch_scc1 L_nopub{k}_%=")
+            e("s_sub_u32 %[x2], %[b], 2")
+            e("s_lshl_b32 %[x2], %[x2], 7")
+            if pub == "lds":
+                e("s_and_b32 %[x2], %[x2], 2047")
+                e("s_add_u32 %[x2], %[x2], %[nb]")
+            e(f"v_add_u32_e32 v{VT}, %[x2], %[lo]")
+            e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
+            e("s_mov_b64 exec, %[hm]")
+            if pub == "lds":
+                e(f"ds_write_b32 v{VT}, v{O0 + 31}")
+            else:
+                e(f"global_store_dword v{VT}, v{O0 + 31}, %[gp] sc1")
+            e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
+            if pub == "lds":
+                e("s_sub_u32 %[x2], %[b], 1")
+                e(f"v_mov_b32_e32 v{VT2}, %[x2]")
+                e(f"ds_write_b32 %[anp], v{VT2}")
+            e(f"L_nopub{k}_%=:")
+        e(f"v_mov_b32_e32 v{VT2}, %[x1]")
+        if not border:
+            e(f"ds_write_b32 %[acn], v{VT2}")
+        if trailing:
+            e(f"ds_write_b32 %[atl], v{VT2}")
+        e("s_mov_b32 %[b], %[x1]")
+
+    # prologue: the first block's subject words into set 0
+    e("s_add_u32 %[x1], %[b], 1")
+    wait(e, "sfp", "%[sf]", "%[x1]", "%[asf]", "%[nsf]" if ts else None)
     e("s_and_b32 %[x2], %[b], 31")
     e("s_lshl_b32 %[x2], %[x2], 11")
     e(f"v_add_u32_e32 v{VA}, %[x2], %[skb]")
     for i in range(4):
         e(f"ds_read2st64_b32 v[{SK0 + 2 * i}:{SK0 + 2 * i + 1}], v{VA} offset0:{2 * i} offset1:{2 * i + 1}")
-    # top row: band 0 writes the scheme's border, others wait for the producer
-    e("s_bitcmp1_b32 %[fl], 0")
-    e("s_cbranch_scc0 L_notborder_%=")
-    e("s_mul_i32 %[x2], %[x0], %[bvs]")
-    e(f"v_add_u32_e32 v{VT}, %[x2], %[bvb]")
-    e("s_lshl_b32 %[x2], %[x0], 2")
-    e(f"v_add_u32_e32 v{VT2}, %[x2], %[lid4]")
-    e(f"v_and_b32_e32 v{VT2}, 0x7ff, v{VT2}")
-    e(f"v_add_u32_e32 v{VT2}, %[rb], v{VT2}")
-    e(f"ds_write_b32 v{VT2}, v{VT}")
-    e("s_branch L_havetop_%=")
-    e("L_notborder_%=:")
-    wait(e, "pr", "%[sp]", "%[x1]", "%[apr]", "%[npr]" if ts else None)
-    e("L_havetop_%=:")
-    if ts:
-        # diagnostic builds: s_memrealtime when block 0's inputs are ready (-> %[ts])
-        e("s_cmp_lg_u32 %[b], 0")
-        e("s_cbranch_scc1 L_nots_%=")
-        e("s_memrealtime %[ts]")
-        e("s_waitcnt lgkmcnt(0)")
-        e("L_nots_%=:")
-    # back-pressure: chunk b-2 goes to slot (b-2) & 15, free once the consumer is at >= b-17
-    e("s_bitcmp1_b32 %[fl], 2")
-    e("s_cbranch_scc0 L_nobp_%=")
-    e("s_cmp_lt_u32 %[b], 17")
-    e("s_cbranch_scc1 L_nobp_%=")
-    e("s_sub_u32 %[x4], %[b], 17")
-    wait(e, "bp", "%[sc]", "%[x4]", "%[anc]", "%[nbp]" if ts else None)
-    e("L_nobp_%=:")
-    # the 32 top values of chunk b
-    e("s_and_b32 %[x2], %[x0], 511")
-    e("s_lshl_b32 %[x2], %[x2], 2")
-    e("s_add_u32 %[x2], %[x2], %[rb]")
-    e(f"v_mov_b32_e32 v{VB}, %[x2]")
-    for i in range(8):
-        e(f"ds_read_b128 v[{T0 + 4 * i}:{T0 + 4 * i + 3}], v{VB} offset:{16 * i}")
-    # ops in flight: 4 subject reads, then 8 top reads
-    cur = "%[cur]"
-    dg = "%[dg]"
-    for u in range(32):
-        c = u // 8
-        if u % 8 == 0:
-            r = (8 * c + 6) // 4          # last top read chunk c needs
-            e(f"s_waitcnt lgkmcnt({7 - r})")
-        sw = v(SK0 + u // 4)
-        b = u % 4
-        tv = "%[tf]" if u == 0 else v(T0 + u - 1)
-        ov = v(O0 + u)
-        e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{b}")
-        e(f"v_cndmask_b32_e32 v{W}, %[wx], %[wm], vcc")
-        e(f"v_add_u32_e32 v{A}, {dg}, v{W}")
-        e(f"v_mov_b32_dpp {tv}, {cur} wave_shr:1 row_mask:0xf bank_mask:0xf")
-        e(f"v_max3_i32 {ov}, v{A}, {cur}, {tv}")
-        if L:
-            e(f"v_sub_u32_e64 {ov}, {ov}, %[ng] clamp")
-            e(f"v_max_i32_e32 %[best], %[best], {ov}")
-        if u >= 2:
-            e(f"v_mov_b32_dpp {v(O0 + u - 1)}, {v(O0 + u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-        cur = ov
-        dg = tv
-    e(f"v_mov_b32_e32 %[cur], v{O0 + 31}")
-    e(f"v_mov_b32_e32 %[dg], v{T0 + 30}")
-    e(f"v_mov_b32_dpp {v(O0 + 31)}, {v(O0 + 30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-    e(f"v_mov_b32_e32 %[tf], v{T0 + 31}")
-    # publish chunk j = b - 2 (lanes 32..63 of O31 hold it in column order)
-    e("s_bitcmp1_b32 %[fl], 2")
-    e("s_cbranch_scc0 L_nopub_%=")
-    e("s_cmp_lt_u32 %[b], 2")
-    e("s_cbranch_scc1 L_nopub_%=")
-    e("s_sub_u32 %[x2], %[b], 2")
-    e("s_lshl_b32 %[x2], %[x2], 7")
-    e("s_and_b32 %[x2], %[x2], 2047")
-    e("s_add_u32 %[x2], %[x2], %[nb]")
-    e(f"v_add_u32_e32 v{VT}, %[x2], %[lo]")
-    e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
-    e("s_mov_b64 exec, %[hm]")
-    e(f"ds_write_b32 v{VT}, v{O0 + 31}")
-    e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
-    e("s_sub_u32 %[x2], %[b], 1")
-    e(f"v_mov_b32_e32 v{VT2}, %[x2]")
-    e(f"ds_write_b32 %[anp], v{VT2}")
-    e("L_nopub_%=:")
-    # the group's last band: chunk j = b - 2 straight to global memory (sc1, lanes 32..63)
-    e("s_bitcmp1_b32 %[fl], 3")
-    e("s_cbranch_scc0 L_nogpub_%=")
-    e("s_cmp_lt_u32 %[b], 2")
-    e("s_cbranch_scc1 L_nogpub_%=")
-    e("s_sub_u32 %[x2], %[b], 2")
-    e("s_lshl_b32 %[x2], %[x2], 7")
-    e(f"v_add_u32_e32 v{VT}, %[x2], %[lo]")
-    e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
-    e("s_mov_b64 exec, %[hm]")
-    e(f"global_store_dword v{VT}, v{O0 + 31}, %[gp] sc1")
-    e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
-    e("L_nogpub_%=:")
-    # release the in-ring slot / report the trailing wave's progress
-    e(f"v_mov_b32_e32 v{VT2}, %[x1]")
-    e("s_bitcmp1_b32 %[fl], 0")
-    e("s_cbranch_scc1 L_nocons_%=")
-    e(f"ds_write_b32 %[acn], v{VT2}")
-    e("L_nocons_%=:")
-    e("s_bitcmp1_b32 %[fl], 1")
-    e("s_cbranch_scc0 L_notail_%=")
-    e(f"ds_write_b32 %[atl], v{VT2}")
-    e("L_notail_%=:")
-    e("s_mov_b32 %[b], %[x1]")
+    e("L_top_%=:")
+    body(0)
+    e("s_cmp_lt_u32 %[b], %[be]")
+    e("s_cbranch_scc0 L_done_%=")
+    body(1)
     e("s_cmp_lt_u32 %[b], %[be]")
     e("s_cbranch_scc1 L_top_%=")
+    e("L_done_%=:")
     e("s_mov_b32 %[st], 0")
     e("s_branch L_end_%=")
     e("L_timeout_%=:")
@@ -297,16 +300,21 @@ def main():
         for ln in body:
             lines.append(f'    "{ln}\\n" \\')
         lines.append("")
-    for name, kind, ts in (("G", "G", False), ("L", "L", False), ("G_TS", "G", True), ("L_TS", "L", True)):
-        lines.append(f"#define ANYSEQ_LOOP_ASM_{name} \\")
-        for ln in gen_loop(kind, ts):
-            lines.append(f'    "{ln}\\n" \\')
-        lines.append("")
+    for kind in ("G", "L"):
+        for border in (0, 1):
+            for pub in ("none", "lds", "glob"):
+                for ts in (False, True):
+                    name = f"ANYSEQ_LOOP2_{kind}_B{border}_{pub.upper()}" + ("_TS" if ts else "")
+                    lines.append(f"#define {name} \\")
+                    for ln in gen_loop2(kind, border, pub, ts):
+                        lines.append(f'    "{ln}\\n" \\')
+                    lines.append("")
     clob = ", ".join(f'"v{n}"' for n in range(T0, A + 1))
     lines.append(f"#define ANYSEQ_BLOCK_ASM_CLOBBERS {clob}, \"vcc\"")
-    clob = ", ".join(f'"v{n}"' for n in range(T0, VB + 1))
+    clob = ", ".join(f'"v{n}"' for n in range(T0, SKB_ + 8))
     sclob = ", ".join(f'"s{n}"' for n in range(TA, TB + 2))
-    lines.append(f"#define ANYSEQ_LOOP_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
+    lines.append(f"#define ANYSEQ_LOOP2_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
+
     lines.append("")
     with open(dst, "w") as f:
         f.write("\n".join(lines))
