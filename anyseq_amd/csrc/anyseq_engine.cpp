@@ -23,6 +23,11 @@ using namespace anyseq;
 extern "C" {
 hipError_t anyseq_launch_fill(int R, int CH, int NW, const DPProblem* probs, const GroupRef* groups, int ngroups,
                               uint32_t* dq, uint32_t* err, const FillParams* fp, int grid, hipStream_t st);
+hipError_t anyseq_launch_fill_affine(int NW, const DPProblem* probs, const GroupRef* groups, int ngroups,
+                                     uint32_t* dq, uint32_t* err, const FillParams* fp, int grid, hipStream_t st);
+hipError_t anyseq_launch_aff_reduce(int kind, int two, const void* rowF, int h1, const void* rowB, int h2, int m,
+                                    int go, int ge, const int32_t* colF, const int32_t* colB, int32_t* out,
+                                    hipStream_t st);
 hipError_t anyseq_launch_semiglobal_reduce(const int32_t* row_g, int m, const int32_t* col_h, int n, int ng,
                                            int32_t* out, hipStream_t st);
 hipError_t anyseq_launch_front_combine(int kind, const int32_t* rowF, int h1, const int32_t* rowB, int h2, int m,
@@ -94,6 +99,9 @@ struct Tuning {
     int NW = 4;
     int grid = 0;
     int fronts = 2;
+    int NWa = 4;    // affine fill: compute waves per workgroup (3 or 4)
+    int grida = 0;  // affine fill: persistent grid (0 = one workgroup per CU)
+    int affasm = 1; // affine fill: asm steady state (0 = C++ blocks only, diagnostics)
 };
 
 struct Engine {
@@ -151,14 +159,17 @@ int waves_per_group() {
 // ---------------------------------------------------------------- fill --
 // Runs one batched fill launch over `probs` (host copies; device pointers set).
 void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st) {
-    const int R = rows_per_lane(), NW = waves_per_group();
+    const bool aff = fp.affine != 0;
+    // the affine fill has one row per lane and hands (G, F) pairs over (twice the row bytes)
+    const int R = aff ? 1 : rows_per_lane(), NW = aff ? (g_tuning.NWa == 3 ? 3 : 4) : waves_per_group();
+    const int vpc = aff ? 2 : 1;
     size_t rowbuf_ints = 0, flag_words = 0;
     int max_groups = 0;
     for (auto& P : probs) {
         P.nbands = (P.h + 64 * R - 1) / (64 * R);
         P.ngroups = (P.nbands + NW - 1) / NW;
         P.wpad = (P.w + 63) & ~63;
-        rowbuf_ints += (size_t)std::max(P.ngroups - 1, 0) * P.wpad;
+        rowbuf_ints += (size_t)std::max(P.ngroups - 1, 0) * P.wpad * vpc;
         flag_words += P.ngroups;
         max_groups = std::max(max_groups, P.ngroups);
     }
@@ -168,7 +179,7 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     for (auto& P : probs) {
         P.rowbuf = rowbuf + ro;
         P.flags = flags + fo;
-        ro += (size_t)std::max(P.ngroups - 1, 0) * P.wpad;
+        ro += (size_t)std::max(P.ngroups - 1, 0) * P.wpad * vpc;
         fo += P.ngroups;
     }
     // group table: round-robin over problems so every sub-problem progresses
@@ -182,11 +193,12 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     HIPCHECK(hipMemcpyAsync(d_probs, probs.data(), probs.size() * sizeof(DPProblem), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(d_groups, groups.data(), groups.size() * sizeof(GroupRef), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemsetAsync(flags, 0, flag_words * 4, st));
-    // group -> group hand-off rows start as the sentinel -1 (the consumer polls the data)
-    if (rowbuf_ints) HIPCHECK(hipMemsetAsync(rowbuf, 0xff, rowbuf_ints * 4, st));
+    // group -> group hand-off rows start as a sentinel (the consumer polls the data):
+    // -1 for linear, 0x80808080 for affine
+    if (rowbuf_ints) HIPCHECK(hipMemsetAsync(rowbuf, aff ? 0x80 : 0xff, rowbuf_ints * 4, st));
     uint32_t* ctr = (uint32_t*)E.ctr.get(128);
     HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));  // ctr[0] = dequeue counter, ctr[1] = error word
-    int grid = g_tuning.grid > 0 ? g_tuning.grid : E.num_cus;
+    int grid = aff ? (g_tuning.grida > 0 ? g_tuning.grida : E.num_cus) : (g_tuning.grid > 0 ? g_tuning.grid : E.num_cus);
     grid = std::min<int>(grid, (int)groups.size());
     FillParams fpl = fp;
     unsigned long long* dbg = nullptr;
@@ -197,8 +209,11 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
         fpl.dbg = dbg;
     }
     HIPCHECK(hipEventRecord(E.ev0, st));
-    HIPCHECK(anyseq_launch_fill(R, g_tuning.CH, NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fpl, grid,
-                                st));
+    if (aff)
+        HIPCHECK(anyseq_launch_fill_affine(NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fpl, grid, st));
+    else
+        HIPCHECK(anyseq_launch_fill(R, g_tuning.CH, NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fpl,
+                                    grid, st));
     HIPCHECK(hipEventRecord(E.ev1, st));
     HIPCHECK(hipEventSynchronize(E.ev1));
     float ms = 0.f;
@@ -246,6 +261,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.gap_extend = sc.gap_extend;
     fp.affine = sc.gap_open != 0;
     fp.dbg = nullptr;
+    fp.pad = (g_tuning.affasm & 1) ? (g_tuning.affasm & 2) : (1 | (g_tuning.affasm & 2));  // affine_asm bit0: asm steady state, bit1: scalar row stores (diagnostics)
     return fp;
 }
 
@@ -253,12 +269,19 @@ void check_scoring(int kind, const anyseq_scoring& sc) {
     if (kind < 0 || kind > 2) fail("invalid alignment kind %d", kind);
     if (sc.gap_extend >= 0) fail("gap_extend must be negative (got %d)", sc.gap_extend);
     if (sc.gap_open > 0) fail("gap_open must be <= 0 (got %d)", sc.gap_open);
-    if (sc.gap_open != 0) fail("affine gaps are not available in this build yet");
+    // |scores| stay far from the kernels' -2^29 "minus infinity" and int32 range
+    const long long mx = std::max({std::llabs(sc.match), std::llabs(sc.mismatch), std::llabs(sc.gap_open),
+                                   std::llabs(sc.gap_extend)});
+    if (mx > 1024) fail("scoring parameters must be within [-1024, 1024]");
 }
 
 // Score of an empty matrix (reference semantics with benchmark restored).
 int64_t empty_score(int kind, int n, int m, const anyseq_scoring& sc) {
-    if (kind == KIND_GLOBAL) return (int64_t)(n > 0 ? n : m) * sc.gap_extend;  // init(n-1) or init(m-1)
+    if (kind == KIND_GLOBAL) {
+        const int len = n > 0 ? n : m;
+        if (len <= 0) return 0;
+        return (int64_t)sc.gap_open + (int64_t)len * sc.gap_extend;  // init(n-1) or init(m-1)
+    }
     if (kind == KIND_SEMIGLOBAL) return 0;
     return SCORE_MIN_VALUE;  // local: no slot is ever written
 }
@@ -267,9 +290,13 @@ int64_t empty_score(int kind, int n, int m, const anyseq_scoring& sc) {
 // Matrices with enough rows run as two fronts (top half forward, bottom half on
 // reversed sequences) in ONE launch and are combined by a row split
 // (front_combine_kernel): the pipeline depth of the band wavefront halves.
+int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds,
+                         int m, hipStream_t st);
+
 int64_t score_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds, int m,
                   hipStream_t st) {
     if (n <= 0 || m <= 0) return empty_score(kind, n, m, sc);
+    if (sc.gap_open != 0) return score_dev_affine(E, kind, sc, dq, n, ds, m, st);
     const FillParams fp = make_params(kind, sc);
     const int wpad = (m + 63) & ~63;
     int32_t* res = (int32_t*)E.ctr.get(128) + 4;
@@ -326,6 +353,57 @@ int64_t score_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* 
                                          cols ? cols + h1 : nullptr, res, st));
     int32_t v = 0;
     HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    return v;
+}
+
+// Affine (Gotoh) score: the same one- or two-front scheme as score_dev over
+// fill_affine_kernel; rows are (G, F) pairs, so the combine also joins a vertical
+// gap that crosses the split row (aff_reduce_kernel).
+int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds,
+                         int m, hipStream_t st) {
+    const FillParams fp = make_params(kind, sc);
+    const int wpad = (m + 63) & ~63;
+    const int NW = g_tuning.NWa == 3 ? 3 : 4;
+    int32_t* res = (int32_t*)E.ctr.get(128) + 4;
+    HIPCHECK(hipMemsetAsync(res, kind == KIND_LOCAL ? 0 : 0x80, 4, st));
+    const bool two = g_tuning.fronts > 1 && n >= 2 * 64 * NW;
+    std::vector<DPProblem> probs;
+    DPProblem P;
+    memset(&P, 0, sizeof P);
+    P.q = dq;
+    P.s = ds;
+    P.q_step = 1;
+    P.s_step = 1;
+    P.w = m;
+    const int h1 = two ? n / 2 : n, h2 = n - h1;
+    int32_t* rows = (int32_t*)E.outrow.get((size_t)2 * 2 * wpad * 4);
+    int32_t* cols = kind != KIND_LOCAL ? (int32_t*)E.outcol.get((size_t)n * 4) : nullptr;
+    P.h = h1;
+    P.out_row = (kind != KIND_GLOBAL || two) ? rows : nullptr;
+    P.out_col = cols;
+    if (kind == KIND_LOCAL) P.best = res;
+    probs.push_back(P);
+    if (two) {
+        P.q_off = n - 1;
+        P.q_step = -1;
+        P.s_off = m - 1;
+        P.s_step = -1;
+        P.h = h2;
+        P.out_row = rows + 2 * wpad;
+        P.out_col = cols ? cols + h1 : nullptr;
+        probs.push_back(P);
+    }
+    run_fill(E, probs, fp, st);
+    int32_t v = 0;
+    if (!two && kind == KIND_GLOBAL) {
+        HIPCHECK(hipMemcpyAsync(&v, cols + (n - 1), 4, hipMemcpyDeviceToHost, st));
+    } else {
+        if (two || kind == KIND_SEMIGLOBAL)
+            HIPCHECK(anyseq_launch_aff_reduce(kind, two ? 1 : 0, rows, h1, rows + 2 * wpad, h2, m, sc.gap_open,
+                                              sc.gap_extend, cols, cols ? cols + h1 : nullptr, res, st));
+        HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, st));
+    }
     HIPCHECK(hipStreamSynchronize(st));
     return v;
 }
@@ -616,6 +694,9 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "waves_per_group") g_tuning.NW = value;
     else if (n == "grid") g_tuning.grid = value;
     else if (n == "fronts") g_tuning.fronts = value;
+    else if (n == "affine_waves_per_group") g_tuning.NWa = value;
+    else if (n == "affine_grid") g_tuning.grida = value;
+    else if (n == "affine_asm") g_tuning.affasm = value;
     else return -1;
     return 0;
 }

@@ -33,7 +33,7 @@ struct DPProblem {
     int32_t* rowbuf;       // (ngroups-1) * wpad ints: group -> group hand-off rows
     uint32_t* flags;       // ngroups entries, chunk progress of each group's last band
     int32_t* best;         // optional (local): atomicMax of every cell
-    int32_t* pad1;
+    int32_t* out_col_e;    // optional (affine): E[r][w-1] (H space) for r in [0,h)
 };
 
 struct GroupRef {
@@ -46,7 +46,7 @@ struct FillParams {
     int32_t match, mismatch, gap;     // linear (gap < 0)
     int32_t gap_open, gap_extend;     // affine (gap_open <= 0, gap_extend < 0)
     int32_t affine;
-    int32_t pad;
+    int32_t pad;                      // affine: bit 0 = C++ steady state only (diagnostics)
     unsigned long long* dbg;          // diagnostic build only (ANYSEQ_STAMPS): per-launch stamp sums
 };
 

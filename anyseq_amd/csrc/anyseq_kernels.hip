@@ -655,9 +655,37 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
 //  * copies this group's bottom row from the out-ring to HBM (sc1 stores,
 //    vmcnt(0), then the flag).
 // The HBM hand-off latency therefore never sits on a compute wave's critical path.
-template <int CH, bool SKEW>
+// Hand-off element: the linear fill passes one int per column (G or H), the affine
+// fill an int2 (G, F-down).  Rows waiting for data hold a sentinel no kernel value
+// takes: -1 for linear (G >= 0, local H >= 0), 0x80808080 in .x for affine.
+template <typename T>
+struct HandOff;
+template <>
+struct HandOff<int32_t> {
+    __device__ static int32_t load(const int32_t* p) {
+        return __hip_atomic_load(gmem(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static bool pending(int32_t v) { return v == -1; }
+    __device__ static int32_t zero() { return 0; }
+};
+template <>
+struct HandOff<int2> {
+    __device__ static int2 load(const int2* p) {
+        const uint64_t u = __hip_atomic_load(gmem(reinterpret_cast<const uint64_t*>(p)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        return make_int2((int)(uint32_t)u, (int)(uint32_t)(u >> 32));
+    }
+    __device__ static void store(int2* p, int2 v) {
+        const uint64_t u = (uint64_t)(uint32_t)v.x | ((uint64_t)(uint32_t)v.y << 32);
+        __hip_atomic_store(gmem(reinterpret_cast<uint64_t*>(p)), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static bool pending(int2 v) { return v.x == (int)0x80808080; }
+    __device__ static int2 zero() { return make_int2(0, 0); }
+};
+
+template <int CH, bool SKEW, typename T = int32_t>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
-                        uint32_t* s_filled, uint32_t* tail, const int32_t* g_in, int32_t* ring0, uint32_t* prod0,
+                        uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
                         uint32_t* cons0, uint32_t* err) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
@@ -724,21 +752,19 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             const int lim = min((int)lds_ld(cons0) + kSlots, nchunks);
             if (lim > in_next) {
                 constexpr int PER = kSlots * CH / 64;   // 2 chunks per load row
-                int v[PER];
+                T v[PER];
                 const int c0 = in_next * CH, c1 = lim * CH;
 #pragma unroll
                 for (int i = 0; i < PER; ++i) {
                     const int col = c0 + i * 64 + lane;
-                    v[i] = col < c1 && col < w
-                               ? __hip_atomic_load(gmem(g_in) + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : 0;
+                    v[i] = col < c1 && col < w ? HandOff<T>::load(g_in + col) : HandOff<T>::zero();
                 }
                 // leading run of complete chunks
                 int ready = 0;
                 bool stop = false;
 #pragma unroll
                 for (int i = 0; i < PER; ++i) {
-                    const uint64_t bad = __ballot(v[i] == -1);
+                    const uint64_t bad = __ballot(HandOff<T>::pending(v[i]));
                     if (!stop && in_next + 2 * i < lim && (uint32_t)bad == 0u) ++ready; else stop = true;
                     if (!stop && in_next + 2 * i + 1 < lim && (uint32_t)(bad >> 32) == 0u) ++ready; else stop = true;
                 }
@@ -850,6 +876,452 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
         }
         __syncthreads();
     }
+}
+
+// ------------------------------------------------------------- affine fill --
+// Gotoh (build-defined: affine_scoring_scheme, align.impala:153-166, is dead in the
+// reference; semantics = oracle_affine_score in oracle/anyseq_oracle.c):
+//   E[r][c] = max(E[r][c-1] + ge, H[r][c-1] + go + ge)   (horizontal, left)
+//   F[r][c] = max(F[r-1][c] + ge, H[r-1][c] + go + ge)   (vertical, up)
+//   H[r][c] = max(H[r-1][c-1] + sub, E, F)               (local: max(., 0))
+// All kinds run in G-space, X_G = X - (r+c+2)*ge for X in {H,E,F}: every gap
+// extension is free there, so
+//   E_G = max(E_G, G_left + go),  F_G = max(F_G, G_up + go),
+//   G   = max3(G_diag + sub - 2 ge, E_G, F_G),
+// and local's clamp H >= 0 becomes G >= Z_t = (r+c+2)(-ge), which is the SAME for
+// every lane of a step (r + c = rb + t - 1 on the anti-diagonal): one v_max with a
+// wave-uniform bound.  Same geometry as fill_kernel (R = 1, X = 0, CH = 32): lane l
+// owns row rb + l of a 64-row band and processes column t - 1 - l at step t.  From
+// the lane above it receives, by DPP wave_shr:1, G[r-1][c] (the next step's
+// diagonal) and F[r][c] ("F-down" of the row above); lane 0 reads both from the
+// band's input ring (int2 per column).  G + go is computed once per cell and
+// serves both the F-down of this cell and the E of the next column.
+constexpr int kAffNeg = -(1 << 29);   // "minus infinity" of the E/F states (the oracle's AFF_NEG_INF)
+
+struct AffK {
+    int wm, wx;   // diagonal weight sub - 2 ge
+    int go;       // gap open (<= 0): added to a cell to open a gap (G space)
+    int nge;      // -ge > 0
+    int flags;    // bit 0: no asm steady state (diagnostics)
+};
+
+// Border cell G[-1][i] / G[i][-1], i >= -1 (G space).
+template <int KIND>
+__device__ __forceinline__ int aff_border(int i, int go, int nge) {
+    if (KIND == KIND_GLOBAL) return i < 0 ? 0 : go;
+    return (i + 1) * nge;   // semiglobal / local: H border 0
+}
+__device__ __forceinline__ int aff_to_h(int v, int r, int c, int nge) { return v - (r + c + 2) * nge; }
+
+template <int NW>
+struct AffShared {
+    int2 in_ring[NW + 1][kSlots * 32];
+    uint8_t s_ring[kSRing + 64];
+    uint32_t prod[NW + 1];
+    uint32_t cons[NW + 1];
+    uint32_t skew[kSkewBlocks][8][64];   // pre-skewed subject, as FillShared::skew
+    uint32_t s_filled;
+    uint32_t tail;
+    int32_t group;
+};
+
+struct AffIO {
+    bool in_border, trailing, out_lds;
+    int2* my_ring;
+    uint32_t* my_prod;
+    uint32_t* my_cons;
+    int2* next_ring;
+    uint32_t* next_prod;
+    uint32_t* next_cons;
+    const uint8_t* s_ring;
+    const uint32_t* skew;
+    uint32_t* s_filled;
+    uint32_t* tail;
+    int2* gout;   // last band of a group: HBM destination of the bottom row (G, F)
+};
+
+// 32 steps in C++ (prologue / epilogue / partial bands; the steady state is the asm
+// loop below).  c0 = this lane's column at the first step, tf = top row at column
+// t0 - 1, rv[u] = top row at column t0 + u, z = local clamp bound of the first step.
+// MASK: some lanes are outside [0, w).  PARTIAL: rows >= h pass the row above
+// through.  FINOUT: the problem's last row publishes F[h-1][c] (not F-down), as
+// the two-front combine needs.  og/of: this lane's (G, F-out) after each step
+// (lane 63's are the band's bottom row).
+template <int KIND, bool MASK, bool PARTIAL, bool FINOUT, bool VIRT>
+__device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&rv)[32], const uint32_t (&sw)[8], int q,
+                                          bool dead, bool lastrow, int z, int& g, int& e, int& hg, int& fdn, int& dg,
+                                          int& best, int (&og)[32], int (&of)[32], const AffK k) {
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+        const int2 top = u == 0 ? tf : rv[u - 1];
+        const int upg = wave_shr1(top.x, g);
+        const int fin = wave_shr1(top.y, fdn);
+        const int sb = (int)((sw[u >> 2] >> (8 * (u & 3))) & 0xffu);
+        const int wgt = q == sb ? k.wm : k.wx;
+        const int en = max(e, hg);
+        int v = max(max(dg + wgt, en), fin);
+        if (KIND == KIND_LOCAL) v = max(v, z + u * k.nge);
+        const int hn = v + k.go;
+        int fn = max(fin, hn);
+        if (PARTIAL && dead) {
+            v = upg;
+            fn = fin;
+        }
+        if (FINOUT && lastrow) fn = fin;
+        // VIRT: columns < 0 are virtual and computed like real ones
+        const bool act = MASK ? (VIRT ? (c0 + u < w) : ((unsigned)(c0 + u) < (unsigned)w)) : true;
+        // branch-free masking: inactive lanes keep their state
+        e = act ? en : e;
+        g = act ? v : g;
+        hg = act ? hn : hg;
+        fdn = act ? fn : fdn;
+        if (KIND == KIND_LOCAL) best = act ? max(best, v - (z + u * k.nge)) : best;
+        dg = upg;
+        og[u] = g;
+        of[u] = fdn;
+    }
+}
+
+// Steady-state blocks b .. be-1 of a band (tools/gen_block_asm.py, gen_loop_aff),
+// specialised by role like band_loop_asm.  Returns 0, or 1 on a spin timeout.
+struct AffLoopArgs {
+    uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs;
+    uint64_t gp;
+};
+#define AFF_ASM(NAME)                                                                                           \
+    asm volatile(NAME                                                                                          \
+                 : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
+                   [hg] "+v"(hg), [best] "+v"(best), [z] "+s"(z), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf),      \
+                   [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3), \
+                   [x4] "=&s"(x4)                                                                              \
+                 : [be] "s"(be), [q] "v"(q), [wm] "v"(k.wm), [wx] "v"(k.wx), [go] "v"(k.go), [nge] "s"(nge),     \
+                   [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp),          \
+                   [anc] "v"(la.anc), [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo),  \
+                   [lid8] "v"(la.lid8), [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp)            \
+                 : ANYSEQ_AFF_ASM_CLOBBERS, "memory")
+template <int KIND, bool BORDER, int PUB>
+__device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
+                                                 const AffLoopArgs& la, int q, int& g, int& fdn, int& dg, int2& tf,
+                                                 int& e, int& hg, int& best, uint32_t& z, const AffK& k) {
+    uint32_t st, x0, x1, x2, x3, x4;
+    const uint64_t hm = 0xffffffff00000000ull;
+#define RFL(x) __builtin_amdgcn_readfirstlane(x)
+    b = RFL(b);
+    sp = RFL(sp);
+    sf = RFL(sf);
+    sc = RFL(sc);
+    be = RFL(be);
+    z = RFL(z);
+    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), nge = RFL(k.nge);
+    const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
+#undef RFL
+    int tfg = tf.x, tff = tf.y;
+    if constexpr (KIND == KIND_LOCAL) {
+        if constexpr (BORDER && PUB == 0) AFF_ASM(ANYSEQ_AFF_L_B1_NONE);
+        if constexpr (BORDER && PUB == 1) AFF_ASM(ANYSEQ_AFF_L_B1_LDS);
+        if constexpr (BORDER && PUB == 2) AFF_ASM(ANYSEQ_AFF_L_B1_GLOB);
+        if constexpr (!BORDER && PUB == 0) AFF_ASM(ANYSEQ_AFF_L_B0_NONE);
+        if constexpr (!BORDER && PUB == 1) AFF_ASM(ANYSEQ_AFF_L_B0_LDS);
+        if constexpr (!BORDER && PUB == 2) AFF_ASM(ANYSEQ_AFF_L_B0_GLOB);
+    } else {
+        if constexpr (BORDER && PUB == 0) AFF_ASM(ANYSEQ_AFF_G_B1_NONE);
+        if constexpr (BORDER && PUB == 1) AFF_ASM(ANYSEQ_AFF_G_B1_LDS);
+        if constexpr (BORDER && PUB == 2) AFF_ASM(ANYSEQ_AFF_G_B1_GLOB);
+        if constexpr (!BORDER && PUB == 0) AFF_ASM(ANYSEQ_AFF_G_B0_NONE);
+        if constexpr (!BORDER && PUB == 1) AFF_ASM(ANYSEQ_AFF_G_B0_LDS);
+        if constexpr (!BORDER && PUB == 2) AFF_ASM(ANYSEQ_AFF_G_B0_GLOB);
+    }
+    tf = make_int2(tfg, tff);
+    return st;
+}
+#undef AFF_ASM
+
+template <int KIND, bool PARTIAL, bool FINOUT>
+__device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k) {
+    constexpr int CH = 32;
+    constexpr int IRM = kSlots * CH - 1;
+    constexpr int LAG = 2;   // lane 63 finishes column c at step c + 64: chunk j is complete after block j + 2
+    // VIRT (global): lanes left of column 0 compute virtual cells from "minus
+    // infinity" states; lane 0's top value at column -1 is (G[rb-1][-1], go), so
+    // column -1 computes G = F = go, the left border, and E at column 0 = 2 go, as
+    // the oracle's.  The prologue then runs in the asm loop.  Semiglobal / local
+    // borders grow with the row and keep the masked C++ prologue.
+    constexpr bool VIRT = KIND == KIND_GLOBAL && !PARTIAL && !FINOUT;
+    constexpr bool ASM = !PARTIAL && !FINOUT;
+    const int h = P.h, w = P.w, go = k.go, nge = k.nge;
+    const int rb = band * 64;
+    const int row = rb + lane;
+    const bool dead = row >= h;
+    const bool lastrow = row == h - 1;
+    int q = dead ? 0x100 : (int)gmem(P.q)[P.q_off + P.q_step * row];
+    // settle the query load here: a vmcnt wait inside the step loop would also wait
+    // for lane 63's HBM row stores
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(q)::"memory");
+    int g, e = kAffNeg, hg, fdn = kAffNeg, dg;
+    int2 tf;
+    if (VIRT) {
+        g = kAffNeg;
+        hg = kAffNeg;
+        dg = kAffNeg;
+        tf = make_int2(aff_border<KIND>(rb - 1, go, nge), go);
+    } else {
+        g = aff_border<KIND>(row, go, nge);
+        hg = g + go;   // the next column's E candidate: G[r][-1] + go
+        dg = aff_border<KIND>(row - 1, go, nge);
+        tf = make_int2(aff_border<KIND>(rb - 1, go, nge), kAffNeg);
+    }
+    int best = 0;
+    const int nchunks = (w + CH - 1) / CH;
+    const int nblocks = nchunks + LAG;
+    const int fe = w >= CH - 1 ? (w - (CH - 1)) / CH + 1 : 0;   // full blocks: 32b + 30 < w
+    uint32_t seen_prod = 0, seen_sfill = 0, seen_cons = 0;
+    AffLoopArgs la;
+    if constexpr (ASM) {
+        la.rb = lds_addr(io.my_ring);
+        la.nb = io.out_lds ? lds_addr(io.next_ring) : 0u;
+        la.apr = lds_addr(io.my_prod);
+        la.acn = lds_addr(io.my_cons);
+        la.anp = io.out_lds ? lds_addr(io.next_prod) : 0u;
+        la.anc = io.out_lds ? lds_addr(io.next_cons) : 0u;
+        la.asf = lds_addr(io.s_filled);
+        la.atl = lds_addr(io.tail);
+        la.skb = lds_addr(io.skew) + 4u * lane;
+        la.lo = 8u * (lane - 32);
+        la.lid8 = 8u * lane;
+        la.bvb = (uint32_t)aff_border<KIND>(lane, go, nge);
+        la.bvs = (uint32_t)(aff_border<KIND>(1, go, nge) - aff_border<KIND>(0, go, nge));
+        la.gp = (uint64_t)(size_t)io.gout;
+    }
+    for (int b = 0; b < nblocks; ++b) {
+        const int t0 = b * CH;
+        if constexpr (ASM) {
+            if ((VIRT || t0 >= 64) && b < fe && !(k.flags & 1)) {
+                uint32_t bb = (uint32_t)b;
+                uint32_t z = (uint32_t)((rb + t0 + 1) * nge);
+                const int role = (io.in_border ? 3 : 0) + (io.out_lds ? 1 : (io.gout ? 2 : 0));
+                uint32_t st = 0;
+#define AF_CALL(BD, PB)                                                                                    \
+    st = aff_loop_asm<KIND, BD, PB>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, q, g, fdn, dg, tf, e, \
+                                    hg, best, z, k)
+                switch (role) {
+                    case 0: AF_CALL(false, 0); break;
+                    case 1: AF_CALL(false, 1); break;
+                    case 2: AF_CALL(false, 2); break;
+                    case 3: AF_CALL(true, 0); break;
+                    case 4: AF_CALL(true, 1); break;
+                    default: AF_CALL(true, 2); break;
+                }
+#undef AF_CALL
+                if (st) {
+                    atomicOr(err, ERR_SPIN_TIMEOUT);
+                    return;
+                }
+                b = (int)bb - 1;   // ++b of the for
+                continue;
+            }
+        }
+        if (b < nchunks && seen_sfill < (uint32_t)(b + 1)) {
+            if (!(seen_sfill = spin_lds_ge(io.s_filled, (uint32_t)(b + 1), err))) return;
+        }
+        uint32_t sw[8];
+        load_sbytes<CH>(io.s_ring, (t0 - 1 - lane) & (kSRing - 1), sw);
+        int2 rv[CH];
+        if (b < nchunks) {
+            if (io.in_border) {
+                const int bv = aff_border<KIND>(t0 + lane, go, nge);
+                io.my_ring[(t0 + lane) & IRM] = make_int2(bv, bv + go);
+            } else if (seen_prod < (uint32_t)(b + 1)) {
+                if (!(seen_prod = spin_lds_ge(io.my_prod, (uint32_t)(b + 1), err))) return;
+            }
+            const int4* src = reinterpret_cast<const int4*>(io.my_ring + (t0 & IRM));
+#pragma unroll
+            for (int i = 0; i < CH / 2; ++i) {
+                const int4 v = src[i];
+                rv[2 * i] = make_int2(v.x, v.y);
+                rv[2 * i + 1] = make_int2(v.z, v.w);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < CH; ++i) rv[i] = make_int2(kAffNeg, kAffNeg);
+        }
+        const int j = b - LAG;
+        const bool pub = io.out_lds && j >= 0;
+        if (pub) {
+            const uint32_t need = (uint32_t)max(0, j - kSlots + 1);
+            if (seen_cons < need) {
+                if (!(seen_cons = spin_lds_ge(io.next_cons, need, err))) return;
+            }
+        }
+        int og[CH], of[CH];
+        const int c0 = t0 - 1 - lane;
+        const int z = (rb + t0 + 1) * nge;
+        const bool full = (VIRT || t0 >= 64) && b < fe;
+        if (full)
+            aff_block<KIND, false, PARTIAL, FINOUT, VIRT>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg, best,
+                                                    og, of, k);
+        else
+            aff_block<KIND, true, PARTIAL, FINOUT, VIRT>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg, best,
+                                                   og, of, k);
+        tf = rv[CH - 1];
+        if (pub && lane == 63) {
+            int4* dst = reinterpret_cast<int4*>(io.next_ring + ((j * CH) & IRM));
+#pragma unroll
+            for (int i = 0; i < CH / 2; ++i) dst[i] = make_int4(og[2 * i], of[2 * i], og[2 * i + 1], of[2 * i + 1]);
+        }
+        if (io.gout && j >= 0 && lane == 63) {
+            // 16-byte write-through stores of two (G, F) columns; each column's 8 bytes
+            // land together, so the consumer's 64-bit poll never sees half a column
+            int2* dst = io.gout + j * CH;
+            if (j * CH + CH <= w && !(k.flags & 2)) {
+#pragma unroll
+                for (int i = 0; i < CH / 2; ++i) {
+                    typedef int v4i __attribute__((ext_vector_type(4)));
+                    const v4i v = {og[2 * i], of[2 * i], og[2 * i + 1], of[2 * i + 1]};
+                    // s_nop: a >64-bit store's data VGPRs must not be rewritten by the next
+                    // VALU (VMEM store-data hazard; the compiler cannot pad inline asm)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1\n s_nop 1" ::"v"(dst + 2 * i), "v"(v)
+                                 : "memory");
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+                    if (j * CH + u < w) HandOff<int2>::store(io.gout + j * CH + u, make_int2(og[u], of[u]));
+            }
+        }
+        if (!io.in_border && b < nchunks) lds_st(io.my_cons, (uint32_t)(b + 1));
+        if (io.trailing) lds_st(io.tail, (uint32_t)(b + 1));
+        if (pub) lds_st(io.next_prod, (uint32_t)(j + 1));
+    }
+    if (!io.in_border) lds_st(io.my_cons, (uint32_t)(nchunks + kSlots));
+    if (io.trailing) lds_st(io.tail, 0x7fffffffu);
+    if (!dead) {
+        if (P.out_col) gmem(P.out_col)[row] = aff_to_h(g, row, w - 1, nge);
+        if (P.out_col_e) gmem(P.out_col_e)[row] = aff_to_h(e, row, w - 1, nge);
+    }
+    if (KIND == KIND_LOCAL && P.best) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
+        if (lane == 0) atomicMax(P.best, best);
+    }
+}
+
+template <int KIND, int NW>
+__global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProblem* __restrict__ probs,
+                                                                     const GroupRef* __restrict__ groups,
+                                                                     int ngroups_total, uint32_t* dq, uint32_t* err,
+                                                                     FillParams fp) {
+    __shared__ __attribute__((aligned(16))) AffShared<NW> sh;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    AffK k;
+    k.go = fp.gap_open;
+    k.nge = -fp.gap_extend;
+    k.wm = fp.match + 2 * k.nge;
+    k.wx = fp.mismatch + 2 * k.nge;
+    k.flags = fp.pad;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            sh.group = (int32_t)atomicAdd(dq, 1u);
+            sh.s_filled = 0;
+            sh.tail = 0;
+        }
+        if (threadIdx.x <= NW) {
+            sh.prod[threadIdx.x] = 0;
+            sh.cons[threadIdx.x] = 0;
+        }
+        __syncthreads();
+        const int gi = __builtin_amdgcn_readfirstlane(sh.group);
+        if (gi >= ngroups_total || err_set(err)) break;
+        const GroupRef gr = groups[gi];
+        const DPProblem P = probs[gr.prob];
+        const int first = gr.group * NW;
+        const int last = min(P.nbands, first + NW) - 1;
+        int2* rows = reinterpret_cast<int2*>(P.rowbuf);
+        int2* g_out = nullptr;
+        if (last < P.nbands - 1)
+            g_out = rows + (size_t)gr.group * P.wpad;
+        else if (P.out_row)
+            g_out = reinterpret_cast<int2*>(P.out_row);
+        if (wave == NW) {
+            const int2* g_in = gr.group > 0 ? rows + (size_t)(gr.group - 1) * P.wpad : nullptr;
+            io_wave<32, true, int2>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0], &sh.s_filled,
+                                    &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err);
+        } else {
+            const int band = first + wave;
+            if (band <= last) {
+                AffIO io;
+                io.in_border = band == 0;
+                io.trailing = band == last;
+                io.my_ring = sh.in_ring[wave];
+                io.my_prod = &sh.prod[wave];
+                io.my_cons = &sh.cons[wave];
+                io.s_ring = sh.s_ring;
+                io.skew = &sh.skew[0][0][0];
+                io.s_filled = &sh.s_filled;
+                io.tail = &sh.tail;
+                io.out_lds = band < last;
+                io.next_ring = band < last ? sh.in_ring[wave + 1] : nullptr;
+                io.next_prod = band < last ? &sh.prod[wave + 1] : nullptr;
+                io.next_cons = band < last ? &sh.cons[wave + 1] : nullptr;
+                io.gout = band < last ? nullptr : g_out;
+                const bool partial = (band + 1) * 64 > P.h;
+                const bool finout = band == P.nbands - 1 && P.out_row != nullptr;
+                if (partial) {
+                    if (finout) run_band_aff<KIND, true, true>(P, band, lane, io, err, k);
+                    else run_band_aff<KIND, true, false>(P, band, lane, io, err, k);
+                } else {
+                    if (finout) run_band_aff<KIND, false, true>(P, band, lane, io, err, k);
+                    else run_band_aff<KIND, false, false>(P, band, lane, io, err, k);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Affine score reductions (H space; rows are (G, F) pairs of the kernel value space).
+// Single front: semiglobal max over the last row (index -1 = border 0), the last
+// column and 0.  Two fronts (top rows [0,h1) forward, bottom rows [h1,n) reversed):
+// for every split column j in [-1, m-1], with jb = m-2-j,
+//     max(Ht[j] + Hb[jb], Ft[j] + Fb[jb] - go)
+// (F = vertical-gap state of the last row; a vertical gap across the split is
+// opened once), plus the semiglobal end columns / the local best cells.
+__global__ void aff_reduce_kernel(int kind, int two, const int2* __restrict__ rowF, int h1,
+                                  const int2* __restrict__ rowB, int h2, int m, int go, int ge,
+                                  const int32_t* __restrict__ colF, const int32_t* __restrict__ colB, int32_t* out) {
+    auto toh = [&](int v, int r, int c) { return v + (r + c + 2) * ge; };   // all kinds run in G space
+    const int NEG2 = 2 * kAffNeg;
+    int best = kind == KIND_SEMIGLOBAL ? 0 : -2147483647;
+    const int tid = threadIdx.x + blockIdx.x * blockDim.x, nth = blockDim.x * gridDim.x;
+    if (two) {
+        const int bt = kind == KIND_GLOBAL ? go + h1 * ge : 0;   // H[h1-1][-1]
+        const int bb = kind == KIND_GLOBAL ? go + h2 * ge : 0;
+        const int ft = kind == KIND_GLOBAL ? bt : kAffNeg;       // global borders are vertical gaps
+        const int fb = kind == KIND_GLOBAL ? bb : kAffNeg;
+        for (int j = tid - 1; j < m; j += nth) {
+            int Ht = bt, Ft = ft, Hb = bb, Fb = fb;
+            if (j >= 0) {
+                const int2 t = rowF[j];
+                Ht = toh(t.x, h1 - 1, j);
+                Ft = toh(t.y, h1 - 1, j);
+            }
+            const int jb = m - 2 - j;
+            if (jb >= 0) {
+                const int2 t = rowB[jb];
+                Hb = toh(t.x, h2 - 1, jb);
+                Fb = toh(t.y, h2 - 1, jb);
+            }
+            best = max(best, max(Ht + Hb, max(Ft + Fb - go, NEG2)));
+        }
+        if (kind == KIND_SEMIGLOBAL) {
+            for (int i = tid; i < h1; i += nth) best = max(best, colF[i]);
+            for (int i = tid; i < h2; i += nth) best = max(best, colB[i]);
+        }
+    } else if (kind == KIND_SEMIGLOBAL) {
+        for (int j = tid; j < m; j += nth) best = max(best, toh(rowF[j].x, h1 - 1, j));
+        for (int i = tid; i < h1; i += nth) best = max(best, colF[i]);
+    }
+    for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, best);
 }
 
 // ------------------------------------------------------------ reductions --
@@ -1095,6 +1567,25 @@ static hipError_t launch_fill_c(int R, int NW, const DPProblem* probs, const Gro
     }
 }
 
+template <int NW>
+static hipError_t launch_fill_aff_n(const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
+                                    uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
+    const dim3 blk(64 * (NW + 1));
+    switch (fp.kind) {
+        case KIND_GLOBAL:
+            hipLaunchKernelGGL((fill_affine_kernel<KIND_GLOBAL, NW>), dim3(grid), blk, 0, st, probs, groups, ngroups,
+                               dq, err, fp);
+            break;
+        case KIND_SEMIGLOBAL:
+            hipLaunchKernelGGL((fill_affine_kernel<KIND_SEMIGLOBAL, NW>), dim3(grid), blk, 0, st, probs, groups,
+                               ngroups, dq, err, fp);
+            break;
+        default:
+            hipLaunchKernelGGL((fill_affine_kernel<KIND_LOCAL, NW>), dim3(grid), blk, 0, st, probs, groups, ngroups,
+                               dq, err, fp);
+    }
+    return hipGetLastError();
+}
 #endif  // ANYSEQ_MICRO
 }  // namespace anyseq
 
@@ -1109,6 +1600,24 @@ hipError_t anyseq_launch_fill(int R, int CH, int NW, const anyseq::DPProblem* pr
     using namespace anyseq;
     if (CH == 16) return launch_fill_c<16>(R, NW, probs, groups, ngroups, dq, err, *fp, grid, st);
     return launch_fill_c<32>(R, NW, probs, groups, ngroups, dq, err, *fp, grid, st);
+}
+
+// Affine fill launcher: NW compute waves per workgroup in {3, 4} (+1 I/O wave).
+hipError_t anyseq_launch_fill_affine(int NW, const anyseq::DPProblem* probs, const anyseq::GroupRef* groups,
+                                     int ngroups, uint32_t* dq, uint32_t* err, const anyseq::FillParams* fp, int grid,
+                                     hipStream_t st) {
+    using namespace anyseq;
+    // (the asm steady state holds ~150 fixed VGPRs: at most 2 waves per SIMD, NW <= 7)
+    if (NW == 3) return launch_fill_aff_n<3>(probs, groups, ngroups, dq, err, *fp, grid, st);
+    return launch_fill_aff_n<4>(probs, groups, ngroups, dq, err, *fp, grid, st);
+}
+
+hipError_t anyseq_launch_aff_reduce(int kind, int two, const void* rowF, int h1, const void* rowB, int h2, int m,
+                                    int go, int ge, const int32_t* colF, const int32_t* colB, int32_t* out,
+                                    hipStream_t st) {
+    hipLaunchKernelGGL(anyseq::aff_reduce_kernel, dim3(64), dim3(256), 0, st, kind, two, (const int2*)rowF, h1,
+                       (const int2*)rowB, h2, m, go, ge, colF, colB, out);
+    return hipGetLastError();
 }
 
 hipError_t anyseq_launch_semiglobal_reduce(const int32_t* row_g, int m, const int32_t* col_h, int n, int ng,

@@ -1,0 +1,113 @@
+"""GPU parity for the affine-gap (Gotoh) fill: HIP path (C-ABI anyseq_score) vs the oracle.
+
+Affine semantics are build-defined (the reference's affine_scoring_scheme,
+align.impala:153-166, is dead code): oracle_affine_score in oracle/anyseq_oracle.c,
+pinned on the CPU by `open == 0 => linear` and an independent textbook Gotoh
+(tests/test_oracle.py).  Scores are integers: bit-exact.
+"""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ("global", "semiglobal", "local")
+SCHEMES = [(2, -1, -2, -1), (2, -1, 0, -1), (1, -3, -5, -2), (5, -4, -10, -1), (3, -2, -1, -3)]
+
+
+def rnd(rng, n, alphabet="ACGT"):
+    return "".join(rng.choice(alphabet) for _ in range(n))
+
+
+def gpu(anyseq, kind, q, s, sc):
+    return anyseq.score(kind, q, s, match=sc[0], mismatch=sc[1], gap_open=sc[2], gap_extend=sc[3])
+
+
+def ora(oracle, kind, q, s, sc):
+    return oracle.affine_score(kind, q, s, *sc)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_small_random(anyseq, oracle, kind):
+    rng = random.Random(21)
+    for it in range(60):
+        sc = SCHEMES[it % len(SCHEMES)]
+        n, m = rng.randint(1, 300), rng.randint(1, 300)
+        q, s = rnd(rng, n), rnd(rng, m)
+        assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, n, m, sc)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_edge_shapes(anyseq, oracle, kind):
+    rng = random.Random(22)
+    sc = (2, -1, -2, -1)
+    for n in [0, 1, 2, 31, 32, 33, 63, 64, 65, 127, 128, 129, 511, 512, 513, 1023, 1024, 1025, 2049]:
+        for m in (0, 1, 31, 32, 33, 63, 64, 65, 1000):
+            q, s = rnd(rng, n), rnd(rng, m)
+            assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, n, m)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_multi_group_two_fronts(anyseq, oracle, kind):
+    """Several workgroups per problem (HBM hand-off of (G, F) rows) and the two-front split."""
+    rng = random.Random(23)
+    for (n, m), sc in zip([(5000, 3000), (3000, 7000), (4097, 4095), (9000, 300), (2100, 2100)],
+                          [(2, -1, -2, -1), (1, -3, -5, -2), (2, -1, -3, -1), (5, -4, -10, -1), (2, -1, 0, -1)]):
+        q, s = rnd(rng, n), rnd(rng, m)
+        assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, n, m, sc)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_long_gaps_cross_split(anyseq, oracle, kind):
+    """A long vertical gap spanning the two-front split row (opened once, not twice)."""
+    rng = random.Random(24)
+    core = rnd(rng, 1500)
+    ins = rnd(rng, 1200)
+    q = core[:700] + ins + core[700:]        # the query carries an insertion around row n/2
+    s = core
+    for sc in [(2, -1, -8, -1), (2, -1, -2, -1), (1, -1, -20, -1)]:
+        assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, sc)
+        assert gpu(anyseq, kind, s, q, sc) == ora(oracle, kind, s, q, sc), (kind, sc)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_open_zero_is_linear(anyseq, oracle, kind):
+    rng = random.Random(25)
+    for n, m in [(700, 900), (3000, 2500)]:
+        q, s = rnd(rng, n), rnd(rng, m)
+        assert anyseq.score(kind, q, s, gap_open=0, gap_extend=-1) == oracle.score(kind, q, s)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_bytes_and_similar(anyseq, oracle, kind):
+    rng = random.Random(26)
+    q = bytes(rng.randrange(256) for _ in range(700))
+    s = bytes(rng.randrange(256) for _ in range(900))
+    sc = (2, -1, -2, -1)
+    assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc)
+    base = rnd(rng, 3000)
+    mut = list(base)
+    for _ in range(150):
+        mut[rng.randrange(len(mut))] = rng.choice("ACGT")
+    s2 = "".join(mut)
+    assert gpu(anyseq, kind, base, s2, sc) == ora(oracle, kind, base, s2, sc)
+
+
+@pytest.mark.parametrize("nw", [3, 4])
+def test_affine_waves_per_group(anyseq, oracle, nw):
+    rng = random.Random(27)
+    anyseq.set_option("affine_waves_per_group", nw)
+    try:
+        for kind in KINDS:
+            q, s = rnd(rng, 2600), rnd(rng, 1900)
+            sc = (2, -1, -3, -1)
+            assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, nw)
+    finally:
+        anyseq.set_option("affine_waves_per_group", 4)
+
+
+def test_affine_rejects_bad_scoring(anyseq):
+    with pytest.raises(anyseq.AnySeqError):
+        anyseq.score("global", "ACGT", "ACGT", gap_open=1, gap_extend=-1)
+    with pytest.raises(anyseq.AnySeqError):
+        anyseq.score("global", "ACGT", "ACGT", gap_open=-1, gap_extend=0)

@@ -112,7 +112,7 @@ SK0, VT, VT2, VA, VB = 130, 138, 139, 140, 141   # subject words, temps, LDS add
 TA, TB = 96, 98                                   # fixed SGPR pairs for s_memrealtime
 
 
-def wait(e, name, seen, target, addr, count=None):
+def wait(e, name, seen, target, addr, count=None, tmp=None):
     """Spin until seen >= target, refreshing `seen` from the LDS word at `addr`
     (wave-uniform), with s_sleep between polls and a 10 s s_memrealtime limit
     checked every 256 polls (-> L_timeout)."""
@@ -121,9 +121,10 @@ def wait(e, name, seen, target, addr, count=None):
     e(f"s_memrealtime s[{TA}:{TA + 1}]")
     e("s_mov_b32 %[x3], 0")
     e(f"L_{name}_loop_%=:")
-    e(f"ds_read_b32 v{VT2}, {addr}")
+    tmp = VT2 if tmp is None else tmp
+    e(f"ds_read_b32 v{tmp}, {addr}")
     e("s_waitcnt lgkmcnt(0)")
-    e(f"v_readfirstlane_b32 {seen}, v{VT2}")
+    e(f"v_readfirstlane_b32 {seen}, v{tmp}")
     e(f"s_cmp_ge_u32 {seen}, {target}")
     e(f"s_cbranch_scc1 L_{name}_ok_%=")
     if count:
@@ -283,6 +284,182 @@ def gen_loop2(kind, border, pub, ts=False):
     return out
 
 
+# ---------------------------------------------------------------- affine --
+AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v191
+AW, AA, AH = 192, 193, 194  # weight, diag + weight, H - Z temp (local best)
+ASK0, ASK1 = 196, 204       # subject words, double buffered
+AVT, AVT2, AVA, AVB = 212, 213, 214, 215
+
+
+def gen_loop_aff(kind, border, pub):
+    """Affine (Gotoh, G-space) steady-state loop over full blocks b .. be-1 of a
+    band; same LDS protocol as gen_loop2 with (G, F) pairs in the rings.
+    Per step (kind G: global / semiglobal; L: local adds the clamp and the best):
+        C  v_cmp_eq_u32_sdwa vcc, q, s.byte
+        D  v_cndmask_b32     W, wx, wm, vcc
+        F1 v_mov_b32_dpp     TF, Fprev wave_shr:1   F of this cell from the row above
+        G1 v_mov_b32_dpp     TG, Gprev wave_shr:1   G of the row above (next diagonal)
+        X  v_max_i32         e, e, hg               E_G = max(E_G, G_left + go)
+        E  v_add_u32         A, dg, W
+        M  v_max3_i32        OG, A, e, TF           cell
+       (L  v_max_i32         OG, Z, OG              clamp: H >= 0 <=> G >= Z_t (wave-uniform))
+        H  v_add_u32         hg, go, OG             G + go (next E, this F-down)
+        Fm v_max_i32         OF, TF, hg             F-down
+       (L  every 2nd step: best = max3(best, OG - Z, OG' - Z'))
+        S  two wave_shl:1 shift-register steps (publishing roles)."""
+    L = kind == "L"
+    trailing = pub != "lds"
+    out = []
+    e = out.append
+    sets = (ASK0, ASK1)
+
+    def TG(u):
+        return v(AT0 + 2 * u)
+
+    def TF(u):
+        return v(AT0 + 2 * u + 1)
+
+    def OG(u):
+        return v(AO0 + 2 * u)
+
+    def OF(u):
+        return v(AO0 + 2 * u + 1)
+
+    def body(k):
+        cs, ns = sets[k], sets[1 - k]
+        e("s_add_u32 %[x1], %[b], 1")
+        if border:
+            # band 0: lanes write the top border (G, G + go) of column 32b + lane
+            e("s_lshl_b32 %[x0], %[b], 5")
+            e("s_mul_i32 %[x2], %[x0], %[bvs]")
+            e(f"v_add_u32_e32 v{AVT}, %[x2], %[bvb]")
+            e(f"v_add_u32_e32 v{AVT + 1}, %[go], v{AVT}")
+            e("s_lshl_b32 %[x2], %[x0], 3")
+            e(f"v_add_u32_e32 v{AVA}, %[x2], %[lid8]")
+            e(f"v_and_b32_e32 v{AVA}, 0xfff, v{AVA}")
+            e(f"v_add_u32_e32 v{AVA}, %[rb], v{AVA}")
+            e(f"ds_write_b64 v{AVA}, v[{AVT}:{AVT + 1}]")
+            e("s_waitcnt lgkmcnt(0)")
+        else:
+            wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=AVT2)
+        if pub == "lds":
+            e("s_cmp_lt_u32 %[b], 17")
+            e(f"s_cbranch_scc1 L_nobp{k}_%=")
+            e("s_sub_u32 %[x4], %[b], 17")
+            wait(e, f"bp{k}", "%[sc]", "%[x4]", "%[anc]", tmp=AVT2)
+            e(f"L_nobp{k}_%=:")
+        # top row of block b: 32 (G, F) pairs
+        e("s_lshl_b32 %[x2], %[b], 8")
+        e("s_and_b32 %[x2], %[x2], 4095")
+        e("s_add_u32 %[x2], %[x2], %[rb]")
+        e(f"v_mov_b32_e32 v{AVB}, %[x2]")
+        for i in range(16):
+            e(f"ds_read_b128 v[{AT0 + 4 * i}:{AT0 + 4 * i + 3}], v{AVB} offset:{16 * i}")
+        g, f, dg = "%[cur]", "%[fd]", "%[dg]"
+        pf = 0   # prefetch reads issued (outstanding behind the ring reads)
+        for u in range(32):
+            if u == 16:
+                # prefetch the next block's subject words (behind the ring reads)
+                e("s_cmp_ge_u32 %[x1], %[be]")
+                e(f"s_cbranch_scc1 L_nopf{k}_%=")
+                e("s_add_u32 %[x4], %[b], 2")
+                wait(e, f"sf{k}", "%[sf]", "%[x4]", "%[asf]", tmp=AVT2)
+                e("s_and_b32 %[x2], %[x1], 31")
+                e("s_lshl_b32 %[x2], %[x2], 11")
+                e(f"v_add_u32_e32 v{AVA}, %[x2], %[skb]")
+                for i in range(4):
+                    e(f"ds_read2st64_b32 v[{ns + 2 * i}:{ns + 2 * i + 1}], v{AVA} offset0:{2 * i} offset1:{2 * i + 1}")
+                e(f"L_nopf{k}_%=:")
+                pf = 4
+            if u >= 1 and (u - 1) % 2 == 0:
+                i = (u - 1) // 2      # ring read holding column 32b + u - 1
+                e(f"s_waitcnt lgkmcnt({min(15, 15 - i + pf)})")
+            sw = v(cs + u // 4)
+            tg = "%[tfg]" if u == 0 else TG(u - 1)
+            tf = "%[tff]" if u == 0 else TF(u - 1)
+            e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+            e(f"v_cndmask_b32_e32 v{AW}, %[wx], %[wm], vcc")
+            e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
+            e("v_max_i32_e32 %[e], %[e], %[hg]")
+            e(f"v_add_u32_e32 v{AA}, {dg}, v{AW}")
+            e(f"v_max3_i32 {OG(u)}, v{AA}, %[e], {tf}")
+            if L:
+                e(f"v_max_i32_e32 {OG(u)}, %[z], {OG(u)}")
+            e(f"v_add_u32_e32 %[hg], %[go], {OG(u)}")
+            e(f"v_max_i32_e32 {OF(u)}, {tf}, %[hg]")
+            if L:
+                if u % 2 == 0:
+                    e(f"v_subrev_u32_e32 v{AH}, %[z], {OG(u)}")
+                else:
+                    e(f"v_subrev_u32_e32 v{AVT2}, %[z], {OG(u)}")
+                    e(f"v_max3_i32 %[best], %[best], v{AH}, v{AVT2}")
+                e("s_add_u32 %[z], %[z], %[nge]")
+            if u >= 2 and pub != "none":
+                e(f"v_mov_b32_dpp {OG(u - 1)}, {OG(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_mov_b32_dpp {OF(u - 1)}, {OF(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            g, f, dg = OG(u), OF(u), tg
+        e(f"v_mov_b32_e32 %[cur], {OG(31)}")
+        e(f"v_mov_b32_e32 %[fd], {OF(31)}")
+        e(f"v_mov_b32_e32 %[dg], {TG(30)}")
+        if pub != "none":
+            e(f"v_mov_b32_dpp {OG(31)}, {OG(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_mov_b32_dpp {OF(31)}, {OF(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+        e(f"v_mov_b32_e32 %[tfg], {TG(31)}")
+        e(f"v_mov_b32_e32 %[tff], {TF(31)}")
+        if pub != "none":
+            e("s_cmp_lt_u32 %[b], 2")
+            e(f"s_cbranch_scc1 L_nopub{k}_%=")
+            e("s_sub_u32 %[x2], %[b], 2")
+            e("s_lshl_b32 %[x2], %[x2], 8")
+            if pub == "lds":
+                e("s_and_b32 %[x2], %[x2], 4095")
+                e("s_add_u32 %[x2], %[x2], %[nb]")
+            e(f"v_add_u32_e32 v{AVT}, %[x2], %[lo]")
+            e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
+            e("s_mov_b64 exec, %[hm]")
+            if pub == "lds":
+                e(f"ds_write_b64 v{AVT}, v[{AO0 + 62}:{AO0 + 63}]")
+            else:
+                e(f"global_store_dwordx2 v{AVT}, v[{AO0 + 62}:{AO0 + 63}], %[gp] sc1")
+            e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
+            if pub == "lds":
+                e("s_sub_u32 %[x2], %[b], 1")
+                e(f"v_mov_b32_e32 v{AVT2}, %[x2]")
+                e(f"ds_write_b32 %[anp], v{AVT2}")
+            e(f"L_nopub{k}_%=:")
+        e(f"v_mov_b32_e32 v{AVT2}, %[x1]")
+        if not border:
+            e(f"ds_write_b32 %[acn], v{AVT2}")
+        if trailing:
+            e(f"ds_write_b32 %[atl], v{AVT2}")
+        e("s_mov_b32 %[b], %[x1]")
+
+    # prologue: the first block's subject words into set 0
+    e("s_add_u32 %[x1], %[b], 1")
+    wait(e, "sfp", "%[sf]", "%[x1]", "%[asf]", tmp=AVT2)
+    e("s_and_b32 %[x2], %[b], 31")
+    e("s_lshl_b32 %[x2], %[x2], 11")
+    e(f"v_add_u32_e32 v{AVA}, %[x2], %[skb]")
+    for i in range(4):
+        e(f"ds_read2st64_b32 v[{ASK0 + 2 * i}:{ASK0 + 2 * i + 1}], v{AVA} offset0:{2 * i} offset1:{2 * i + 1}")
+    e("s_waitcnt lgkmcnt(0)")
+    e("L_top_%=:")
+    body(0)
+    e("s_cmp_lt_u32 %[b], %[be]")
+    e("s_cbranch_scc0 L_done_%=")
+    body(1)
+    e("s_cmp_lt_u32 %[b], %[be]")
+    e("s_cbranch_scc1 L_top_%=")
+    e("L_done_%=:")
+    e("s_mov_b32 %[st], 0")
+    e("s_branch L_end_%=")
+    e("L_timeout_%=:")
+    e("s_mov_b32 %[st], 1")
+    e("L_end_%=:")
+    return out
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
     dst = os.path.join(here, "..", "anyseq_amd", "csrc", "anyseq_block_asm.inc")
@@ -309,6 +486,17 @@ def main():
                     for ln in gen_loop2(kind, border, pub, ts):
                         lines.append(f'    "{ln}\\n" \\')
                     lines.append("")
+    for kind in ("G", "L"):
+        for border in (0, 1):
+            for pub in ("none", "lds", "glob"):
+                name = f"ANYSEQ_AFF_{kind}_B{border}_{pub.upper()}"
+                lines.append(f"#define {name} \\")
+                for ln in gen_loop_aff(kind, border, pub):
+                    lines.append(f'    "{ln}\\n" \\')
+                lines.append("")
+    clob = ", ".join(f'"v{n}"' for n in range(AT0, AVB + 1))
+    sclob = ", ".join(f'"s{n}"' for n in range(TA, TB + 2))
+    lines.append(f"#define ANYSEQ_AFF_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, A + 1))
     lines.append(f"#define ANYSEQ_BLOCK_ASM_CLOBBERS {clob}, \"vcc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, SKB_ + 8))
