@@ -14,29 +14,32 @@ $(SRC)/anyseq_block_asm.inc: tools/gen_block_asm.py
 $(SRC)/anyseq_kernels.o: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_internal.h $(SRC)/anyseq_block_asm.inc
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -c $< -o $@
 
-$(SRC)/anyseq_engine.o: $(SRC)/anyseq_engine.cpp $(SRC)/anyseq_internal.h include/anyseq.h
+$(SRC)/anyseq_engine.o: $(SRC)/anyseq_engine.cpp $(SRC)/anyseq_internal.h $(SRC)/anyseq_host.h include/anyseq.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(SRC)/anyseq_kernels.o $(SRC)/anyseq_engine.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
+$(SRC)/anyseq_shard.o: $(SRC)/anyseq_shard.cpp $(SRC)/anyseq_internal.h $(SRC)/anyseq_host.h include/anyseq.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(SRC)/anyseq_kernels.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -L/opt/rocm/lib -lrccl
 
 oracle:
 	$(MAKE) -s -C oracle
 
 # diagnostic build with s_memtime stamps (tools only; never loaded by the product path)
 stamps: anyseq_amd/libanyseq_stamps.so
-anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_internal.h $(SRC)/anyseq_block_asm.inc
+anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_internal.h $(SRC)/anyseq_block_asm.inc
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_stamps.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o -L/opt/rocm/lib -lrccl
 
 # timing experiments (ANYSEQ_EXP bits, see anyseq_kernels.hip); wrong results by design
 anyseq_amd/libanyseq_e%.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_internal.h
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_EXP=$* -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_e$*.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_e$*.o $(SRC)/anyseq_engine.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_e$*.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o -L/opt/rocm/lib -lrccl
 
 anyseq_amd/libanyseq_se%.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_internal.h
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -DANYSEQ_EXP=$* -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_se$*.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_se$*.o $(SRC)/anyseq_engine.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_se$*.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o -L/opt/rocm/lib -lrccl
 
 clean:
 	rm -f $(SRC)/*.o $(LIB) anyseq_amd/libanyseq_*.so

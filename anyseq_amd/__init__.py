@@ -61,6 +61,18 @@ _lib.anyseq_score_device.argtypes = [_c_int, ctypes.POINTER(Scoring), _vp, _c_in
 _lib.anyseq_construct.restype = _c_int
 _lib.anyseq_construct.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _vp, _vp,
                                   ctypes.POINTER(_c_i64)]
+_lib.anyseq_shard_score_local.restype = _c_int
+_lib.anyseq_shard_score_local.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _c_int,
+                                          ctypes.POINTER(_c_i64)]
+_lib.anyseq_shard_unique_ids.restype = _c_int
+_lib.anyseq_shard_unique_ids.argtypes = [_vp, _c_int]
+_lib.anyseq_shard_init.restype = _c_int
+_lib.anyseq_shard_init.argtypes = [_c_int, _c_int, _c_p, _c_int]
+_lib.anyseq_shard_load.restype = _c_int
+_lib.anyseq_shard_load.argtypes = [_c_p, _c_int, _c_p, _c_int, _c_int, _c_int]
+_lib.anyseq_shard_score.restype = _c_int
+_lib.anyseq_shard_score.argtypes = [_c_int, ctypes.POINTER(Scoring), ctypes.POINTER(_c_i64)]
+_lib.anyseq_shard_finalize.restype = _c_int
 _lib.anyseq_last_error.restype = _c_p
 _lib.anyseq_set_device.argtypes = [_c_int]
 _lib.anyseq_set_tuning.argtypes = [_c_int, _c_int, _c_int]
@@ -168,6 +180,19 @@ def construct(kind, query, subject, match=2, mismatch=-1, gap_open=0, gap_extend
                              ctypes.byref(out)) != 0:
         raise AnySeqError(_err())
     return out.value, aq.raw[:L], as_.raw[:L]
+
+
+def shard_score_local(kind, query, subject, nshards: int, match=2, mismatch=-1, gap_open=0, gap_extend=-1) -> int:
+    """Column-block sharded score with `nshards` shards in this process on one GPU
+    (the same kernels, progress counters and chunked hand-off as the RCCL path,
+    with device copies as the transport) -- DESIGN.md §6."""
+    q, s = _b(query), _b(subject)
+    out = _c_i64(0)
+    sc = _scoring(match, mismatch, gap_open, gap_extend)
+    if _lib.anyseq_shard_score_local(_kind(kind), ctypes.byref(sc), q, len(q), s, len(s), int(nshards),
+                                     ctypes.byref(out)) != 0:
+        raise AnySeqError(_err())
+    return out.value
 
 
 def set_device(dev: int) -> None:

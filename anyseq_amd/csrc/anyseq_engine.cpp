@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/anyseq.h"
+#include "anyseq_host.h"
 #include "anyseq_internal.h"
 
 using namespace anyseq;
@@ -41,9 +42,9 @@ hipError_t anyseq_launch_walk(const void* blocks, int nblocks, const uint8_t* Q,
                               const uint8_t* pred, int kind, uint8_t* alq, uint8_t* als, hipStream_t st);
 }
 
-namespace {
+namespace anyseq {
+namespace host {
 
-constexpr int32_t SCORE_MIN_VALUE = -2147483647;  // align.impala:16
 constexpr int32_t SPLIT_UNSET = 0x7fff0000;
 constexpr int MIN_PART_WIDTH_HB = 128;             // align.impala:18
 constexpr int CPU_BLOCK_WIDTH = 1024;              // iteration_cpu.impala:1 (hb_sum stride)
@@ -52,9 +53,7 @@ thread_local std::string g_last_error;
 thread_local double g_fill_ms = 0.0;
 thread_local int g_fill_launches = 0;
 
-struct Failure {
-    std::string msg;
-};
+void set_last_error(const std::string& m) { g_last_error = m; }
 
 [[noreturn]] void fail(const char* fmt, ...) {
     char buf[512];
@@ -65,65 +64,38 @@ struct Failure {
     throw Failure{buf};
 }
 
-#define HIPCHECK(x)                                                                       \
-    do {                                                                                  \
-        hipError_t e_ = (x);                                                              \
-        if (e_ != hipSuccess) fail("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
-    } while (0)
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    void* get(size_t bytes) {
-        if (bytes == 0) bytes = 16;
-        if (bytes > cap) {
-            if (p) HIPCHECK(hipFree(p));
-            p = nullptr;
-            size_t c = std::max(bytes, cap * 3 / 2);
-            c = (c + 255) & ~size_t(255);
-            HIPCHECK(hipMalloc(&p, c));
-            cap = c;
-        }
-        return p;
+void* DevBuf::get(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes > cap) {
+        if (p) HIPCHECK(hipFree(p));
+        p = nullptr;
+        size_t c = std::max(bytes, cap * 3 / 2);
+        c = (c + 255) & ~size_t(255);
+        if (uncached) HIPCHECK(hipExtMallocWithFlags(&p, c, hipDeviceMallocUncached));
+        else HIPCHECK(hipMalloc(&p, c));
+        cap = c;
     }
-};
+    return p;
+}
 
 int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return (v && *v) ? atoi(v) : dflt;
 }
 
-struct Tuning {
-    int R = 1;
-    int CH = 32;
-    int NW = 4;
-    int grid = 0;
-    int fronts = 2;
-    int NWa = 4;    // affine fill: compute waves per workgroup (3 or 4)
-    int grida = 0;  // affine fill: persistent grid (0 = one workgroup per CU)
-    int affasm = 1; // affine fill: asm steady state (0 = C++ blocks only, diagnostics)
-};
+void FillCtx::init() {
+    if (!ev0) HIPCHECK(hipEventCreate(&ev0));
+    if (!ev1) HIPCHECK(hipEventCreate(&ev1));
+}
 
-struct Engine {
-    int device = 0;
-    int num_cus = 256;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::mutex mu;
-    DevBuf q, s, probs, groups, rowbuf, flags, ctr, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq,
-        als;
-    std::vector<int32_t> host_i32;
-
-    explicit Engine(int dev) : device(dev) {
-        HIPCHECK(hipSetDevice(dev));
-        hipDeviceProp_t prop;
-        HIPCHECK(hipGetDeviceProperties(&prop, dev));
-        num_cus = prop.multiProcessorCount;
-        HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        HIPCHECK(hipEventCreate(&ev0));
-        HIPCHECK(hipEventCreate(&ev1));
-    }
-};
+Engine::Engine(int dev) : device(dev) {
+    HIPCHECK(hipSetDevice(dev));
+    hipDeviceProp_t prop;
+    HIPCHECK(hipGetDeviceProperties(&prop, dev));
+    num_cus = prop.multiProcessorCount;
+    HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    fc.init();
+}
 
 std::mutex g_engines_mu;
 std::vector<std::unique_ptr<Engine>> g_engines;
@@ -157,8 +129,12 @@ int waves_per_group() {
 }
 
 // ---------------------------------------------------------------- fill --
-// Runs one batched fill launch over `probs` (host copies; device pointers set).
-void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st) {
+// Prepares one batched fill launch over `probs` (host copies; device pointers set):
+// every allocation, upload and sentinel fill, enqueued on st.  No kernel yet.
+void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
+                  int grid_req) {
+    C.init();
+    C.pending = false;
     const bool aff = fp.affine != 0;
     // the affine fill has one row per lane and hands (G, F) pairs over (twice the row bytes)
     const int R = aff ? 1 : rows_per_lane(), NW = aff ? (g_tuning.NWa == 3 ? 3 : 4) : waves_per_group();
@@ -173,8 +149,8 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
         flag_words += P.ngroups;
         max_groups = std::max(max_groups, P.ngroups);
     }
-    int32_t* rowbuf = (int32_t*)E.rowbuf.get(rowbuf_ints * 4);
-    uint32_t* flags = (uint32_t*)E.flags.get((flag_words + 4) * 4);
+    int32_t* rowbuf = (int32_t*)C.rowbuf.get(rowbuf_ints * 4);
+    uint32_t* flags = (uint32_t*)C.flags.get((flag_words + 4) * 4);
     size_t ro = 0, fo = 0;
     for (auto& P : probs) {
         P.rowbuf = rowbuf + ro;
@@ -187,18 +163,25 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     for (int k = 0; k < max_groups; ++k)
         for (size_t p = 0; p < probs.size(); ++p)
             if (k < probs[p].ngroups) groups.push_back(GroupRef{(int32_t)p, k});
-    if (groups.empty()) return;
-    DPProblem* d_probs = (DPProblem*)E.probs.get(probs.size() * sizeof(DPProblem));
-    GroupRef* d_groups = (GroupRef*)E.groups.get(groups.size() * sizeof(GroupRef));
+    C.R = R;
+    C.NW = NW;
+    if (groups.empty()) {
+        HIPCHECK(hipEventRecord(C.ev0, st));
+        HIPCHECK(hipEventRecord(C.ev1, st));
+        return;
+    }
+    DPProblem* d_probs = (DPProblem*)C.probs.get(probs.size() * sizeof(DPProblem));
+    GroupRef* d_groups = (GroupRef*)C.groups.get(groups.size() * sizeof(GroupRef));
     HIPCHECK(hipMemcpyAsync(d_probs, probs.data(), probs.size() * sizeof(DPProblem), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(d_groups, groups.data(), groups.size() * sizeof(GroupRef), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemsetAsync(flags, 0, flag_words * 4, st));
     // group -> group hand-off rows start as a sentinel (the consumer polls the data):
     // -1 for linear, 0x80808080 for affine
     if (rowbuf_ints) HIPCHECK(hipMemsetAsync(rowbuf, aff ? 0x80 : 0xff, rowbuf_ints * 4, st));
-    uint32_t* ctr = (uint32_t*)E.ctr.get(128);
+    uint32_t* ctr = (uint32_t*)C.ctr.get(128);
     HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));  // ctr[0] = dequeue counter, ctr[1] = error word
     int grid = aff ? (g_tuning.grida > 0 ? g_tuning.grida : E.num_cus) : (g_tuning.grid > 0 ? g_tuning.grid : E.num_cus);
+    if (grid_req > 0) grid = grid_req;
     grid = std::min<int>(grid, (int)groups.size());
     FillParams fpl = fp;
     unsigned long long* dbg = nullptr;
@@ -208,19 +191,46 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
         HIPCHECK(hipMemsetAsync(dbg, 0, 8 * (16 + 4 * 4096), st));
         fpl.dbg = dbg;
     }
-    HIPCHECK(hipEventRecord(E.ev0, st));
-    if (aff)
-        HIPCHECK(anyseq_launch_fill_affine(NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fpl, grid, st));
+    C.stamps = dbg;
+    C.pending = true;
+    C.aff = aff;
+    C.d_probs = d_probs;
+    C.d_groups = d_groups;
+    C.ngroups = (int)groups.size();
+    C.grid = grid;
+    C.fp = fpl;
+    C.st = st;
+}
+
+void fill_launch(FillCtx& C) {
+    if (!C.pending) return;   // nothing to compute (events already recorded)
+    C.pending = false;
+    uint32_t* ctr = (uint32_t*)C.ctr.p;
+    HIPCHECK(hipEventRecord(C.ev0, C.st));
+    if (C.aff)
+        HIPCHECK(anyseq_launch_fill_affine(C.NW, C.d_probs, C.d_groups, C.ngroups, ctr, ctr + 1, &C.fp, C.grid, C.st));
     else
-        HIPCHECK(anyseq_launch_fill(R, g_tuning.CH, NW, d_probs, d_groups, (int)groups.size(), ctr, ctr + 1, &fpl,
-                                    grid, st));
-    HIPCHECK(hipEventRecord(E.ev1, st));
-    HIPCHECK(hipEventSynchronize(E.ev1));
+        HIPCHECK(anyseq_launch_fill(C.R, g_tuning.CH, C.NW, C.d_probs, C.d_groups, C.ngroups, ctr, ctr + 1, &C.fp,
+                                    C.grid, C.st));
+    HIPCHECK(hipEventRecord(C.ev1, C.st));
+}
+
+void fill_async(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
+                int grid_req) {
+    fill_prepare(E, C, probs, fp, st, grid_req);
+    fill_launch(C);
+}
+
+void fill_finish(FillCtx& C) {
+    const int R = C.R, NW = C.NW;
+    unsigned long long* dbg = C.stamps;
+    HIPCHECK(hipEventSynchronize(C.ev1));
     float ms = 0.f;
-    HIPCHECK(hipEventElapsedTime(&ms, E.ev0, E.ev1));
+    HIPCHECK(hipEventElapsedTime(&ms, C.ev0, C.ev1));
     g_fill_ms += ms;
     g_fill_launches += 1;
     uint32_t err = 0;
+    uint32_t* ctr = (uint32_t*)C.ctr.get(128);
     HIPCHECK(hipMemcpy(&err, ctr + 1, 4, hipMemcpyDeviceToHost));
     if (dbg) {
         unsigned long long h[16];
@@ -250,6 +260,11 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     if (err) fail("fill kernel reported error %u (spin timeout)", err);
 }
 
+void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st) {
+    fill_async(E, E.fc, probs, fp, st);
+    fill_finish(E.fc);
+}
+
 FillParams make_params(int kind, const anyseq_scoring& sc) {
     FillParams fp;
     memset(&fp, 0, sizeof fp);
@@ -275,6 +290,8 @@ void check_scoring(int kind, const anyseq_scoring& sc) {
     if (mx > 1024) fail("scoring parameters must be within [-1024, 1024]");
 }
 
+namespace {
+
 // Score of an empty matrix (reference semantics with benchmark restored).
 int64_t empty_score(int kind, int n, int m, const anyseq_scoring& sc) {
     if (kind == KIND_GLOBAL) {
@@ -299,7 +316,7 @@ int64_t score_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* 
     if (sc.gap_open != 0) return score_dev_affine(E, kind, sc, dq, n, ds, m, st);
     const FillParams fp = make_params(kind, sc);
     const int wpad = (m + 63) & ~63;
-    int32_t* res = (int32_t*)E.ctr.get(128) + 4;
+    int32_t* res = (int32_t*)E.fc.ctr.get(128) + 4;
     HIPCHECK(hipMemsetAsync(res, kind == KIND_LOCAL ? 0 : 0x80, 4, st));  // local: 0; else ~INT_MIN
     const bool two_fronts = g_tuning.fronts > 1 && n >= 2 * 64 * rows_per_lane() * waves_per_group();
     std::vector<DPProblem> probs;
@@ -365,7 +382,7 @@ int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const ui
     const FillParams fp = make_params(kind, sc);
     const int wpad = (m + 63) & ~63;
     const int NW = g_tuning.NWa == 3 ? 3 : 4;
-    int32_t* res = (int32_t*)E.ctr.get(128) + 4;
+    int32_t* res = (int32_t*)E.fc.ctr.get(128) + 4;
     HIPCHECK(hipMemsetAsync(res, kind == KIND_LOCAL ? 0 : 0x80, 4, st));
     const bool two = g_tuning.fronts > 1 && n >= 2 * 64 * NW;
     std::vector<DPProblem> probs;
@@ -585,6 +602,10 @@ int64_t abi_construct(int kind, const char* q, int n, const char* s, int m, char
 }
 
 }  // namespace
+}  // namespace host
+}  // namespace anyseq
+
+using namespace anyseq::host;
 
 // ======================================================================= ABI
 extern "C" {

@@ -1,0 +1,111 @@
+// anyseq_host.h — host-side core shared by the engine (anyseq_engine.cpp) and the
+// column-block sharded driver (anyseq_shard.cpp): per-device state, device
+// buffers, error handling, and the asynchronous fill launch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/anyseq.h"
+#include "anyseq_internal.h"
+
+namespace anyseq {
+namespace host {
+
+constexpr int32_t SCORE_MIN_VALUE = -2147483647;  // align.impala:16
+
+struct Failure {
+    std::string msg;
+};
+
+[[noreturn]] void fail(const char* fmt, ...);
+
+#define HIPCHECK(x)                                                                                         \
+    do {                                                                                                    \
+        hipError_t e_ = (x);                                                                                \
+        if (e_ != hipSuccess)                                                                               \
+            ::anyseq::host::fail("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+// Grow-only device buffer.  uncached: MTYPE UC (hipDeviceMallocUncached), for
+// words that a running kernel polls while another kernel or engine writes them:
+// per-XCD L2s are not coherent, an uncached line is never served stale.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool uncached = false;
+    void* get(size_t bytes);
+};
+
+int env_int(const char* name, int dflt);
+
+struct Tuning {
+    int R = 1;
+    int CH = 32;
+    int NW = 4;
+    int grid = 0;
+    int fronts = 2;
+    int NWa = 4;     // affine fill: compute waves per workgroup (3 or 4)
+    int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
+    int affasm = 1;  // affine fill: asm steady state (0 = C++ blocks only, diagnostics)
+};
+extern Tuning g_tuning;
+
+// Buffers and events of one in-flight fill launch (one per concurrently running
+// fill: the engine has one, each local shard of the sharded driver its own).
+struct FillCtx {
+    DevBuf probs, groups, rowbuf, flags, ctr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int R = 1, NW = 4;
+    unsigned long long* stamps = nullptr;   // diagnostic build only
+    // the prepared launch (fill_prepare -> fill_launch)
+    bool pending = false, aff = false;
+    DPProblem* d_probs = nullptr;
+    GroupRef* d_groups = nullptr;
+    int ngroups = 0, grid = 0;
+    FillParams fp{};
+    hipStream_t st = nullptr;
+    void init();
+};
+
+struct Engine {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    FillCtx fc;
+    DevBuf q, s, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq, als;
+    std::vector<int32_t> host_i32;
+    explicit Engine(int dev);
+};
+
+Engine& engine();
+int rows_per_lane();
+int waves_per_group();
+
+FillParams make_params(int kind, const anyseq_scoring& sc);
+void check_scoring(int kind, const anyseq_scoring& sc);
+
+// Enqueues one batched fill over `probs` on `st` (the problems' nbands/ngroups/
+// wpad/rowbuf/flags are filled in here).  grid <= 0: the tuning's grid.
+// fill_prepare does every allocation and upload (allocation and hipFree can
+// synchronise the device, which must not happen while another shard's persistent
+// fill waits for this one) and fill_launch only enqueues the kernel.
+void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
+                  int grid = 0);
+void fill_launch(FillCtx& C);
+void fill_async(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
+                int grid = 0);
+// Waits for the launch of fill_async, accounts its time, checks the error word.
+void fill_finish(FillCtx& C);
+// fill_async + fill_finish on the engine's context.
+void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st);
+
+void set_last_error(const std::string& m);
+
+}  // namespace host
+}  // namespace anyseq

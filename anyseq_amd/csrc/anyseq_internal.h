@@ -34,7 +34,22 @@ struct DPProblem {
     uint32_t* flags;       // ngroups entries, chunk progress of each group's last band
     int32_t* best;         // optional (local): atomicMax of every cell
     int32_t* out_col_e;    // optional (affine): E[r][w-1] (H space) for r in [0,h)
+    // Column-block sharding.  left_in: the left border column
+    // H[r][-1] for r in [0,h), written progressively by the neighbour shard's
+    // transport into a buffer pre-filled with kShardSentinel; the band polls it.
+    // Values are in the sender's frame and move into this problem's frame by
+    // + left_shift.  progress: bands whose out_col rows are complete, bumped in
+    // band order with a system-scope release (the transport stream waits on it).
+    const int32_t* left_in;
+    int32_t left_shift;
+    int32_t pad1;
+    uint32_t* progress;
+    uint32_t* stage;       // diagnostics (ANYSEQ_SHARD_DEBUG): per-band stage reached
 };
+
+// Sentinel of a not-yet-received left-border value (memset byte 0x80): no H value
+// of a supported problem reaches it.
+constexpr int32_t kShardSentinel = (int32_t)0x80808080;
 
 struct GroupRef {
     int32_t prob;

@@ -386,6 +386,51 @@ __device__ __forceinline__ void load_sbytes(const uint8_t* s_ring, int p, uint32
     for (int i = 0; i < CH / 4; ++i) out[i] = __builtin_amdgcn_alignbit(d[i + 1], d[i], sh);
 }
 
+// Column-block sharding: this lane's left-border values H[row][-1] and H[row-1][-1]
+// from the problem's left_in buffer (sentinel-polled; row -1 is the corner, whose
+// value is the scheme's border in every shard frame).  Returns false on timeout.
+__device__ __forceinline__ bool poll_left(const DPProblem& P, int row, int32_t& v1, int32_t& v0, uint32_t* err) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t it = 0;
+    for (;;) {
+        const bool has1 = row < P.h, has0 = row >= 1 && row - 1 < P.h;
+        v1 = has1 ? __hip_atomic_load(gmem(P.left_in) + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        v0 = has0 ? __hip_atomic_load(gmem(P.left_in) + row - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        if (__ballot((has1 && v1 == kShardSentinel) || (has0 && v0 == kShardSentinel)) == 0) break;
+        __builtin_amdgcn_s_sleep(4);
+        if ((++it & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
+            atomicOr(err, ERR_SPIN_TIMEOUT | 2u);
+            return false;
+        }
+    }
+    v1 += P.left_shift;
+    v0 += P.left_shift;
+    return true;
+}
+
+// After a band has stored its out_col rows: publish "band + 1 bands complete" in
+// band order (waits for the band above to publish first), system scope, so the
+// transport stream's hipStreamWaitValue32 and the kernel that sends the rows see
+// the data.  Returns false on timeout.
+__device__ __forceinline__ bool publish_progress(const DPProblem& P, int band, int lane, uint32_t* err) {
+    __threadfence_system();
+    bool ok = true;
+    if (lane == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t it = 0;
+        while (__hip_atomic_load(P.progress, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != (uint32_t)band) {
+            __builtin_amdgcn_s_sleep(2);
+            if ((++it & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
+                atomicOr(err, ERR_SPIN_TIMEOUT | 4u);
+                ok = false;
+                break;
+            }
+        }
+        if (ok) __hip_atomic_store(P.progress, (uint32_t)(band + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return __shfl(ok ? 1 : 0, 0) != 0;
+}
+
 template <int KIND, int R, int X, int CH, bool PARTIAL>
 __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& io, uint32_t* err, const CellK ck,
                          unsigned long long* dbg) {
@@ -410,6 +455,22 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
     // left border grows with the row in G space and keeps the masked prologue.
     constexpr bool VIRT = KIND != KIND_SEMIGLOBAL && R == 1 && X == 0 && !PARTIAL;
     constexpr int kVirtNeg = -(1 << 29);
+    // a shard with a received left column (R = 1 only, enforced by the host) runs
+    // the masked prologue on the received values instead of the virtual one
+    const bool shard_left = P.left_in != nullptr;
+    const bool virt = VIRT && !shard_left;
+    int lv1 = 0, lv0 = 0;   // H[row0][-1], H[row0-1][-1] in kernel value space
+    if (P.stage && lane == 0) P.stage[band] = 1 | ((uint32_t)(__builtin_amdgcn_s_memrealtime() >> 4) & ~7u);
+    if (shard_left) {
+        if (!poll_left(P, row0, lv1, lv0, err)) return;
+        if (P.stage && lane == 0) P.stage[band] = 2;
+        if (KIND != KIND_LOCAL) {
+            lv1 += (row0 + 1) * ng;
+            lv0 += row0 * ng;
+        }
+        if (row0 == 0) lv0 = border_left<KIND>(-1, ng);
+    }
+    auto left_val = [&](int r) { return shard_left ? (r == row0 ? lv1 : lv0) : border_left<KIND>(r, ng); };
     int qv[R];
     bool dead[R];
     int cur[R], prev[R];
@@ -418,13 +479,13 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         const int r = row0 + k;
         dead[k] = r >= h;
         qv[k] = dead[k] ? 0x100 : (int)gmem(P.q)[P.q_off + P.q_step * r];
-        cur[k] = VIRT ? kVirtNeg : border_left<KIND>(r, ng);
+        cur[k] = virt ? kVirtNeg : left_val(r);
         prev[k] = cur[k];
     }
     // settle the query loads here: no global load is in flight inside the block loop
 #pragma unroll
     for (int k = 0; k < R; ++k) asm volatile("" : "+v"(qv[k]));
-    int dg = VIRT ? kVirtNeg : border_left<KIND>(row0 - 1, ng);   // diag of row 0 at its first column
+    int dg = virt ? kVirtNeg : left_val(row0 - 1);   // diag of row 0 at its first column
     int upc = 0;                                 // up of row 0 for the current step
     int outv[CH];
     int best = 0;
@@ -493,7 +554,8 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         return true;
     };
 
-    int top_first = border_left<KIND>(rb - 1, ng);
+    // lane 0's top value at column -1: H[rb-1][-1] (lane 0 of a shard holds it in lv0)
+    int top_first = shard_left ? __shfl(lv0, 0) : border_left<KIND>(rb - 1, ng);
     // full blocks end at fe (they start at 0 for VIRT, at D / CH otherwise)
     const int fe = w + BASE >= CH ? (w + BASE - CH) / CH + 1 : 0;
     LoopArgs la;
@@ -517,7 +579,7 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
     }
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
-        const bool full = (VIRT || t0 >= D) && (t0 + CH <= w + BASE);
+        const bool full = (virt || t0 >= D) && (t0 + CH <= w + BASE);
         if constexpr (ASM) {
             if (full && !(ANYSEQ_EXP & 32)) {
 #ifdef ANYSEQ_STAMPS
@@ -590,9 +652,12 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
             if (full)
                 band_block<KIND, R, X, CH, false, PARTIAL>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev, upc,
                                                            dg, outv, best, ck);
-            else
+            else if (virt)
                 band_block<KIND, R, X, CH, true, PARTIAL, VIRT>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev,
                                                                 upc, dg, outv, best, ck);
+            else
+                band_block<KIND, R, X, CH, true, PARTIAL, false>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev,
+                                                                 upc, dg, outv, best, ck);
             top_first = rv[CH - 1];
             if (pub && lane == 63 && !(ANYSEQ_EXP & 4)) {
                 int4* dst = reinterpret_cast<int4*>(io.next_ring + ((j * CH) & IRM));
@@ -631,6 +696,9 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
             if (r < h) gmem(P.out_col)[r] = to_h<KIND>(cur[k], r, w - 1, ng);
         }
     }
+    if (P.stage && lane == 0) P.stage[band] = 3;
+    if (P.progress && !publish_progress(P, band, lane, err)) return;
+    if (P.stage && lane == 0) P.stage[band] = 4 | ((uint32_t)(__builtin_amdgcn_s_memrealtime() >> 4) & ~7u);
     if (KIND == KIND_LOCAL && P.best) {
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
@@ -784,7 +852,7 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
         if (!progress) {
             __builtin_amdgcn_s_sleep(1);
             if ((++idle & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t_start > SPIN_TICKS || err_set(err))) {
-                atomicOr(err, ERR_SPIN_TIMEOUT);
+                atomicOr(err, ERR_SPIN_TIMEOUT | 8u);
                 lds_st(prod0, (uint32_t)nchunks);
                 lds_st(s_filled, (uint32_t)nchunks);
                 return;
@@ -1369,6 +1437,42 @@ __global__ void front_combine_kernel(int kind, const int32_t* __restrict__ rowF,
     if ((threadIdx.x & 63) == 0) atomicMax(out, best);
 }
 
+// Column-block shard combine: the two-front split of
+// front_combine_kernel restricted to one shard's columns [c0, c0+w).  Split
+// columns j in [-1, w-1) (+ j = w-1 on the last shard): F = top front's last row
+// at local column j (j = -1: the received left column lT[h1-1] + sT, or the
+// scheme border on shard 0), B = bottom front's last row at reversed local column
+// w-2-j (-1: the bottom front's received column lB[h2-1] + sB, or the border on
+// the last shard).  adj moves the sum from the two shard frames to the true
+// score.  Semiglobal adds the end columns colT (last shard) / colB (shard 0).
+__global__ void shard_combine_kernel(int kind, const int32_t* __restrict__ rowT, int h1,
+                                     const int32_t* __restrict__ rowB, int h2, int w, int gap,
+                                     const int32_t* __restrict__ lT, int sT, const int32_t* __restrict__ lB, int sB,
+                                     int last, const int32_t* __restrict__ colT, const int32_t* __restrict__ colB,
+                                     int adj, int32_t* out) {
+    const int ng = -gap;
+    auto init = [&](int i) { return kind == KIND_GLOBAL ? (i + 1) * gap : 0; };
+    auto toh = [&](int v, int r, int c) { return kind == KIND_LOCAL ? v : v - (r + c + 2) * ng; };
+    int best = kind == KIND_SEMIGLOBAL ? 0 : -2147483647;
+    const int jend = last ? w : w - 1;
+    for (int j = (int)(threadIdx.x + blockIdx.x * blockDim.x) - 1; j < jend; j += blockDim.x * gridDim.x) {
+        const int F = j >= 0 ? toh(rowT[j], h1 - 1, j) : (lT ? lT[h1 - 1] + sT : init(h1 - 1));
+        const int jb = w - 2 - j;
+        const int B = jb >= 0 ? toh(rowB[jb], h2 - 1, jb) : (lB ? lB[h2 - 1] + sB : init(h2 - 1));
+        best = max(best, F + B + adj);
+    }
+    if (kind == KIND_SEMIGLOBAL) {
+        if (colT)
+            for (int i = threadIdx.x + blockIdx.x * blockDim.x; i < h1; i += blockDim.x * gridDim.x)
+                best = max(best, colT[i]);
+        if (colB)
+            for (int i = threadIdx.x + blockIdx.x * blockDim.x; i < h2; i += blockDim.x * gridDim.x)
+                best = max(best, colB[i]);
+    }
+    for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, best);
+}
+
 // ---------------------------------------------------------------- hb_sum --
 // Stage 1: one thread per (part, stride class) — traceback_lintime.impala:56-96.
 __global__ void hb_sum_stage1(const PartInfo* __restrict__ parts, int nparts, int bpp, int half,
@@ -1631,6 +1735,15 @@ hipError_t anyseq_launch_front_combine(int kind, const int32_t* rowF, int h1, co
                                        hipStream_t st) {
     hipLaunchKernelGGL(anyseq::front_combine_kernel, dim3(64), dim3(256), 0, st, kind, rowF, h1, rowB, h2, m, gap,
                        colF, colB, out);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_shard_combine(int kind, const int32_t* rowT, int h1, const int32_t* rowB, int h2, int w,
+                                       int gap, const int32_t* lT, int sT, const int32_t* lB, int sB, int last,
+                                       const int32_t* colT, const int32_t* colB, int adj, int32_t* out,
+                                       hipStream_t st) {
+    hipLaunchKernelGGL(anyseq::shard_combine_kernel, dim3(64), dim3(256), 0, st, kind, rowT, h1, rowB, h2, w, gap, lT,
+                       sT, lB, sB, last, colT, colB, adj, out);
     return hipGetLastError();
 }
 

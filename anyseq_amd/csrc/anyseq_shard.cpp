@@ -1,0 +1,649 @@
+// anyseq_shard.cpp — column-block sharded score fill.
+//
+// The matrix is split into contiguous subject column blocks, one per shard:
+// shard g owns columns [c0_g, c0_g + w_g), query replicated.  Each shard runs the
+// two-front fill of score_dev on its block:
+//   * the top front (rows [0, h1), forward) needs H[r][c0_g - 1] from shard g-1
+//     and sends its own last column to shard g+1;
+//   * the bottom front (rows [h1, n), query and subject reversed) flows the other
+//     way: it needs the column c0_g + w_g from shard g+1 and sends its first
+//     column to shard g-1.
+// A front's band publishes its last-column rows (out_col) and then bumps a
+// progress counter in signal memory in band order (publish_progress); the
+// transport stream of that front waits on the counter (hipStreamWaitValue32) and
+// ships each chunk of rows to the neighbour, whose band polls the sentinel-filled
+// left_in buffer (poll_left).  No host thread sits in the loop.
+//
+// Two transports:
+//   * RCCL (one process per GPU, anyseq_shard_init): ncclSend / ncclRecv over
+//     xGMI, four communicators so that every communicator is used by exactly one
+//     stream of a rank (top/bottom direction x link parity);
+//   * local (anyseq_shard_score_local): several shards in one process on one
+//     device, hipMemcpyAsync between them -- the same kernels, counters and
+//     chunk protocol, runnable on a single GPU (parity tests).
+// The per-shard combine (shard_combine_kernel) gives every shard's best split
+// candidate in true-score units; RCCL reduces them with a MAX all-reduce.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "anyseq_host.h"
+
+extern "C" hipError_t anyseq_launch_shard_combine(int kind, const int32_t* rowT, int h1, const int32_t* rowB, int h2,
+                                                  int w, int gap, const int32_t* lT, int sT, const int32_t* lB,
+                                                  int sB, int last, const int32_t* colT, const int32_t* colB, int adj,
+                                                  int32_t* out, hipStream_t st);
+
+namespace anyseq {
+namespace host {
+namespace {
+
+#define NCCLCHECK(x)                                                                                   \
+    do {                                                                                               \
+        ncclResult_t r_ = (x);                                                                         \
+        if (r_ != ncclSuccess) fail("%s failed: %s (%s:%d)", #x, ncclGetErrorString(r_), __FILE__, __LINE__); \
+    } while (0)
+
+constexpr int kComms = 4;   // top even/odd links, bottom even/odd links
+
+// Transport trigger: by default a host thread per direction polls the progress
+// counter in pinned host memory and issues each chunk's transfer; with
+// ANYSEQ_SHARD_WAITVALUE=1 the chunk transfers are enqueued up front behind
+// hipStreamWaitValue32 on signal memory.  ANYSEQ_SHARD_DIRECT=1 (local shards
+// only): the receiver polls the sender's out_col itself, no transfer at all.
+bool use_wait_value() { return env_int("ANYSEQ_SHARD_WAITVALUE", 0) != 0; }
+bool use_direct() { return env_int("ANYSEQ_SHARD_DIRECT", 0) != 0; }
+
+
+struct Front {
+    DevBuf out_col, left_in, out_row;
+    uint32_t* progress = nullptr;     // device view of the counter (what the kernel bumps)
+    uint32_t* progress_h = nullptr;   // host view (pinned, coherent) -- host-poll transport
+    uint32_t* progress_sig = nullptr; // signal memory -- hipStreamWaitValue32 transport
+    hipStream_t s_send = nullptr, s_recv = nullptr;
+    int h = 0;
+};
+
+struct Shard {
+    int g = 0, c0 = 0, w = 0;
+    hipStream_t st = nullptr;
+    hipEvent_t ready = nullptr;
+    FillCtx fc;
+    Front top, bot;
+    DevBuf res;
+    const int32_t* lT = nullptr;   // where the fronts read their received columns (combine reads them too)
+    const int32_t* lB = nullptr;
+    void init() {
+        if (st) return;
+        // polled across kernels / XCDs: never L2-cached (see DevBuf::uncached)
+        for (Front* f : {&top, &bot}) f->out_col.uncached = f->left_in.uncached = true;
+        HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIPCHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        for (Front* f : {&top, &bot}) {
+            void* p = nullptr;
+            HIPCHECK(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+            f->progress_h = (uint32_t*)p;
+            void* d = nullptr;
+            HIPCHECK(hipHostGetDevicePointer(&d, p, 0));
+            HIPCHECK(hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory));
+            f->progress_sig = (uint32_t*)p;
+            f->progress = use_wait_value() ? f->progress_sig : (uint32_t*)d;
+        }
+        fc.init();
+    }
+};
+
+// Transport streams are created on first use: every stream of the process needs a
+// hardware queue of its own.  HIP multiplexes streams over GPU_MAX_HW_QUEUES
+// queues (default 4), and a queue is in-order: a transfer queued behind the
+// persistent fill kernel (or behind another direction's stream wait) would never
+// run while the fill waits for it.
+hipStream_t lazy_stream(hipStream_t& s) {
+    if (!s) HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+}
+
+void check_hw_queues(int streams) {
+    // this process's streams: the engine's, torch's null stream, the shards' fill and transport streams
+    const int need = streams + 2;
+    const int have = env_int("GPU_MAX_HW_QUEUES", 4);
+    if (have < need)
+        fail("the sharded fill runs %d concurrent streams: set GPU_MAX_HW_QUEUES >= %d (<= 32) in the environment "
+             "before the first HIP call (it is %d); streams sharing a hardware queue would deadlock behind the "
+             "persistent fill kernel", streams, need, have);
+}
+
+// Column block of shard g of N over m columns (balanced, contiguous).
+inline int block_c0(int g, int N, int m) { return (int)((int64_t)g * m / N); }
+
+struct RcclState {
+    int rank = -1, world = 0;
+    ncclComm_t comm[kComms] = {};
+    Shard shard;
+    // resident inputs of this rank (anyseq_shard_load)
+    DevBuf q, s;
+    int n = 0, m = 0, c0 = 0, w = 0;
+};
+std::unique_ptr<RcclState> g_rccl;
+
+int chunk_rows() {
+    const int c = env_int("ANYSEQ_SHARD_CHUNK", 1024);
+    return std::max(64, c / 64 * 64);
+}
+
+// Host-side wait with a deadline: a lost message must not hang the caller.
+void wait_stream(hipStream_t s, double seconds, const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) fail("%s: %s", what, hipGetErrorString(e));
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > seconds)
+            fail("%s: timed out after %.0f s", what, seconds);
+        std::this_thread::yield();
+    }
+}
+
+// Per-step setup of one shard: problems, sentinel buffers, counters.
+void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds_block,
+                 int m, std::vector<DPProblem>& probs, int& h1, int& h2, bool direct = false) {
+    h1 = n / 2;
+    h2 = n - h1;
+    const int g = S.g, w = S.w;
+    const int wpad = (w + 63) & ~63;
+    const bool has_left = g > 0, has_right = g < N - 1;
+    const int ng = -sc.gap_extend;
+    S.top.h = h1;
+    S.bot.h = h2;
+    int32_t* rowT = (int32_t*)S.top.out_row.get((size_t)wpad * 4);
+    int32_t* rowB = (int32_t*)S.bot.out_row.get((size_t)wpad * 4);
+    // out_col: sent downstream; also the semiglobal end column on the edge shards
+    int32_t* colT = (int32_t*)S.top.out_col.get((size_t)h1 * 4);
+    int32_t* colB = (int32_t*)S.bot.out_col.get((size_t)h2 * 4);
+    int32_t* inT = has_left ? (int32_t*)S.top.left_in.get((size_t)h1 * 4) : nullptr;
+    int32_t* inB = has_right ? (int32_t*)S.bot.left_in.get((size_t)h2 * 4) : nullptr;
+    if (inT) HIPCHECK(hipMemsetAsync(inT, 0x80, (size_t)h1 * 4, S.st));
+    if (inB) HIPCHECK(hipMemsetAsync(inB, 0x80, (size_t)h2 * 4, S.st));
+    if (direct) {   // local direct mode: the neighbours poll these columns themselves
+        HIPCHECK(hipMemsetAsync(colT, 0x80, (size_t)h1 * 4, S.st));
+        HIPCHECK(hipMemsetAsync(colB, 0x80, (size_t)h2 * 4, S.st));
+    }
+    for (Front* f : {&S.top, &S.bot}) {
+        if (use_wait_value()) HIPCHECK(hipMemsetAsync(f->progress, 0, 4, S.st));
+        else __atomic_store_n(f->progress_h, 0u, __ATOMIC_RELEASE);   // before the launch below
+    }
+    HIPCHECK(hipEventRecord(S.ready, S.st));
+    for (Front* f : {&S.top, &S.bot}) {
+        if (f->s_send) HIPCHECK(hipStreamWaitEvent(f->s_send, S.ready, 0));
+        if (f->s_recv) HIPCHECK(hipStreamWaitEvent(f->s_recv, S.ready, 0));
+    }
+    // frames: a shard's top border is the scheme's, so global values are shifted by
+    // the shard's column offset; a received column moves by the sender's width
+    const int shT = (kind == KIND_GLOBAL && has_left) ? block_c0(g, N, m) - block_c0(g - 1, N, m) : 0;
+    const int shB = (kind == KIND_GLOBAL && has_right) ? block_c0(g + 2, N, m) - block_c0(g + 1, N, m) : 0;
+    DPProblem P;
+    memset(&P, 0, sizeof P);
+    P.q = dq;
+    P.s = ds_block;
+    P.q_step = 1;
+    P.s_step = 1;
+    P.w = w;
+    P.h = h1;
+    P.out_row = rowT;
+    P.out_col = colT;
+    P.left_in = inT;
+    S.lT = inT;
+    S.lB = inB;
+    P.left_shift = shT * ng;
+    P.progress = S.top.progress;
+    probs.push_back(P);
+    P.q_off = n - 1;
+    P.q_step = -1;
+    P.s_off = w - 1;
+    P.s_step = -1;
+    P.h = h2;
+    P.out_row = rowB;
+    P.out_col = colB;
+    P.left_in = inB;
+    P.left_shift = shB * ng;
+    P.progress = S.bot.progress;
+    probs.push_back(P);
+}
+
+// Bands of rows [0, r1) of a front: chunk k of rows is shipped once they are done.
+inline uint32_t bands_for_rows(int r1) { return (uint32_t)((r1 + 63) / 64); }
+
+// One direction of one front: wait for the sender's progress, ship each chunk.
+// Runs on its own host thread (hipStreamWaitValue32 may block the calling
+// thread on some runtimes; a thread per direction never orders one direction's
+// wait before another direction's enqueue).
+struct Xfer {
+    int device = 0;
+    Front* src = nullptr;
+    int32_t* dst = nullptr;         // local transport: the neighbour's left_in
+    ncclComm_t comm = nullptr;      // RCCL transport
+    int peer = -1;
+    bool recv = false;              // RCCL: receive into dst instead of sending
+    int h = 0;
+    std::string error;
+};
+
+void run_xfer(Xfer* x) {
+    try {
+        HIPCHECK(hipSetDevice(x->device));
+        const int CR = chunk_rows();
+        for (int r0 = 0; r0 < x->h; r0 += CR) {
+            const int r1 = std::min(x->h, r0 + CR);
+            if (x->recv) {
+                NCCLCHECK(ncclRecv(x->dst + r0, (size_t)(r1 - r0), ncclInt32, x->peer, x->comm, x->src->s_recv));
+                continue;
+            }
+            const uint32_t need = bands_for_rows(r1);
+            if (use_wait_value()) {
+                HIPCHECK(hipStreamWaitValue32(x->src->s_send, x->src->progress, need, hipStreamWaitValueGte,
+                                              0xffffffffu));
+            } else {
+                const auto t0 = std::chrono::steady_clock::now();
+                while (__atomic_load_n(x->src->progress_h, __ATOMIC_ACQUIRE) < need) {
+                    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 120.0)
+                        fail("shard transport: no progress from the fill (chunk rows %d..%d)", r0, r1);
+                    std::this_thread::yield();
+                }
+            }
+            const int32_t* src = (const int32_t*)x->src->out_col.p + r0;
+            if (x->comm)
+                NCCLCHECK(ncclSend(src, (size_t)(r1 - r0), ncclInt32, x->peer, x->comm, x->src->s_send));
+            else
+                HIPCHECK(hipMemcpyAsync(x->dst + r0, src, (size_t)(r1 - r0) * 4, hipMemcpyDeviceToDevice,
+                                        x->src->s_send));
+        }
+    } catch (const Failure& f) {
+        x->error = f.msg;
+    }
+}
+
+// Starts every transfer on its own thread; returns the threads to join.
+std::vector<std::thread> start_xfers(std::vector<Xfer>& xs) {
+    std::vector<std::thread> th;
+    for (Xfer& x : xs) th.emplace_back(run_xfer, &x);
+    return th;
+}
+
+// After the fills ended: a failed fill never reaches its progress targets, so
+// release every counter (waiting transfers then drain), join, report.
+void finish_xfers(std::vector<std::thread>& th, std::vector<Xfer>& xs, std::vector<Shard*> shards, bool fill_ok) {
+    if (!fill_ok)
+        for (Shard* S : shards)
+            for (Front* f : {&S->top, &S->bot}) {
+                const uint32_t big = 0x7fffffffu;
+                if (use_wait_value()) (void)hipMemcpy(f->progress, &big, 4, hipMemcpyHostToDevice);
+                else __atomic_store_n(f->progress_h, big, __ATOMIC_RELEASE);
+            }
+    for (auto& t : th) t.join();
+    for (auto& x : xs)
+        if (!x.error.empty()) fail("shard transport: %s", x.error.c_str());
+}
+
+std::vector<Xfer> local_xfers(std::vector<Shard>& shards, int N, int device) {
+    std::vector<Xfer> xs;
+    for (int g = 0; g < N; ++g) {
+        Shard& S = shards[g];
+        if (g + 1 < N) {   // top: g -> g+1
+            Xfer x;
+            x.device = device;
+            x.src = &S.top;
+            x.dst = (int32_t*)shards[g + 1].top.left_in.p;
+            x.h = S.top.h;
+            xs.push_back(x);
+        }
+        if (g > 0) {       // bottom: g -> g-1
+            Xfer x;
+            x.device = device;
+            x.src = &S.bot;
+            x.dst = (int32_t*)shards[g - 1].bot.left_in.p;
+            x.h = S.bot.h;
+            xs.push_back(x);
+        }
+    }
+    return xs;
+}
+
+std::vector<Xfer> rccl_xfers(RcclState& R, int device) {
+    Shard& S = R.shard;
+    const int g = R.rank, N = R.world;
+    std::vector<Xfer> xs;
+    // link a joins ranks a and a+1: top data a -> a+1 on comm[a % 2], bottom data
+    // a+1 -> a on comm[2 + a % 2]; every communicator is used by one stream per rank
+    auto add = [&](Front* f, bool recv, int peer, ncclComm_t c) {
+        Xfer x;
+        x.device = device;
+        x.src = f;
+        x.recv = recv;
+        x.peer = peer;
+        x.comm = c;
+        x.dst = recv ? (int32_t*)f->left_in.p : nullptr;
+        x.h = f->h;
+        xs.push_back(x);
+    };
+    if (g > 0) {
+        add(&S.top, true, g - 1, R.comm[(g - 1) % 2]);
+        add(&S.bot, false, g - 1, R.comm[2 + (g - 1) % 2]);
+    }
+    if (g < N - 1) {
+        add(&S.top, false, g + 1, R.comm[g % 2]);
+        add(&S.bot, true, g + 1, R.comm[2 + g % 2]);
+    }
+    return xs;
+}
+
+// Combine of one shard into *res (true-score units).
+void enqueue_combine(Shard& S, int N, int kind, const anyseq_scoring& sc, int m, int h1, int h2, int32_t* res) {
+    const int g = S.g, w = S.w;
+    const int gap = sc.gap_extend;
+    const int shT = (kind == KIND_GLOBAL && g > 0) ? (block_c0(g, N, m) - block_c0(g - 1, N, m)) * -gap : 0;
+    const int shB = (kind == KIND_GLOBAL && g < N - 1) ? (block_c0(g + 2, N, m) - block_c0(g + 1, N, m)) * -gap : 0;
+    // top frame: H_true = H + c0 gap; bottom frame (reversed): H_true = H + (m - c0 - w) gap
+    const int adj = kind == KIND_GLOBAL ? (m - w) * gap : 0;
+    const int32_t* colT = (kind == KIND_SEMIGLOBAL && g == N - 1) ? (const int32_t*)S.top.out_col.p : nullptr;
+    const int32_t* colB = (kind == KIND_SEMIGLOBAL && g == 0) ? (const int32_t*)S.bot.out_col.p : nullptr;
+    HIPCHECK(anyseq_launch_shard_combine(kind, (const int32_t*)S.top.out_row.p, h1, (const int32_t*)S.bot.out_row.p,
+                                         h2, w, gap, S.lT, shT, S.lB, shB,
+                                         g == N - 1 ? 1 : 0, colT, colB, adj, res, S.st));
+}
+
+void check_shard_shape(int kind, const anyseq_scoring& sc, int n, int m, int N) {
+    check_scoring(kind, sc);
+    if (sc.gap_open != 0) fail("sharded fill: affine gaps are not supported yet (linear only)");
+    if (N < 1) fail("sharded fill: need at least one shard");
+    if (n < 2) fail("sharded fill: need at least 2 query rows (two fronts), got %d", n);
+    if (m < N) fail("sharded fill: %d columns cannot be split over %d shards", m, N);
+    if (g_tuning.R != 1) fail("sharded fill: rows_per_lane must be 1");
+}
+
+int grid_per_shard(const Engine& E, int nshards) {
+    // leave CUs for the transport (RCCL kernels / copy blits) next to the persistent fills
+    return std::max(8, (E.num_cus - 16) / nshards);
+}
+
+int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m, int N) {
+    check_shard_shape(kind, sc, n, m, N);
+    Engine& E = engine();
+    std::lock_guard<std::mutex> lk(E.mu);
+    static std::vector<Shard> shards;   // kept: streams, counters, buffers are reused
+    if ((int)shards.size() < N) shards.resize(N);
+    uint8_t* dq = (uint8_t*)E.q.get((size_t)n);
+    uint8_t* ds = (uint8_t*)E.s.get((size_t)m);
+    HIPCHECK(hipMemcpy(dq, q, (size_t)n, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(ds, s, (size_t)m, hipMemcpyHostToDevice));
+    const bool direct = use_direct();
+    check_hw_queues(direct || N == 1 ? N : 3 * N - 2);
+    for (int g = 0; g < N; ++g) {
+        shards[g].init();
+        if (direct) continue;
+        if (g + 1 < N) lazy_stream(shards[g].top.s_send);
+        if (g > 0) lazy_stream(shards[g].bot.s_send);
+    }
+    int32_t* res = (int32_t*)E.fc.ctr.get(128) + 4;
+    HIPCHECK(hipMemset(res, kind == KIND_LOCAL ? 0 : 0x80, 4));
+    const FillParams fp = make_params(kind, sc);
+    std::vector<std::vector<DPProblem>> probs(N);
+    int h1 = 0, h2 = 0;
+    for (int g = 0; g < N; ++g) {
+        Shard& S = shards[g];
+        S.init();
+        S.g = g;
+        S.c0 = block_c0(g, N, m);
+        S.w = block_c0(g + 1, N, m) - S.c0;
+        setup_shard(S, N, kind, sc, dq, n, ds + S.c0, m, probs[g], h1, h2, direct);
+        if (kind == KIND_LOCAL) {
+            probs[g][0].best = res;
+            probs[g][1].best = res;
+        }
+    }
+    if (direct) {
+        // each shard polls its neighbours' out_col: every sentinel fill precedes every fill
+        for (int g = 0; g < N; ++g) {
+            if (g > 0) shards[g].lT = probs[g][0].left_in = (const int32_t*)shards[g - 1].top.out_col.p;
+            if (g + 1 < N) shards[g].lB = probs[g][1].left_in = (const int32_t*)shards[g + 1].bot.out_col.p;
+            for (int k = 0; k < N; ++k)
+                if (k != g) HIPCHECK(hipStreamWaitEvent(shards[g].st, shards[k].ready, 0));
+        }
+    }
+    // a copy lands in the neighbour's left_in: it must follow that shard's sentinel fill
+    for (int g = 0; g < N; ++g)
+        for (int k = 0; k < N; ++k)
+            if (k != g) {
+                if (shards[g].top.s_send) HIPCHECK(hipStreamWaitEvent(shards[g].top.s_send, shards[k].ready, 0));
+                if (shards[g].bot.s_send) HIPCHECK(hipStreamWaitEvent(shards[g].bot.s_send, shards[k].ready, 0));
+            }
+    static DevBuf stage_buf;
+    uint32_t* stage = nullptr;
+    const int nbmax = (n + 63) / 64 + 1;
+    if (env_int("ANYSEQ_SHARD_DEBUG", 0)) {
+        stage = (uint32_t*)stage_buf.get((size_t)N * 2 * nbmax * 4);
+        HIPCHECK(hipMemset(stage, 0, (size_t)N * 2 * nbmax * 4));
+        for (int g = 0; g < N; ++g)
+            for (int f = 0; f < 2; ++f) probs[g][f].stage = stage + (g * 2 + f) * nbmax;
+    }
+    const int grid = grid_per_shard(E, N);
+    // every shard's allocations and uploads first: the fills wait for each other once launched
+    for (int g = 0; g < N; ++g) fill_prepare(E, shards[g].fc, probs[g], fp, shards[g].st, grid);
+    for (int g = 0; g < N; ++g) fill_launch(shards[g].fc);
+    std::vector<Xfer> xs = direct ? std::vector<Xfer>() : local_xfers(shards, N, E.device);
+    std::vector<std::thread> th = start_xfers(xs);
+    std::vector<Shard*> sp;
+    for (int g = 0; g < N; ++g) sp.push_back(&shards[g]);
+    bool ok = true;
+    std::string err;
+    for (int g = 0; g < N; ++g) {
+        try {
+            wait_stream(shards[g].st, 120.0, "sharded fill");
+            fill_finish(shards[g].fc);
+        } catch (const Failure& f) {
+            ok = false;
+            if (err.empty()) err = f.msg;
+        }
+    }
+    if (!ok && stage) {
+        std::vector<uint32_t> st((size_t)N * 2 * nbmax);
+        (void)hipMemcpy(st.data(), stage, st.size() * 4, hipMemcpyDeviceToHost);
+        for (int g = 0; g < N; ++g)
+            for (int f = 0; f < 2; ++f) {
+                fprintf(stderr, "shard %d front %d stages:", g, f);
+                for (int b = 0; b < (f ? h2 : h1 + 63) / 64 + (f ? 1 : 0) && b < nbmax; ++b)
+                    fprintf(stderr, " %u@%.1fus", st[(g * 2 + f) * nbmax + b] & 7u,
+                            (double)((st[(g * 2 + f) * nbmax + b] & ~7u) - (st[0] & ~7u)) * 0.16);
+                fprintf(stderr, "\n");
+            }
+    }
+    if (!ok && env_int("ANYSEQ_SHARD_DEBUG", 0)) {
+        for (int g = 0; g < N; ++g)
+            for (Front* f : {&shards[g].top, &shards[g].bot}) {
+                uint32_t pv = 0;
+                pv = use_wait_value() ? 0u : __atomic_load_n(f->progress_h, __ATOMIC_ACQUIRE);
+                if (use_wait_value()) (void)hipMemcpy(&pv, f->progress, 4, hipMemcpyDeviceToHost);
+                int32_t lv[4] = {0, 0, 0, 0}, oc[4] = {0, 0, 0, 0};
+                if (f->left_in.p) (void)hipMemcpy(lv, f->left_in.p, 4 * std::min(4, f->h), hipMemcpyDeviceToHost);
+                (void)hipMemcpy(oc, f->out_col.p, 4 * std::min(4, f->h), hipMemcpyDeviceToHost);
+                fprintf(stderr, "shard %d %s: progress %u left_in %d %d %d %d out_col %d %d %d %d\n", g,
+                        f == &shards[g].top ? "top" : "bot", pv, lv[0], lv[1], lv[2], lv[3], oc[0], oc[1], oc[2],
+                        oc[3]);
+            }
+    }
+    finish_xfers(th, xs, sp, ok);
+    if (!ok) fail("%s", err.c_str());
+    for (int g = 0; g < N; ++g)
+        for (Front* f : {&shards[g].top, &shards[g].bot})
+            if (f->s_send) wait_stream(f->s_send, 30.0, "shard transport");
+    for (int g = 0; g < N; ++g) enqueue_combine(shards[g], N, kind, sc, m, h1, h2, res);
+    int32_t v = 0;
+    for (int g = 0; g < N; ++g) HIPCHECK(hipStreamSynchronize(shards[g].st));
+    HIPCHECK(hipMemcpy(&v, res, 4, hipMemcpyDeviceToHost));
+    return v;
+}
+
+int64_t shard_score_rccl(int kind, const anyseq_scoring& sc) {
+    if (!g_rccl || g_rccl->rank < 0) fail("anyseq_shard_init has not been called");
+    RcclState& R = *g_rccl;
+    if (R.n <= 0) fail("anyseq_shard_load has not been called");
+    check_shard_shape(kind, sc, R.n, R.m, R.world);
+    Engine& E = engine();
+    std::lock_guard<std::mutex> lk(E.mu);
+    Shard& S = R.shard;
+    S.init();
+    check_hw_queues(1 + 2 * ((R.rank > 0) + (R.rank < R.world - 1)));
+    if (R.rank > 0) {
+        lazy_stream(S.top.s_recv);
+        lazy_stream(S.bot.s_send);
+    }
+    if (R.rank < R.world - 1) {
+        lazy_stream(S.top.s_send);
+        lazy_stream(S.bot.s_recv);
+    }
+    S.g = R.rank;
+    S.c0 = R.c0;
+    S.w = R.w;
+    int32_t* res = (int32_t*)S.res.get(64);
+    HIPCHECK(hipMemsetAsync(res, kind == KIND_LOCAL ? 0 : 0x80, 4, S.st));
+    const FillParams fp = make_params(kind, sc);
+    std::vector<DPProblem> probs;
+    int h1 = 0, h2 = 0;
+    setup_shard(S, R.world, kind, sc, (const uint8_t*)R.q.p, R.n, (const uint8_t*)R.s.p, R.m, probs, h1, h2);
+    if (kind == KIND_LOCAL) {
+        probs[0].best = res;
+        probs[1].best = res;
+    }
+    fill_async(E, S.fc, probs, fp, S.st, grid_per_shard(E, 1));
+    std::vector<Xfer> xs = rccl_xfers(R, E.device);
+    std::vector<std::thread> th = start_xfers(xs);
+    bool ok = true;
+    std::string err;
+    try {
+        wait_stream(S.st, 300.0, "sharded fill");
+        fill_finish(S.fc);
+    } catch (const Failure& f) {
+        ok = false;
+        err = f.msg;
+    }
+    finish_xfers(th, xs, {&S}, ok);
+    if (!ok) fail("%s", err.c_str());
+    for (hipStream_t t : {S.top.s_send, S.top.s_recv, S.bot.s_send, S.bot.s_recv})
+        if (t) wait_stream(t, 60.0, "shard transport");
+    enqueue_combine(S, R.world, kind, sc, R.m, h1, h2, res);
+    NCCLCHECK(ncclAllReduce(res, res, 1, ncclInt32, ncclMax, R.comm[0], S.st));
+    int32_t v = 0;
+    HIPCHECK(hipMemcpyAsync(&v, res, 4, hipMemcpyDeviceToHost, S.st));
+    wait_stream(S.st, 60.0, "score all-reduce");
+    return v;
+}
+
+}  // namespace
+}  // namespace host
+}  // namespace anyseq
+
+using namespace anyseq::host;
+
+extern "C" {
+
+int anyseq_shard_unique_ids(void* out, int count) {
+    try {
+        for (int i = 0; i < count; ++i) {
+            ncclUniqueId id;
+            NCCLCHECK(ncclGetUniqueId(&id));
+            memcpy((char*)out + (size_t)i * NCCL_UNIQUE_ID_BYTES, &id, NCCL_UNIQUE_ID_BYTES);
+        }
+        return 0;
+    } catch (const Failure& f) {
+        set_last_error(f.msg);
+        return -1;
+    }
+}
+
+int anyseq_shard_init(int rank, int world, const void* ids, int count) {
+    try {
+        if (count < kComms) fail("anyseq_shard_init needs %d unique ids, got %d", kComms, count);
+        if (world < 1 || rank < 0 || rank >= world) fail("bad rank %d / world %d", rank, world);
+        engine();   // selects the device
+        g_rccl.reset(new RcclState);
+        g_rccl->rank = rank;
+        g_rccl->world = world;
+        for (int i = 0; i < kComms; ++i) {
+            ncclUniqueId id;
+            memcpy(&id, (const char*)ids + (size_t)i * NCCL_UNIQUE_ID_BYTES, NCCL_UNIQUE_ID_BYTES);
+            NCCLCHECK(ncclCommInitRank(&g_rccl->comm[i], world, id, rank));
+        }
+        return 0;
+    } catch (const Failure& f) {
+        set_last_error(f.msg);
+        return -1;
+    }
+}
+
+int anyseq_shard_load(const char* query, int lenq, const char* subject_block, int w, int c0, int lens) {
+    try {
+        if (!g_rccl || g_rccl->rank < 0) fail("anyseq_shard_init has not been called");
+        RcclState& R = *g_rccl;
+        if (c0 != block_c0(R.rank, R.world, lens) || w != block_c0(R.rank + 1, R.world, lens) - c0)
+            fail("rank %d must own columns [%d, %d) of %d", R.rank, block_c0(R.rank, R.world, lens),
+                 block_c0(R.rank + 1, R.world, lens), lens);
+        Engine& E = engine();
+        std::lock_guard<std::mutex> lk(E.mu);
+        HIPCHECK(hipMemcpy(R.q.get((size_t)lenq), query, (size_t)lenq, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(R.s.get((size_t)w), subject_block, (size_t)w, hipMemcpyHostToDevice));
+        R.n = lenq;
+        R.m = lens;
+        R.c0 = c0;
+        R.w = w;
+        return 0;
+    } catch (const Failure& f) {
+        set_last_error(f.msg);
+        return -1;
+    }
+}
+
+int anyseq_shard_score(int kind, const anyseq_scoring* sc, int64_t* score) {
+    try {
+        const anyseq_scoring s = sc ? *sc : anyseq_scoring{2, -1, 0, -1};
+        const int64_t v = shard_score_rccl(kind, s);
+        if (score) *score = v;
+        return 0;
+    } catch (const Failure& f) {
+        set_last_error(f.msg);
+        if (g_rccl)
+            for (auto& c : g_rccl->comm)
+                if (c) ncclCommAbort(c), c = nullptr;
+        return -1;
+    }
+}
+
+int anyseq_shard_finalize(void) {
+    if (g_rccl) {
+        for (auto& c : g_rccl->comm)
+            if (c) ncclCommDestroy(c), c = nullptr;
+        g_rccl.reset();
+    }
+    return 0;
+}
+
+int anyseq_shard_score_local(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
+                             int lens, int nshards, int64_t* score) {
+    try {
+        const anyseq_scoring s = sc ? *sc : anyseq_scoring{2, -1, 0, -1};
+        const int64_t v = shard_score_local(kind, s, query, lenq, subject, lens, nshards);
+        if (score) *score = v;
+        return 0;
+    } catch (const Failure& f) {
+        set_last_error(f.msg);
+        return -1;
+    }
+}
+
+}  // extern "C"

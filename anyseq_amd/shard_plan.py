@@ -1,0 +1,66 @@
+"""shard_plan — host-side arithmetic of the column-block sharded fill.
+
+Pure Python, no GPU: the partition, the shard frames and the split-row combine
+that anyseq_amd/csrc/anyseq_shard.cpp implements in C++ (setup_shard,
+enqueue_combine, shard_combine_kernel).  tests/test_shard_plan.py drives this
+plan over world_size-2 ``gloo`` process groups with a CPU stand-in for the fill,
+checking that the decomposition reproduces the oracle's scores.
+
+Frames.  Shard g owns subject columns [c0_g, c0_g + w_g).  Its fill sees the
+scheme's top border (H[-1][c] = (c+1) gap for global), so its values are the true
+ones shifted by c0_g * gap (global; semiglobal and local borders are 0 and need
+no shift).  A left column received from shard g-1 therefore moves into shard g's
+frame by + w_{g-1} * (-gap); the bottom front runs on the reversed sequences and
+receives from shard g+1, shifted by + w_{g+1} * (-gap).
+"""
+from __future__ import annotations
+
+NCOMMS = 4          # RCCL communicators: top/bottom direction x link parity
+GLOBAL, SEMIGLOBAL, LOCAL = 0, 1, 2
+
+
+def block(g: int, nshards: int, m: int):
+    """(c0, w) of shard g: balanced contiguous column blocks (anyseq_shard.cpp block_c0)."""
+    c0 = g * m // nshards
+    return c0, (g + 1) * m // nshards - c0
+
+
+def fronts(n: int):
+    """Rows of the top (forward) and bottom (reversed) fronts: the split is at n // 2."""
+    h1 = n // 2
+    return h1, n - h1
+
+
+def left_shift_top(kind: int, g: int, nshards: int, m: int, gap: int) -> int:
+    """Added to the values received from shard g-1 (top front)."""
+    if kind != GLOBAL or g == 0:
+        return 0
+    return block(g - 1, nshards, m)[1] * -gap
+
+
+def left_shift_bottom(kind: int, g: int, nshards: int, m: int, gap: int) -> int:
+    """Added to the values received from shard g+1 (bottom front, reversed)."""
+    if kind != GLOBAL or g == nshards - 1:
+        return 0
+    return block(g + 1, nshards, m)[1] * -gap
+
+
+def combine_adjust(kind: int, g: int, nshards: int, m: int, gap: int) -> int:
+    """Top frame + bottom frame -> true score: (c0 + (m - c0 - w)) * gap for global."""
+    if kind != GLOBAL:
+        return 0
+    return (m - block(g, nshards, m)[1]) * gap
+
+
+def split_columns(g: int, nshards: int, w: int):
+    """Local split columns j of shard g's combine: [-1, w-1), plus w-1 on the last shard."""
+    return range(-1, w if g == nshards - 1 else w - 1)
+
+
+def chunks(h: int, chunk_rows: int = 1024):
+    """Row chunks [r0, r1) shipped per message, and the band count each waits for."""
+    out = []
+    for r0 in range(0, h, chunk_rows):
+        r1 = min(h, r0 + chunk_rows)
+        out.append((r0, r1, (r1 + 63) // 64))
+    return out

@@ -1,0 +1,68 @@
+"""anyseq_amd.sharded — column-block sharded score, one process per GPU over RCCL.
+
+SURVEY.md §8(e) / DESIGN.md §6.  Rank g owns subject columns
+``shard_plan.block(g, world, m)``; the boundary columns travel between
+neighbouring ranks with RCCL ncclSend/ncclRecv over xGMI inside
+libanyseq.so (anyseq_shard.cpp) while the fills run; the per-rank split
+candidates are reduced with one MAX all-reduce.  torch.distributed (any backend,
+``gloo`` is enough) only broadcasts the RCCL unique ids.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import AnySeqError, _b, _err, _kind, _lib, _scoring, main_random_pair
+from . import shard_plan
+
+_ID_BYTES = 128
+
+
+def init(dist, rank: int, world: int) -> None:
+    """Create the RCCL communicators of this rank (collective over the process group)."""
+    payload = [None]
+    if rank == 0:
+        ids = ctypes.create_string_buffer(_ID_BYTES * shard_plan.NCOMMS)
+        if _lib.anyseq_shard_unique_ids(ids, shard_plan.NCOMMS) != 0:
+            raise AnySeqError(_err())
+        payload = [ids.raw]
+    dist.broadcast_object_list(payload, src=0)
+    if _lib.anyseq_shard_init(rank, world, payload[0], shard_plan.NCOMMS) != 0:
+        raise AnySeqError(_err())
+
+
+def load(query, subject, rank: int, world: int) -> None:
+    """Make this rank's inputs resident: the whole query and its subject block."""
+    q, s = _b(query), _b(subject)
+    c0, w = shard_plan.block(rank, world, len(s))
+    blk = s[c0:c0 + w]
+    if _lib.anyseq_shard_load(q, len(q), blk, w, c0, len(s)) != 0:
+        raise AnySeqError(_err())
+
+
+def score(kind, match=2, mismatch=-1, gap_open=0, gap_extend=-1) -> int:
+    """One sharded fill over the loaded inputs; every rank gets the full score."""
+    out = ctypes.c_int64(0)
+    sc = _scoring(match, mismatch, gap_open, gap_extend)
+    if _lib.anyseq_shard_score(_kind(kind), ctypes.byref(sc), ctypes.byref(out)) != 0:
+        raise AnySeqError(_err())
+    return out.value
+
+
+def finalize() -> None:
+    _lib.anyseq_shard_finalize()
+
+
+def make_weak_step(dist, rank: int, world: int, kind: str, rows: int = 65536, cols_per_rank: int = 65536):
+    """bench.py's weak-scaling workload: `rows` x (cols_per_rank * world) cells, each
+    rank owning one block of cols_per_rank columns (main.cpp generator inputs)."""
+    L = cols_per_rank * world
+    q, s = main_random_pair(max(L, rows), max(L, rows))
+    q, s = q[:rows], s[:L]
+    init(dist, rank, world)
+    load(q, s, rank, world)
+
+    def step():
+        return score(kind)
+
+    par = f"column blocks x{world} (RCCL boundary columns over xGMI)"
+    return step, rows, cols_per_rank, par

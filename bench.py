@@ -8,10 +8,12 @@ reproduced by anyseq_main_random_pair; fingerprints in SURVEY.md App. B).
 One step = one global_alignment_score-equivalent fill of the whole matrix with
 both sequences already resident in HBM (anyseq_score_device), score copied back.
 
-N>1 (one process per GPU, torch.distributed.run): weak scaling over a
+N>1 (one process per GPU, torch.distributed.run): weak scaling over ONE
 column-blocked matrix of 65536 rows x 65536*N columns; rank g owns columns
-[65536 g, 65536 (g+1)) and the left-boundary column of each row chunk arrives
-from rank g-1.
+[65536 g, 65536 (g+1)); the two fronts' boundary columns travel between
+neighbouring ranks in 1024-row chunks with RCCL send/recv over xGMI while the
+fills run (libanyseq.so, anyseq_shard.cpp).  torch.distributed
+(gloo) is the control plane only: barrier, max-over-ranks time, RCCL ids.
 
 Prints ONE JSON line on rank 0.
 """
@@ -40,6 +42,8 @@ def parse():
     ap.add_argument("--m", type=int, default=65536)
     ap.add_argument("--kind", default="global", choices=["global", "semiglobal", "local"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the RCCL column-block path even at N=1 (plumbing check; the N=1 line is single GPU)")
     ap.add_argument("--cpu-threads", type=int, default=4,
                     help="oracle threads (reference get_thread_count() = 4, backend_cpu.impala:13)")
     return ap.parse_args()
@@ -75,6 +79,10 @@ def cpu_baseline(q: bytes, s: bytes, kind: str, threads: int, expect: int):
 
 def main():
     args = parse()
+    # the sharded path's fill + transport streams each need a hardware queue of their own
+    # (anyseq_shard.cpp check_hw_queues); HIP reads this at its first call
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -82,32 +90,28 @@ def main():
     import anyseq_amd as A
 
     dist = None
-    if world > 1:
+    if world > 1 or args.sharded:
+        # control plane only (barrier, timing max, RCCL id broadcast): gloo on the host.
+        # The data path is libanyseq.so's own RCCL communicators (anyseq_shard.cpp).
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(0)
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     A.set_device(local_rank if world > 1 else 0)
+    torch.cuda.set_device(local_rank if world > 1 else 0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    q, s = A.main_random_pair(args.n, args.m)
-    n, m = len(q), len(s)
     kind = args.kind
-    stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
-
     parallelism = "single GPU"
-    step = None
-    if world > 1:
-        try:
-            from anyseq_amd import sharded
-            step, n, m, parallelism = sharded.make_weak_step(A, dist, rank, world, kind, dev, stream)
-        except (ImportError, NotImplementedError):
-            step = None
-            parallelism = f"replicas x{world} (independent {n}x{m} problems, no exchange)"
-    if step is None:
+    if dist:
+        from anyseq_amd import sharded
+        step, n, m, parallelism = sharded.make_weak_step(dist, rank, world, kind, rows=args.n, cols_per_rank=args.m)
+        q = s = None
+    else:
+        q, s = A.main_random_pair(args.n, args.m)
+        n, m = len(q), len(s)
+        stream = torch.cuda.current_stream()
+        sh = stream.cuda_stream
         dq = torch.frombuffer(bytearray(q), dtype=torch.uint8).to(dev)
         ds = torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev)
 
@@ -132,7 +136,7 @@ def main():
     fill_ms, launches = A.last_fill_timing()
     elapsed = t1 - t0
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -172,11 +176,12 @@ def main():
                                         "(SURVEY.md 8(d))",
                          "traffic_source": traffic_src},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not dist and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(q, s, kind, args.cpu_threads, int(score))
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
+        sharded.finalize()
         dist.destroy_process_group()
 
 

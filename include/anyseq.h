@@ -92,6 +92,26 @@ int anyseq_set_option(const char* name, int value);
  * HIP events on the engine stream: total kernel milliseconds and launch count. */
 void anyseq_last_fill_timing(double* ms, int* launches);
 
+/* ---- column-block sharded score (build-defined) ----
+ * Subject columns are split into contiguous blocks, block g = [g*m/N, (g+1)*m/N);
+ * the boundary columns of the two fill fronts travel between neighbouring shards
+ * in row chunks while the fills run.  Linear gaps only.
+ *
+ * One process per GPU over RCCL: rank 0 calls anyseq_shard_unique_ids (count = 4),
+ * the bytes (count * 128) are broadcast out of band, every rank calls
+ * anyseq_shard_init, anyseq_shard_load (its block), then anyseq_shard_score
+ * (collective; every rank receives the full score). */
+int anyseq_shard_unique_ids(void* ids, int count);
+int anyseq_shard_init(int rank, int world, const void* ids, int count);
+int anyseq_shard_load(const char* query, int lenq, const char* subject_block, int block_len, int block_offset,
+                      int lens);
+int anyseq_shard_score(int kind, const anyseq_scoring* sc, int64_t* score);
+int anyseq_shard_finalize(void);
+/* The same sharded fill with `nshards` shards inside this process on the current
+ * device (device copies instead of RCCL between them). */
+int anyseq_shard_score_local(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
+                             int lens, int nshards, int64_t* score);
+
 /* main.cpp's random input generator (main.cpp:90-120, 200-210): mt19937_64 with the
  * default seed, lengths uniform in [minlen, maxlen], bases uniform over ACGT.
  * query/subject must hold maxlen bytes; lengths are returned. */

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# The sharded fill runs several concurrent streams, each needing its own hardware
+# queue (anyseq_shard.cpp check_hw_queues); set before the first HIP call.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -1,0 +1,132 @@
+"""CPU test of the column-block sharded decomposition.
+
+world_size-2 (and 3) ``gloo`` process groups run anyseq_amd/shard_plan.py's plan
+with a small pure-Python stand-in for each shard's fill (test infrastructure
+only): the top front sends its last column to rank g+1, the reversed bottom front
+to rank g-1, each rank combines its split columns, and a MAX all-reduce gives the
+score, which must equal the oracle's.  The GPU path (anyseq_shard.cpp) implements
+the same plan; tests/test_gpu_shard.py checks it on the device.
+"""
+import os
+import random
+import socket
+
+import pytest
+
+from anyseq_amd import shard_plan as SP
+
+KINDS = {"global": 0, "semiglobal": 1, "local": 2}
+
+
+def _fill(kind, rows, cols, left, match=2, mismatch=-1, gap=-1):
+    """H of one shard front in its own frame; left = received column (shifted) or None."""
+    h, w = len(rows), len(cols)
+    init = (lambda i: (i + 1) * gap) if kind == 0 else (lambda i: 0)
+    prev = [0] + [init(c) for c in range(w)]          # row -1: corner 0, then the scheme border
+    H = []
+    for r in range(h):
+        cur = [left[r] if left is not None else init(r)] + [0] * w
+        for c in range(w):
+            v = prev[c] + (match if rows[r] == cols[c] else mismatch)
+            v = max(v, cur[c] + gap, prev[c + 1] + gap)
+            if kind == 2:
+                v = max(v, 0)
+            cur[c + 1] = v
+        H.append(cur[1:])
+        prev = cur
+    return H
+
+
+def _worker(rank, world, port, cases, results):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    for kind_name, q, s in cases:
+        kind = KINDS[kind_name]
+        n, m = len(q), len(s)
+        c0, w = SP.block(rank, world, m)
+        h1, h2 = SP.fronts(n)
+        gap = -1
+        blk = s[c0:c0 + w]
+        # top front: receive from rank-1, send to rank+1
+        lt = None
+        if rank > 0:
+            t = torch.zeros(h1, dtype=torch.int64)
+            dist.recv(t, src=rank - 1)
+            lt = [int(x) + SP.left_shift_top(kind, rank, world, m, gap) for x in t]
+        Ht = _fill(kind, q[:h1], blk, lt)
+        if rank < world - 1:
+            dist.send(torch.tensor([row[w - 1] for row in Ht], dtype=torch.int64), dst=rank + 1)
+        # bottom front (reversed): receive from rank+1, send to rank-1
+        lb = None
+        if rank < world - 1:
+            t = torch.zeros(h2, dtype=torch.int64)
+            dist.recv(t, src=rank + 1)
+            lb = [int(x) + SP.left_shift_bottom(kind, rank, world, m, gap) for x in t]
+        Hb = _fill(kind, q[::-1][:h2], blk[::-1], lb)
+        if rank > 0:
+            dist.send(torch.tensor([row[w - 1] for row in Hb], dtype=torch.int64), dst=rank - 1)
+        init = (lambda i: (i + 1) * gap) if kind == 0 else (lambda i: 0)
+        adj = SP.combine_adjust(kind, rank, world, m, gap)
+        best = 0 if kind == 1 else -2147483647
+        for j in SP.split_columns(rank, world, w):
+            F = Ht[h1 - 1][j] if j >= 0 else (lt[h1 - 1] if lt is not None else init(h1 - 1))
+            jb = w - 2 - j
+            B = Hb[h2 - 1][jb] if jb >= 0 else (lb[h2 - 1] if lb is not None else init(h2 - 1))
+            best = max(best, F + B + adj)
+        if kind == 1:
+            if rank == world - 1:
+                best = max([best] + [row[w - 1] for row in Ht])
+            if rank == 0:
+                best = max([best] + [row[w - 1] for row in Hb])
+        if kind == 2:
+            best = max([best] + [max(r) for r in Ht] + [max(r) for r in Hb])
+        t = torch.tensor([best], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out.append(int(t.item()))
+    if rank == 0:
+        results.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_plan_matches_oracle(oracle, world):
+    import torch.multiprocessing as mp
+    rng = random.Random(31 + world)
+    cases = []
+    for kind in KINDS:
+        for n, m in [(2, 7), (9, 13), (40, 33), (57, 90)]:
+            q = bytes(rng.choice(b"ACGT") for _ in range(n))
+            s = bytes(rng.choice(b"ACGT") for _ in range(m))
+            cases.append((kind, q, s))
+    ctx = mp.get_context("spawn")
+    results = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, results)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = results.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [oracle.score(k, q, s) for k, q, s in cases]
+    assert got == want
+
+
+def test_plan_partition_and_chunks():
+    for m, N in [(10, 3), (65536 * 8, 8), (7, 7)]:
+        blocks = [SP.block(g, N, m) for g in range(N)]
+        assert blocks[0][0] == 0 and sum(w for _, w in blocks) == m
+        assert all(blocks[g][0] + blocks[g][1] == blocks[g + 1][0] for g in range(N - 1))
+    ch = SP.chunks(2500, 1024)
+    assert ch == [(0, 1024, 16), (1024, 2048, 32), (2048, 2500, 40)]
