@@ -672,3 +672,258 @@ int64_t oracle_affine_score(int kind, const char* qc, int n, const char* sc_, in
     free(H); free(F);
     return result;
 }
+
+/* ===================================================================== */
+/* Build-defined affine CONSTRUCT (linear space).  No reference semantics */
+/* (see above); this is the semantics of the HIP path, restated:         */
+/*  1. the aligned rectangle [is,ie] x [js,je]:                          */
+/*     global: the whole matrix;                                         */
+/*     local: end = oracle_affine_score's position (max H, then smallest */
+/*       i, then smallest j); start = argmax of the GLOBAL DP of the     */
+/*       reversed prefixes q[0..ie], s[0..je] (same tie rule, reversed   */
+/*       coordinates); best <= 0 -> empty alignment;                     */
+/*     semiglobal: end = oracle_affine_score's position (j or i = -1 ->  */
+/*       empty); start = best cell of that reversed GLOBAL DP's last row */
+/*       (b = -1 .. je, first max) then last column (a = -1 .. ie, only  */
+/*       if strictly greater);                                           */
+/*  2. a GLOBAL affine alignment of the rectangle by the column-split    */
+/*     Hirschberg of the linear construct (same levels, parts, splits),  */
+/*     where a split also records its crossing state: H (any) or E (a    */
+/*     horizontal gap crossing the column boundary, opened once).  A     */
+/*     sub-problem starting after an E crossing forbids a non-gap start  */
+/*     and pays no open for its first gap (BM_EFREE); one ending before  */
+/*     it must end in a horizontal gap (its reversed half: BM_EPAID).    */
+/*     Join of part rows i = -1 .. len-1, ascending, strict >, H before  */
+/*     E: HL(i) + HR(len-i-2), EL(i) + ER(len-i-2) - go;                  */
+/*  3. final 128-column blocks: full Gotoh with predecessors (H: diag >  */
+/*     E > F; E/F: open unless extending is strictly better), walked     */
+/*     from the block's end in state H (or E after an E crossing);       */
+/*     output in the sparse i+j+1 layout of traceback.impala:47-80.      */
+/* ===================================================================== */
+enum { BM_NORMAL = 0, BM_EFREE = 1, BM_EPAID = 2 };
+#define ANEG AFF_NEG_INF
+
+typedef struct { const uint8_t* b; Index off; int step; } Acc;
+static inline uint8_t acc_at(Acc a, Index i) { return a.b[a.off + (Index)a.step * i]; }
+typedef struct { int match, mismatch, go, ge; } AffSc;
+
+/* Global affine DP of q x s (h x w) under border mode bm.  Optional outputs:
+ * last column H/E (h each), last row H (w), argmax over all cells (row-major
+ * first max: smallest row, then smallest column). */
+static void aff_global_fill(Acc q, Index h, Acc s, Index w, const AffSc* sc, int bm,
+                            Score* colH, Score* colE, Score* lastrow,
+                            Score* best, Index* bi, Index* bj) {
+    Score* H = (Score*)malloc(sizeof(Score) * (size_t)(w + 1));
+    Score* F = (Score*)malloc(sizeof(Score) * (size_t)(w + 1));
+    const Score tbase = bm == BM_EFREE ? 0 : sc->go;
+    H[0] = bm == BM_NORMAL ? 0 : ANEG;
+    for (Index c = 0; c < w; ++c) { H[c + 1] = tbase + (c + 1) * sc->ge; F[c + 1] = ANEG; }
+    Score mx = SCORE_MIN_VALUE; Index mi = -1, mj = -1;
+    for (Index r = 0; r < h; ++r) {
+        Score diag = H[0];
+        Score left = bm == BM_NORMAL ? sc->go + (r + 1) * sc->ge : ANEG;
+        H[0] = left;
+        Score E = ANEG;
+        const uint8_t qs = acc_at(q, r);
+        for (Index c = 0; c < w; ++c) {
+            Score e1 = E + sc->ge, e2 = left + sc->go + sc->ge;
+            E = e1 > e2 ? e1 : e2;
+            Score up = H[c + 1];
+            Score f1 = F[c + 1] + sc->ge, f2 = up + sc->go + sc->ge;
+            Score f = f1 > f2 ? f1 : f2;
+            F[c + 1] = f;
+            Score hv = diag + (qs == acc_at(s, c) ? sc->match : sc->mismatch);
+            if (E > hv) hv = E;
+            if (f > hv) hv = f;
+            diag = up;
+            H[c + 1] = hv;
+            left = hv;
+            if (hv > mx) { mx = hv; mi = r; mj = c; }
+        }
+        if (colH) colH[r] = H[w];
+        if (colE) colE[r] = w > 0 ? E : ANEG;
+    }
+    if (lastrow) for (Index c = 0; c < w; ++c) lastrow[c] = H[c + 1];
+    if (best) { *best = mx; *bi = mi; *bj = mj; }
+    free(H); free(F);
+}
+
+typedef struct { Score* v; Index n; } IVec;   /* logical index -1 at v[0] */
+#define IV(x, i) ((x).v[(i) + 1])
+
+/* Final 128-column block: Gotoh with predecessor bytes, walk, sparse output. */
+enum { AP_DIAG = 0, AP_E = 1, AP_F = 2 };
+static void aff_block_walk(const uint8_t* Q, const uint8_t* S, Index oi, Index h, Index oj, Index w,
+                           const AffSc* sc, int smode, int e_end, char* alq, char* als) {
+    uint8_t* P = (uint8_t*)calloc((size_t)(h > 0 ? h : 1) * (size_t)w, 1);
+    Score* H = (Score*)malloc(sizeof(Score) * (size_t)(w + 1));
+    Score* F = (Score*)malloc(sizeof(Score) * (size_t)(w + 1));
+    const Score tbase = smode == BM_EFREE ? 0 : sc->go;
+    H[0] = smode == BM_NORMAL ? 0 : ANEG;
+    for (Index c = 0; c < w; ++c) { H[c + 1] = tbase + (c + 1) * sc->ge; F[c + 1] = ANEG; }
+    for (Index r = 0; r < h; ++r) {
+        Score diag = H[0];
+        Score left = smode == BM_NORMAL ? sc->go + (r + 1) * sc->ge : ANEG;
+        H[0] = left;
+        Score E = ANEG;
+        for (Index c = 0; c < w; ++c) {
+            uint8_t pb = 0;
+            Score e1 = E + sc->ge, e2 = left + sc->go + sc->ge;
+            if (e1 > e2) { E = e1; pb |= 4; } else E = e2;
+            Score up = H[c + 1];
+            Score f1 = F[c + 1] + sc->ge, f2 = up + sc->go + sc->ge;
+            Score f;
+            if (f1 > f2) { f = f1; pb |= 8; } else f = f2;
+            F[c + 1] = f;
+            Score hv = diag + (Q[oi + r] == S[oj + c] ? sc->match : sc->mismatch);
+            int hs = AP_DIAG;
+            if (E > hv) { hv = E; hs = AP_E; }
+            if (f > hv) { hv = f; hs = AP_F; }
+            pb |= (uint8_t)hs;
+            P[(size_t)r * w + c] = pb;
+            diag = up;
+            H[c + 1] = hv;
+            left = hv;
+        }
+    }
+    /* walk: state 0 = H, 1 = E, 2 = F */
+    Index i = h - 1, j = w - 1;
+    int st = e_end ? 1 : 0;
+    const Index base = oi + oj;
+    while (i >= 0 || j >= 0) {
+        if (i < 0) { alq[base + i + j + 1] = '_'; als[base + i + j + 1] = (char)S[oj + j]; --j; continue; }
+        if (j < 0) { alq[base + i + j + 1] = (char)Q[oi + i]; als[base + i + j + 1] = '_'; --i; continue; }
+        const uint8_t pb = P[(size_t)i * w + j];
+        if (st == 0) {
+            const int hs = pb & 3;
+            if (hs == AP_DIAG) {
+                alq[base + i + j + 1] = (char)Q[oi + i]; als[base + i + j + 1] = (char)S[oj + j];
+                --i; --j;
+            } else st = hs == AP_E ? 1 : 2;
+        } else if (st == 1) {
+            alq[base + i + j + 1] = '_'; als[base + i + j + 1] = (char)S[oj + j];
+            st = (pb & 4) ? 1 : 0;
+            --j;
+        } else {
+            alq[base + i + j + 1] = (char)Q[oi + i]; als[base + i + j + 1] = '_';
+            st = (pb & 8) ? 2 : 0;
+            --i;
+        }
+    }
+    free(P); free(H); free(F);
+}
+
+/* Global affine Hirschberg of the rectangle q x s (n x m); output at
+ * alq/als + i + j + 1 (callers pass the rectangle's offset). */
+static void aff_construct_rect(const uint8_t* Q, Index n, const uint8_t* S, Index m, const AffSc* sc,
+                               char* alq, char* als) {
+    if (m <= 0) {   /* all query rows against gaps, down the left border: position i + (-1) + 1 */
+        for (Index i = 0; i < n; ++i) { alq[i] = (char)Q[i]; als[i] = '_'; }
+        return;
+    }
+    const Index nb = round_up_div(m, MIN_PART_WIDTH_HB);
+    IVec spl, typ;
+    spl.n = nb; typ.n = nb;
+    spl.v = (Score*)malloc(sizeof(Score) * (size_t)(nb + 1));
+    typ.v = (Score*)calloc((size_t)(nb + 1), sizeof(Score));
+    for (Index i = -1; i < nb; ++i) IV(spl, i) = SPLIT_UNSET;
+    IV(spl, -1) = 0;
+    IV(spl, nb - 1) = n;
+    Index pw = next_pow_2(m);
+    Index bpp = pw / MIN_PART_WIDTH_HB;
+    Score *LH = (Score*)malloc(sizeof(Score) * (size_t)(n + 1)), *LE = (Score*)malloc(sizeof(Score) * (size_t)(n + 1));
+    Score *RH = (Score*)malloc(sizeof(Score) * (size_t)(n + 1)), *RE = (Score*)malloc(sizeof(Score) * (size_t)(n + 1));
+    while (pw > MIN_PART_WIDTH_HB) {
+        const Index half = pw / 2;
+        const Index parts = (m + half - 1) / pw;
+        for (Index p = 0; p < parts; ++p) {
+            const Index sb = p * bpp - 1, eb = imin((p + 1) * bpp - 1, nb - 1);
+            const Index off = IV(spl, sb), len = IV(spl, eb) - off;
+            if (IV(spl, sb) == SPLIT_UNSET || IV(spl, eb) == SPLIT_UNSET) { g_error = 1; continue; }
+            const int smode = IV(typ, sb) ? BM_EFREE : BM_NORMAL;
+            const int rmode = IV(typ, eb) ? BM_EPAID : BM_NORMAL;
+            const Index hoj_l = p * pw, hoj_r = p * pw + half;
+            const Index hw = imin(half, m - hoj_r);
+            if (len > 0) {
+                Acc qa = {Q, off, 1}, sa = {S, hoj_l, 1};
+                aff_global_fill(qa, len, sa, half, sc, smode, LH + off, LE + off, NULL, NULL, NULL, NULL);
+                Acc qr = {Q, off + len - 1, -1}, sr = {S, hoj_r + hw - 1, -1};
+                aff_global_fill(qr, len, sr, hw, sc, rmode, RH + off, RE + off, NULL, NULL, NULL, NULL);
+            }
+            const Score bL = (smode == BM_EFREE ? 0 : sc->go) + half * sc->ge;
+            const Score bR = sc->go + hw * sc->ge;
+            Score best = SCORE_MIN_VALUE; Index idx = -1; int type = 0;
+            for (Index i = -1; i < len; ++i) {
+                const Index k = len - i - 2;
+                const Score hl = i < 0 ? bL : LH[off + i], el = i < 0 ? bL : LE[off + i];
+                const Score hr = k < 0 ? bR : RH[off + k], er = k < 0 ? bR : RE[off + k];
+                Score v = hl + hr;
+                if (v > best) { best = v; idx = i; type = 0; }
+                v = el + er - sc->go;
+                if (v > best) { best = v; idx = i; type = 1; }
+            }
+            const Index si = p * bpp + bpp / 2 - 1;
+            IV(spl, si) = off + idx + 1;
+            IV(typ, si) = type;
+        }
+        pw /= 2;
+        bpp /= 2;
+    }
+    for (Index b = 0; b < nb; ++b) {
+        const Index oi = IV(spl, b - 1), h = IV(spl, b) - oi;
+        const Index oj = b * MIN_PART_WIDTH_HB, w = imin(MIN_PART_WIDTH_HB, m - oj);
+        if (IV(spl, b - 1) == SPLIT_UNSET || IV(spl, b) == SPLIT_UNSET) { g_error = 1; continue; }
+        aff_block_walk(Q, S, oi, h, oj, w, sc, IV(typ, b - 1) ? BM_EFREE : BM_NORMAL, IV(typ, b) != 0, alq, als);
+    }
+    free(spl.v); free(typ.v); free(LH); free(LE); free(RH); free(RE);
+}
+
+/* The aligned rectangle of step 1; returns 0 for an empty alignment. */
+int oracle_affine_rect(int kind, const char* qc, int n, const char* sc_, int m, int match, int mismatch, int go,
+                       int ge, int32_t* rect, int64_t* score) {
+    const uint8_t* q = (const uint8_t*)qc; const uint8_t* s = (const uint8_t*)sc_;
+    AffSc sc = {match, mismatch, go, ge};
+    int32_t bi = -1, bj = -1;
+    const int64_t res = oracle_affine_score(kind, qc, n, sc_, m, match, mismatch, go, ge, &bi, &bj);
+    *score = res;
+    if (kind == SCHEME_GLOBAL) { rect[0] = 0; rect[1] = n - 1; rect[2] = 0; rect[3] = m - 1; return n > 0 || m > 0; }
+    if (n <= 0 || m <= 0) return 0;
+    if (kind == SCHEME_LOCAL && res <= 0) return 0;
+    if (bi < 0 || bj < 0) return 0;
+    const Index ie = bi, je = bj;
+    Acc qr = {q, ie, -1}, sr = {s, je, -1};
+    if (kind == SCHEME_LOCAL) {
+        Score best; Index a, b;
+        aff_global_fill(qr, ie + 1, sr, je + 1, &sc, BM_NORMAL, NULL, NULL, NULL, &best, &a, &b);
+        rect[0] = ie - a; rect[1] = ie; rect[2] = je - b; rect[3] = je;
+        return 1;
+    }
+    /* semiglobal: reversed GLOBAL DP, best of its last row (b = -1..je) then last column */
+    Score* colH = (Score*)malloc(sizeof(Score) * (size_t)(ie + 1));
+    Score* row = (Score*)malloc(sizeof(Score) * (size_t)(je + 1));
+    aff_global_fill(qr, ie + 1, sr, je + 1, &sc, BM_NORMAL, colH, NULL, row, NULL, NULL, NULL);
+    Score best = go + (ie + 1) * ge;   /* b = -1: the reversed left border at row ie */
+    Index sa = ie, sb = -1;
+    for (Index b = 0; b <= je; ++b) if (row[b] > best) { best = row[b]; sa = ie; sb = b; }
+    {
+        const Score top = go + (je + 1) * ge;   /* a = -1: the reversed top border at column je */
+        if (top > best) { best = top; sa = -1; sb = je; }
+    }
+    for (Index a = 0; a <= ie; ++a) if (colH[a] > best) { best = colH[a]; sa = a; sb = je; }
+    free(colH); free(row);
+    rect[0] = ie - sa; rect[1] = ie; rect[2] = je - sb; rect[3] = je;
+    return 1;
+}
+
+int64_t oracle_affine_construct(int kind, const char* qc, int n, const char* sc_, int m, int match, int mismatch,
+                                int go, int ge, char* alq, char* als) {
+    for (Index i = 0; i < n + m; ++i) { alq[i] = ' '; als[i] = ' '; }
+    int32_t r[4];
+    int64_t score = 0;
+    if (!oracle_affine_rect(kind, qc, n, sc_, m, match, mismatch, go, ge, r, &score)) return score;
+    AffSc sc = {match, mismatch, go, ge};
+    const Index off = r[0] + r[2];
+    aff_construct_rect((const uint8_t*)qc + r[0], r[1] - r[0] + 1, (const uint8_t*)sc_ + r[2], r[3] - r[2] + 1, &sc,
+                       alq + off, als + off);
+    return score;
+}

@@ -45,10 +45,12 @@ def lib() -> ctypes.CDLL:
         L.oracle_affine_score.restype = c_i64
         L.oracle_affine_score.argtypes = [c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_int, c_int,
                                           i32p, i32p]
-        if hasattr(L, "oracle_affine_construct"):
-            L.oracle_affine_construct.restype = c_i64
-            L.oracle_affine_construct.argtypes = [c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_int,
-                                                  c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_affine_construct.restype = c_i64
+        L.oracle_affine_construct.argtypes = [c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_int,
+                                              c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_affine_rect.restype = c_int
+        L.oracle_affine_rect.argtypes = [c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_int, c_int,
+                                         i32p, ctypes.POINTER(c_i64)]
         _lib = L
     return _lib
 
@@ -100,14 +102,28 @@ def affine_score(kind, q, s, match=2, mismatch=-1, gap_open=-2, gap_extend=-1, w
 
 
 def affine_construct(kind, q, s, match=2, mismatch=-1, gap_open=-2, gap_extend=-1):
-    """Build-defined affine alignment (dense strings, see anyseq_oracle.c)."""
+    """Build-defined affine alignment (anyseq_oracle.c oracle_affine_construct):
+    (optimal score, alQuery, alSubject) in the sparse i+j+1 layout, len(q)+len(s) bytes each."""
     k = KINDS[kind] if isinstance(kind, str) else kind
     q, s = _b(q), _b(s)
     n, m = len(q), len(s)
     aq = ctypes.create_string_buffer(n + m + 1)
     as_ = ctypes.create_string_buffer(n + m + 1)
     r = lib().oracle_affine_construct(k, q, n, s, m, match, mismatch, gap_open, gap_extend, aq, as_)
-    return r, aq.value, as_.value
+    if lib().oracle_last_error():
+        raise RuntimeError("oracle read an unset split")
+    return r, aq.raw[: n + m], as_.raw[: n + m]
+
+
+def affine_rect(kind, q, s, match=2, mismatch=-1, gap_open=-2, gap_extend=-1):
+    """(nonempty, (is, ie, js, je), score): the rectangle an affine construct aligns."""
+    k = KINDS[kind] if isinstance(kind, str) else kind
+    q, s = _b(q), _b(s)
+    rect = (ctypes.c_int32 * 4)()
+    sc = ctypes.c_int64(0)
+    ok = lib().oracle_affine_rect(k, q, len(q), s, len(s), match, mismatch, gap_open, gap_extend, rect,
+                                  ctypes.byref(sc))
+    return bool(ok), tuple(rect), sc.value
 
 
 # --------------------------------------------------------------------------
