@@ -40,6 +40,16 @@ hipError_t anyseq_launch_pred(const void* blocks, int nblocks, const uint8_t* Q,
                               const FillParams* fp, hipStream_t st);
 hipError_t anyseq_launch_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
                               const uint8_t* pred, int kind, uint8_t* alq, uint8_t* als, hipStream_t st);
+hipError_t anyseq_launch_aff_rowbest(const void* rowbest, int h, int32_t* out, hipStream_t st);
+hipError_t anyseq_launch_aff_edge_scan(const void* row, int w, const int32_t* col, int h, int nge, int rborder,
+                                       int cborder, int32_t* out, hipStream_t st);
+hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, const int32_t* LH, const int32_t* LE,
+                                     const int32_t* RH, const int32_t* RE, int go, int ge, int32_t* splits,
+                                     int32_t* types, hipStream_t st);
+hipError_t anyseq_launch_aff_pred(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
+                                  int match, int mismatch, int go, int ge, hipStream_t st);
+hipError_t anyseq_launch_aff_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
+                                  const uint8_t* pred, uint8_t* alq, uint8_t* als, hipStream_t st);
 }
 
 namespace anyseq {
@@ -574,6 +584,199 @@ void construct_host(int kind, const anyseq_scoring& sc, const char* q, int n, co
     HIPCHECK(hipStreamSynchronize(st));
 }
 
+// ------------------------------------------------------ affine construct --
+// Build-defined linear-space affine alignment (semantics =
+// oracle_affine_construct).  Step 1 finds the aligned rectangle (global: the
+// matrix; local / semiglobal: end cell from a forward fill, start cell from a
+// GLOBAL fill of the reversed prefixes anchored at the end), step 2 aligns it
+// globally by the column-split Hirschberg of construct_host, carrying the
+// crossing state (H or E) of every split, step 3 walks the final 128-column
+// blocks.  Returns the optimal score.
+struct RectPos {
+    int32_t v, i, j;
+};
+
+RectPos read_pos(Engine& E, hipStream_t st) {
+    RectPos r;
+    HIPCHECK(hipMemcpyAsync(&r, E.pos.p, sizeof r, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    return r;
+}
+
+DPProblem aff_problem(const uint8_t* dq, int q_off, int q_step, int h, const uint8_t* ds, int s_off, int s_step, int w) {
+    DPProblem P;
+    memset(&P, 0, sizeof P);
+    P.q = dq;
+    P.s = ds;
+    P.q_off = q_off;
+    P.q_step = q_step;
+    P.s_off = s_off;
+    P.s_step = s_step;
+    P.h = h;
+    P.w = w;
+    return P;
+}
+
+// Position search fills (single front).  mode 0: TRACK (row-major first max of
+// all cells), 1: edge scan of the last row / column (semiglobal rule).
+RectPos aff_search(Engine& E, int kind, const anyseq_scoring& sc, DPProblem P, int mode, hipStream_t st) {
+    FillParams fp = make_params(kind, sc);
+    int32_t* pos = (int32_t*)E.pos.get(64);
+    std::vector<DPProblem> probs;
+    const int wpad = (P.w + 63) & ~63;
+    if (mode == 0) {
+        P.rowbest = (int2*)E.rowbest.get((size_t)P.h * 8);
+        probs.push_back(P);
+        run_fill(E, probs, fp, st);
+        HIPCHECK(anyseq_launch_aff_rowbest(P.rowbest, P.h, pos, st));
+    } else {
+        P.out_row = (int32_t*)E.outrow.get((size_t)wpad * 8);
+        P.out_col = (int32_t*)E.outcol.get((size_t)P.h * 4);
+        probs.push_back(P);
+        run_fill(E, probs, fp, st);
+        const int nge = -sc.gap_extend;
+        // index -1 of the row / column: the scheme's left / top border cell
+        const int rb = kind == KIND_GLOBAL ? sc.gap_open + P.h * sc.gap_extend : 0;
+        const int cb = kind == KIND_GLOBAL ? sc.gap_open + P.w * sc.gap_extend : 0;
+        HIPCHECK(anyseq_launch_aff_edge_scan(P.out_row, P.w, P.out_col, P.h, nge, rb, cb, pos, st));
+    }
+    return read_pos(E, st);
+}
+
+// Global affine Hirschberg of the rectangle dq[0..n) x ds[0..m) into d_alq/d_als
+// (already offset to the rectangle's i+j+1 origin).
+void aff_construct_rect(Engine& E, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds, int m,
+                        uint8_t* d_alq, uint8_t* d_als, hipStream_t st) {
+    const FillParams fp = make_params(KIND_GLOBAL, sc);
+    HostSplits sp;
+    sp.nb = (m + MIN_PART_WIDTH_HB - 1) / MIN_PART_WIDTH_HB;
+    sp.v.assign((size_t)sp.nb + 1, SPLIT_UNSET);
+    std::vector<int32_t> typ((size_t)sp.nb + 1, 0);
+    int pw = next_pow_2(m);
+    sp.bpp = pw / MIN_PART_WIDTH_HB;
+    sp.v[0] = 0;
+    sp.v[sp.nb] = n;
+    int32_t* d_spl = (int32_t*)E.spl.get(sp.v.size() * 4);
+    int32_t* d_typ = (int32_t*)E.typ.get(typ.size() * 4);
+    HIPCHECK(hipMemcpyAsync(d_spl, sp.v.data(), sp.v.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(d_typ, typ.data(), typ.size() * 4, hipMemcpyHostToDevice, st));
+    const size_t nn = (size_t)std::max(n, 1) * 4;
+    int32_t *LH = (int32_t*)E.L.get(nn), *LE = (int32_t*)E.LE.get(nn);
+    int32_t *RH = (int32_t*)E.R.get(nn), *RE = (int32_t*)E.RE.get(nn);
+    auto tp = [&](int idx) { return typ[idx + 1]; };
+    while (pw > MIN_PART_WIDTH_HB) {
+        const int half = pw / 2;
+        const int parts = (m + half - 1) / pw;
+        std::vector<DPProblem> probs;
+        std::vector<PartInfo> pinfo;
+        for (int p = 0; p < parts; ++p) {
+            int off, len;
+            sp.dims(p, off, len);
+            const int sb = p * sp.bpp - 1, eb = std::min((p + 1) * sp.bpp - 1, sp.nb - 1);
+            const int hoj_l = p * pw, hoj_r = p * pw + half;
+            const int hw = std::min(half, m - hoj_r);
+            PartInfo pi;
+            pi.off = off;
+            pi.len = len;
+            pi.rhw = hw;
+            pi.split_index = p * sp.bpp + sp.bpp / 2 - 1;
+            pi.smode = tp(sb) ? BM_EFREE : BM_NORMAL;
+            pinfo.push_back(pi);
+            if (len <= 0) continue;
+            DPProblem P = aff_problem(dq, off, 1, len, ds, hoj_l, 1, half);
+            P.bmode = pi.smode;
+            P.out_col = LH + off;
+            P.out_col_e = LE + off;
+            probs.push_back(P);
+            P = aff_problem(dq, off + len - 1, -1, len, ds, hoj_r + hw - 1, -1, hw);
+            P.bmode = tp(eb) ? BM_EPAID : BM_NORMAL;
+            P.out_col = RH + off;
+            P.out_col_e = RE + off;
+            probs.push_back(P);
+        }
+        if (!probs.empty()) run_fill(E, probs, fp, st);
+        PartInfo* d_parts = (PartInfo*)E.parts.get(pinfo.size() * sizeof(PartInfo));
+        HIPCHECK(hipMemcpyAsync(d_parts, pinfo.data(), pinfo.size() * sizeof(PartInfo), hipMemcpyHostToDevice, st));
+        HIPCHECK(anyseq_launch_aff_hb_join(d_parts, parts, half, LH, LE, RH, RE, sc.gap_open, sc.gap_extend, d_spl,
+                                           d_typ, st));
+        HIPCHECK(hipMemcpyAsync(sp.v.data(), d_spl, sp.v.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(typ.data(), d_typ, typ.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        pw /= 2;
+        sp.bpp /= 2;
+    }
+    std::vector<BlockInfo> blocks((size_t)sp.nb);
+    int64_t pred_bytes = 0;
+    for (int b = 0; b < sp.nb; ++b) {
+        BlockInfo& bi = blocks[b];
+        bi.oi = sp.at(b - 1);
+        bi.h = sp.at(b) - bi.oi;
+        bi.oj = b * MIN_PART_WIDTH_HB;
+        bi.w = std::min(MIN_PART_WIDTH_HB, m - bi.oj);
+        bi.pred_base = pred_bytes;
+        bi.smode = tp(b - 1) ? BM_EFREE : BM_NORMAL;
+        bi.e_end = tp(b);
+        if (bi.h > 0) pred_bytes += (int64_t)(bi.h + 127) * 128;
+    }
+    BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
+    HIPCHECK(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, st));
+    uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
+    HIPCHECK(anyseq_launch_aff_pred(d_blocks, sp.nb, dq, ds, d_pred, sc.match, sc.mismatch, sc.gap_open,
+                                    sc.gap_extend, st));
+    HIPCHECK(anyseq_launch_aff_walk(d_blocks, sp.nb, dq, ds, d_pred, d_alq, d_als, st));
+}
+
+int64_t construct_affine_host(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m,
+                              char* alq, char* als) {
+    Engine& E = engine();
+    std::lock_guard<std::mutex> lk(E.mu);
+    hipStream_t st = E.stream;
+    const size_t L = (size_t)n + (size_t)m;
+    if (L == 0) return empty_score(kind, n, m, sc);
+    memset(alq, ' ', L);
+    memset(als, ' ', L);
+    if (n <= 0 || m <= 0) {
+        if (kind == KIND_GLOBAL && m <= 0)   // all query rows against gaps, down the left border
+            for (int i = 0; i < n; ++i) {
+                alq[i] = q[i];
+                als[i] = '_';
+            }
+        if (kind != KIND_GLOBAL || m <= 0) return empty_score(kind, n, m, sc);
+    }
+    uint8_t* dq = (uint8_t*)E.q.get((size_t)std::max(n, 1));
+    uint8_t* ds = (uint8_t*)E.s.get((size_t)std::max(m, 1));
+    if (n > 0) HIPCHECK(hipMemcpyAsync(dq, q, (size_t)n, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(ds, s, (size_t)m, hipMemcpyHostToDevice, st));
+    int is = 0, ie = n - 1, js = 0, je = m - 1;
+    int64_t score = 0;
+    if (kind == KIND_GLOBAL) {
+        score = n > 0 ? score_dev(E, kind, sc, dq, n, ds, m, st) : empty_score(kind, n, m, sc);
+    } else {
+        const RectPos end = aff_search(E, kind, sc, aff_problem(dq, 0, 1, n, ds, 0, 1, m),
+                                       kind == KIND_LOCAL ? 0 : 1, st);
+        score = end.v;
+        if (end.i < 0 || end.j < 0 || (kind == KIND_LOCAL && end.v <= 0)) return score;   // empty alignment
+        ie = end.i;
+        je = end.j;
+        // GLOBAL fill of the reversed prefixes anchored at the end cell
+        const RectPos start = aff_search(E, KIND_GLOBAL, sc, aff_problem(dq, ie, -1, ie + 1, ds, je, -1, je + 1),
+                                         kind == KIND_LOCAL ? 0 : 1, st);
+        if (start.v != end.v) fail("affine construct: start search found %d, end search %d", start.v, end.v);
+        is = ie - start.i;
+        js = je - start.j;
+    }
+    const int n2 = ie - is + 1, m2 = je - js + 1;
+    uint8_t* d_alq = (uint8_t*)E.alq.get(L);
+    uint8_t* d_als = (uint8_t*)E.als.get(L);
+    HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
+    HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
+    aff_construct_rect(E, sc, dq + is, n2, ds + js, m2, d_alq + is + js, d_als + is + js, st);
+    HIPCHECK(hipMemcpyAsync(alq, d_alq, L, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(als, d_als, L, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    return score;
+}
+
 const anyseq_scoring kAbiScoring = {2, -1, 0, -1};  // linear_scoring_scheme(2,-1,-1)
 
 int64_t abi_score(int kind, const char* q, int n, const char* s, int m) {
@@ -668,6 +871,11 @@ int anyseq_construct(int kind, const anyseq_scoring* sc, const char* query, int 
     try {
         const anyseq_scoring s = sc ? *sc : kAbiScoring;
         check_scoring(kind, s);
+        if (s.gap_open != 0) {   // build-defined affine construct (true global / semiglobal / local)
+            const int64_t v = construct_affine_host(kind, s, query, lenq, subject, lens, alQuery, alSubject);
+            if (score) *score = v;
+            return 0;
+        }
         construct_host(kind, s, query, lenq, subject, lens, alQuery, alSubject);
         if (score) *score = score_host(kind, s, query, lenq, subject, lens);
         return 0;

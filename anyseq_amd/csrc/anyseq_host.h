@@ -79,6 +79,7 @@ struct Engine {
     std::mutex mu;
     FillCtx fc;
     DevBuf q, s, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq, als;
+    DevBuf LE, RE, typ, rowbest, pos;   // affine construct
     std::vector<int32_t> host_i32;
     explicit Engine(int dev);
 };

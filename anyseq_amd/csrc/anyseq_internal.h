@@ -7,6 +7,7 @@
 //   * linear local runs in "H-space": H = sat(max3(H_diag + sub - gap, H_left, H_up) + gap)
 //     (align.impala:69-79, the clamp at 0 folded into one saturating subtract).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace anyseq {
@@ -42,10 +43,18 @@ struct DPProblem {
     // band order with a system-scope release (the transport stream waits on it).
     const int32_t* left_in;
     int32_t left_shift;
-    int32_t pad1;
+    // Affine global sub-problems of the affine construct: border
+    // mode of the top-left corner.  0: the scheme's borders; 1 (E_FREE): the path
+    // continues a horizontal gap (corner and left column -inf, top row without the
+    // open); 2 (E_PAID): the path starts with a horizontal gap that pays its open.
+    int32_t bmode;
     uint32_t* progress;
     uint32_t* stage;       // diagnostics (ANYSEQ_SHARD_DEBUG): per-band stage reached
+    // Affine position search: (best H of the row, first column reaching it) per row.
+    int2* rowbest;
 };
+
+enum : int32_t { BM_NORMAL = 0, BM_EFREE = 1, BM_EPAID = 2 };
 
 // Sentinel of a not-yet-received left-border value (memset byte 0x80): no H value
 // of a supported problem reaches it.
@@ -71,6 +80,7 @@ struct PartInfo {
     int32_t len;          // rows of the part
     int32_t rhw;          // right-half width
     int32_t split_index;  // logical index into splits set by set_split_position
+    int32_t smode;        // affine construct: border mode of the part's start (left half)
 };
 
 // One final-level 128-column block (iteration_*:121-173).
@@ -78,6 +88,8 @@ struct BlockInfo {
     int32_t oi, h;        // rows [oi, oi+h)
     int32_t oj, w;        // cols [oj, oj+w)
     int64_t pred_base;    // byte offset of the block's anti-diagonal-major predecessor slab
+    int32_t smode;        // affine construct: start border mode (BM_NORMAL / BM_EFREE)
+    int32_t e_end;        // affine construct: the path ends in a horizontal gap (E state)
 };
 
 // Device-side error codes written to the error word.

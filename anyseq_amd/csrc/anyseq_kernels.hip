@@ -1015,10 +1015,10 @@ struct AffIO {
 // through.  FINOUT: the problem's last row publishes F[h-1][c] (not F-down), as
 // the two-front combine needs.  og/of: this lane's (G, F-out) after each step
 // (lane 63's are the band's bottom row).
-template <int KIND, bool MASK, bool PARTIAL, bool FINOUT, bool VIRT>
+template <int KIND, bool MASK, bool PARTIAL, bool FINOUT, bool VIRT, bool TRACK = false>
 __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&rv)[32], const uint32_t (&sw)[8], int q,
                                           bool dead, bool lastrow, int z, int& g, int& e, int& hg, int& fdn, int& dg,
-                                          int& best, int (&og)[32], int (&of)[32], const AffK k) {
+                                          int& best, int (&og)[32], int (&of)[32], const AffK k, int* bcol = nullptr) {
 #pragma unroll
     for (int u = 0; u < 32; ++u) {
         const int2 top = u == 0 ? tf : rv[u - 1];
@@ -1043,7 +1043,16 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
         g = act ? v : g;
         hg = act ? hn : hg;
         fdn = act ? fn : fdn;
-        if (KIND == KIND_LOCAL) best = act ? max(best, v - (z + u * k.nge)) : best;
+        if (TRACK) {
+            // row-major first maximum: this lane's row, first column reaching its best H
+            const int hv = v - (z + u * k.nge);
+            if (act && !dead && (unsigned)(c0 + u) < (unsigned)w && hv > best) {
+                best = hv;
+                *bcol = c0 + u;
+            }
+        } else if (KIND == KIND_LOCAL) {
+            best = act ? max(best, v - (z + u * k.nge)) : best;
+        }
         dg = upg;
         og[u] = g;
         of[u] = fdn;
@@ -1104,7 +1113,7 @@ __device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint3
 }
 #undef AFF_ASM
 
-template <int KIND, bool PARTIAL, bool FINOUT>
+template <int KIND, bool PARTIAL, bool FINOUT, bool TRACK = false>
 __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k) {
     constexpr int CH = 32;
     constexpr int IRM = kSlots * CH - 1;
@@ -1115,8 +1124,16 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     // the oracle's.  The prologue then runs in the asm loop.  Semiglobal / local
     // borders grow with the row and keep the masked C++ prologue.
     constexpr bool VIRT = KIND == KIND_GLOBAL && !PARTIAL && !FINOUT;
-    constexpr bool ASM = !PARTIAL && !FINOUT;
+    constexpr bool ASM = !PARTIAL && !FINOUT && !TRACK;
     const int h = P.h, w = P.w, go = k.go, nge = k.nge;
+    // border values (G space): corner, top row (c >= 0), left column (r >= 0); the
+    // affine construct's global sub-problems change them by border mode (bmode)
+    const int bm = KIND == KIND_GLOBAL ? P.bmode : BM_NORMAL;
+    const int cg = bm == BM_NORMAL ? 0 : kAffNeg;
+    const int tg = bm == BM_EFREE ? 0 : go;
+    const int lg = bm == BM_NORMAL ? go : kAffNeg;
+    auto topv = [&](int c) { return KIND == KIND_GLOBAL ? (c < 0 ? cg : tg) : aff_border<KIND>(c, go, nge); };
+    auto leftv = [&](int r) { return KIND == KIND_GLOBAL ? (r < 0 ? cg : lg) : aff_border<KIND>(r, go, nge); };
     const int rb = band * 64;
     const int row = rb + lane;
     const bool dead = row >= h;
@@ -1131,14 +1148,15 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         g = kAffNeg;
         hg = kAffNeg;
         dg = kAffNeg;
-        tf = make_int2(aff_border<KIND>(rb - 1, go, nge), go);
+        tf = make_int2(leftv(rb - 1), rb == 0 ? cg + go : lg);
     } else {
-        g = aff_border<KIND>(row, go, nge);
+        g = leftv(row);
         hg = g + go;   // the next column's E candidate: G[r][-1] + go
-        dg = aff_border<KIND>(row - 1, go, nge);
-        tf = make_int2(aff_border<KIND>(rb - 1, go, nge), kAffNeg);
+        dg = leftv(row - 1);
+        tf = make_int2(leftv(rb - 1), kAffNeg);
     }
-    int best = 0;
+    int best = TRACK ? -2147483647 : 0;
+    int bcol = -1;
     const int nchunks = (w + CH - 1) / CH;
     const int nblocks = nchunks + LAG;
     const int fe = w >= CH - 1 ? (w - (CH - 1)) / CH + 1 : 0;   // full blocks: 32b + 30 < w
@@ -1156,8 +1174,8 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         la.skb = lds_addr(io.skew) + 4u * lane;
         la.lo = 8u * (lane - 32);
         la.lid8 = 8u * lane;
-        la.bvb = (uint32_t)aff_border<KIND>(lane, go, nge);
-        la.bvs = (uint32_t)(aff_border<KIND>(1, go, nge) - aff_border<KIND>(0, go, nge));
+        la.bvb = (uint32_t)topv(lane);
+        la.bvs = (uint32_t)(topv(1) - topv(0));
         la.gp = (uint64_t)(size_t)io.gout;
     }
     for (int b = 0; b < nblocks; ++b) {
@@ -1196,7 +1214,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         int2 rv[CH];
         if (b < nchunks) {
             if (io.in_border) {
-                const int bv = aff_border<KIND>(t0 + lane, go, nge);
+                const int bv = topv(t0 + lane);
                 io.my_ring[(t0 + lane) & IRM] = make_int2(bv, bv + go);
             } else if (seen_prod < (uint32_t)(b + 1)) {
                 if (!(seen_prod = spin_lds_ge(io.my_prod, (uint32_t)(b + 1), err))) return;
@@ -1224,7 +1242,10 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         const int c0 = t0 - 1 - lane;
         const int z = (rb + t0 + 1) * nge;
         const bool full = (VIRT || t0 >= 64) && b < fe;
-        if (full)
+        if (TRACK)
+            aff_block<KIND, true, PARTIAL, FINOUT, VIRT, true>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg,
+                                                               best, og, of, k, &bcol);
+        else if (full)
             aff_block<KIND, false, PARTIAL, FINOUT, VIRT>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg, best,
                                                     og, of, k);
         else
@@ -1265,8 +1286,9 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     if (!dead) {
         if (P.out_col) gmem(P.out_col)[row] = aff_to_h(g, row, w - 1, nge);
         if (P.out_col_e) gmem(P.out_col_e)[row] = aff_to_h(e, row, w - 1, nge);
+        if (TRACK) P.rowbest[row] = make_int2(best, bcol);
     }
-    if (KIND == KIND_LOCAL && P.best) {
+    if (KIND == KIND_LOCAL && P.best && !TRACK) {
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
         if (lane == 0) atomicMax(P.best, best);
@@ -1333,7 +1355,10 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                 io.gout = band < last ? nullptr : g_out;
                 const bool partial = (band + 1) * 64 > P.h;
                 const bool finout = band == P.nbands - 1 && P.out_row != nullptr;
-                if (partial) {
+                if (KIND != KIND_SEMIGLOBAL && P.rowbest) {   // position search (no out_row)
+                    if (partial) run_band_aff<KIND, true, false, true>(P, band, lane, io, err, k);
+                    else run_band_aff<KIND, false, false, true>(P, band, lane, io, err, k);
+                } else if (partial) {
                     if (finout) run_band_aff<KIND, true, true>(P, band, lane, io, err, k);
                     else run_band_aff<KIND, true, false>(P, band, lane, io, err, k);
                 } else {
@@ -1627,6 +1652,277 @@ __global__ void walk_kernel(const BlockInfo* __restrict__ blocks, int nblocks, c
     }
 }
 
+// ======================================================= affine construct --
+// Build-defined linear-space affine alignment (semantics =
+// oracle_affine_construct in oracle/anyseq_oracle.c).
+
+// Position scans.  Rows' (best H, first column) of a TRACK fill -> the row-major
+// first maximum: out = {value, row, col}.
+__global__ __launch_bounds__(1024) void aff_rowbest_kernel(const int2* __restrict__ rb, int h, int32_t* out) {
+    __shared__ int sv[1024], sr[1024];
+    int best = -2147483647, row = 0x7fffffff;
+    for (int r = threadIdx.x; r < h; r += blockDim.x)
+        if (rb[r].x > best) {
+            best = rb[r].x;
+            row = r;
+        }
+    sv[threadIdx.x] = best;
+    sr[threadIdx.x] = row;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            const int v2 = sv[threadIdx.x + o], r2 = sr[threadIdx.x + o];
+            if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && r2 < sr[threadIdx.x])) {
+                sv[threadIdx.x] = v2;
+                sr[threadIdx.x] = r2;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = sv[0];
+        out[1] = sr[0];
+        out[2] = sr[0] < h ? rb[sr[0]].y : -1;
+    }
+}
+
+// First maximum of a sequence with index -1 = `border` and indices 0..n-1 = the
+// values (a raw (G, F) row converted to H at row `r`, or an H column).
+__device__ void first_max(bool raw, const int2* row, const int32_t* col, int n, int r, int nge, int border, int& bv,
+                          int& bi, int* sv, int* si) {
+    int best = border, idx = -1;
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        const int v = raw ? row[j].x - (r + j + 2) * nge : col[j];
+        if (v > best) {
+            best = v;
+            idx = j;
+        }
+    }
+    sv[threadIdx.x] = best;
+    si[threadIdx.x] = idx;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            const int v2 = sv[threadIdx.x + o], i2 = si[threadIdx.x + o];
+            if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && i2 < si[threadIdx.x])) {
+                sv[threadIdx.x] = v2;
+                si[threadIdx.x] = i2;
+            }
+        }
+        __syncthreads();
+    }
+    bv = sv[0];
+    bi = si[0];
+    __syncthreads();
+}
+
+// Semiglobal end / start search: first max of the last row (index -1 = rborder),
+// then of the last column (index -1 = cborder) only if strictly greater.
+// out = {value, row, col} of the cell (row h-1 / column w-1 for the row / column).
+__global__ __launch_bounds__(1024) void aff_edge_scan_kernel(const int2* __restrict__ row, int w,
+                                                             const int32_t* __restrict__ col, int h, int nge,
+                                                             int rborder, int cborder, int32_t* out) {
+    __shared__ int sv[1024], si[1024];
+    int rv, ri, cv, ci;
+    first_max(true, row, nullptr, w, h - 1, nge, rborder, rv, ri, sv, si);
+    first_max(false, nullptr, col, h, 0, nge, cborder, cv, ci, sv, si);
+    if (threadIdx.x == 0) {
+        if (cv > rv) {
+            out[0] = cv;
+            out[1] = ci;
+            out[2] = w - 1;
+        } else {
+            out[0] = rv;
+            out[1] = h - 1;
+            out[2] = ri;
+        }
+    }
+}
+
+// Hirschberg join of one part per workgroup: rows i = -1 .. len-1 ascending, H
+// join before E join, strict > (first maximum):
+//     HL(i) + HR(len-i-2),   EL(i) + ER(len-i-2) - go
+// (L = forward left half's last column, R = reversed right half's; index -1 =
+// the half's top border, a horizontal gap).  Writes the split row and its
+// crossing state (0 = H, 1 = E) at the part's split index.
+__global__ __launch_bounds__(256) void aff_hb_join_kernel(const PartInfo* __restrict__ parts, int half,
+                                                          const int32_t* __restrict__ LH, const int32_t* __restrict__ LE,
+                                                          const int32_t* __restrict__ RH,
+                                                          const int32_t* __restrict__ RE, int go, int ge,
+                                                          int32_t* splits, int32_t* types) {
+    __shared__ int sv[256], sk[256];
+    const PartInfo pi = parts[blockIdx.x];
+    const int off = pi.off, len = pi.len;
+    const int bL = (pi.smode == BM_EFREE ? 0 : go) + half * ge;
+    const int bR = go + pi.rhw * ge;
+    int best = -2147483647, key = 0x7fffffff;   // key = 2 (i + 1) + type: the candidate order
+    for (int i = (int)threadIdx.x - 1; i < len; i += blockDim.x) {
+        const int k = len - i - 2;
+        const int hl = i < 0 ? bL : LH[off + i], el = i < 0 ? bL : LE[off + i];
+        const int hr = k < 0 ? bR : RH[off + k], er = k < 0 ? bR : RE[off + k];
+        const int vh = hl + hr, ve = el + er - go;
+        if (vh > best) {
+            best = vh;
+            key = 2 * (i + 1);
+        }
+        if (ve > best) {
+            best = ve;
+            key = 2 * (i + 1) + 1;
+        }
+    }
+    sv[threadIdx.x] = best;
+    sk[threadIdx.x] = key;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            const int v2 = sv[threadIdx.x + o], k2 = sk[threadIdx.x + o];
+            if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && k2 < sk[threadIdx.x])) {
+                sv[threadIdx.x] = v2;
+                sk[threadIdx.x] = k2;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const int idx = sk[0] / 2 - 1;
+        splits[pi.split_index + 1] = off + idx + 1;
+        types[pi.split_index + 1] = sk[0] & 1;
+    }
+}
+
+// Final level: Gotoh with predecessor bytes for one 128-column block per wave,
+// the geometry of pred_kernel (lane l owns columns 2l, 2l+1, anti-diagonal
+// sweep, byte pred[base + (i+j)*128 + j]).  Byte: bits 0-1 H source (0 diag,
+// 1 E, 2 F), bit 2 E extends, bit 3 F extends.
+__global__ __launch_bounds__(64) void aff_pred_kernel(const BlockInfo* __restrict__ blocks, int nblocks,
+                                                      const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
+                                                      uint8_t* __restrict__ pred, int match, int mismatch, int go,
+                                                      int ge) {
+    const int b = blockIdx.x;
+    if (b >= nblocks) return;
+    const BlockInfo bi = blocks[b];
+    if (bi.h <= 0) return;
+    const int lane = threadIdx.x;
+    const int NEG = kAffNeg;
+    const int C = bi.smode == BM_NORMAL ? 0 : NEG;
+    const int T0 = bi.smode == BM_EFREE ? 0 : go;
+    auto top = [&](int j) { return j < 0 ? C : T0 + (j + 1) * ge; };
+    auto left = [&](int i) { return i < 0 ? C : (bi.smode == BM_NORMAL ? go + (i + 1) * ge : NEG); };
+    const int jA = 2 * lane, jB = 2 * lane + 1;
+    const int sA = jA < bi.w ? (int)S[bi.oj + jA] : 0x100;
+    const int sB = jB < bi.w ? (int)S[bi.oj + jB] : 0x100;
+    int HA = top(jA), FA = NEG, EA = NEG;   // A's current row state (row -1: the top border)
+    int HB = top(jB), FB = NEG, EB = NEG;
+    int HAo = top(jA);                       // A one step earlier: B's diagonal
+    int dA = left(-1);                       // A's diagonal (lane 0: the left border)
+    uint16_t* out16 = reinterpret_cast<uint16_t*>(pred + bi.pred_base);
+    const int nsteps = bi.h + 127;
+    for (int d = 0; d < nsteps; ++d) {
+        const int iA = d - jA, iB = d - jB;
+        // A's left neighbour = lane l-1's B at row iA (lane 0: the left border)
+        const int lH = wave_shr1(left(iA), HB);
+        const int lE = wave_shr1(NEG, EB);
+        const bool actA = iA >= 0 && iA < bi.h && jA < bi.w;
+        const bool actB = iB >= 0 && iB < bi.h && jB < bi.w;
+        const int qA = (iA >= 0 && iA < bi.h) ? (int)Q[bi.oi + iA] : 0x200;
+        const int qB = (iB >= 0 && iB < bi.h) ? (int)Q[bi.oi + iB] : 0x200;
+        // B (uses A's state before A's update: A at row iB)
+        int pB = 0;
+        int eB;
+        {
+            const int e1 = EA + ge, e2 = HA + go + ge;
+            if (e1 > e2) { eB = e1; pB |= 4; } else eB = e2;
+        }
+        int fB;
+        {
+            const int f1 = FB + ge, f2 = HB + go + ge;
+            if (f1 > f2) { fB = f1; pB |= 8; } else fB = f2;
+        }
+        int hB = HAo + (qB == sB ? match : mismatch);
+        if (eB > hB) { hB = eB; pB = (pB & ~3) | 1; }
+        if (fB > hB) { hB = fB; pB = (pB & ~3) | 2; }
+        // A
+        int pA = 0;
+        int eA;
+        {
+            const int e1 = lE + ge, e2 = lH + go + ge;
+            if (e1 > e2) { eA = e1; pA |= 4; } else eA = e2;
+        }
+        int fA;
+        {
+            const int f1 = FA + ge, f2 = HA + go + ge;
+            if (f1 > f2) { fA = f1; pA |= 8; } else fA = f2;
+        }
+        int hA = dA + (qA == sA ? match : mismatch);
+        if (eA > hA) { hA = eA; pA = (pA & ~3) | 1; }
+        if (fA > hA) { hA = fA; pA = (pA & ~3) | 2; }
+        dA = lH;   // next step's diagonal of A: lane l-1's B at row iA
+        if (actB) {
+            HB = hB;
+            FB = fB;
+            EB = eB;
+        }
+        HAo = HA;
+        if (actA) {
+            HA = hA;
+            FA = fA;
+            EA = eA;
+        }
+        const uint16_t pk = (uint16_t)((actA ? pA : 0) | ((actB ? pB : 0) << 8));
+        out16[(size_t)d * 64 + lane] = pk;
+    }
+}
+
+// One thread per block: walk from the block's end (state H, or E after an E
+// crossing) to its start; borders are gap runs; sparse i+j+1 output.
+__global__ void aff_walk_kernel(const BlockInfo* __restrict__ blocks, int nblocks, const uint8_t* __restrict__ Q,
+                                const uint8_t* __restrict__ S, const uint8_t* __restrict__ pred, uint8_t* alq,
+                                uint8_t* als) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblocks) return;
+    const BlockInfo bi = blocks[b];
+    const int64_t base = (int64_t)bi.oi + bi.oj;
+    int i = bi.h - 1, j = bi.w - 1;
+    int st = bi.e_end ? 1 : 0;
+    while (i >= 0 || j >= 0) {
+        const int64_t pos = base + i + j + 1;
+        if (i < 0) {
+            alq[pos] = '_';
+            als[pos] = S[bi.oj + j];
+            --j;
+            continue;
+        }
+        if (j < 0) {
+            alq[pos] = Q[bi.oi + i];
+            als[pos] = '_';
+            --i;
+            continue;
+        }
+        const int pb = pred[bi.pred_base + (int64_t)(i + j) * 128 + j];
+        if (st == 0) {
+            const int hs = pb & 3;
+            if (hs == 0) {
+                alq[pos] = Q[bi.oi + i];
+                als[pos] = S[bi.oj + j];
+                --i;
+                --j;
+            } else {
+                st = hs;
+            }
+        } else if (st == 1) {
+            alq[pos] = '_';
+            als[pos] = S[bi.oj + j];
+            st = (pb & 4) ? 1 : 0;
+            --j;
+        } else {
+            alq[pos] = Q[bi.oi + i];
+            als[pos] = '_';
+            st = (pb & 8) ? 2 : 0;
+            --i;
+        }
+    }
+}
+
 // --------------------------------------------------------------- launchers --
 #ifndef ANYSEQ_MICRO   // tools/micro includes the kernels without the launchers
 template <int KIND, int R, int X, int NW, int CH>
@@ -1744,6 +2040,43 @@ hipError_t anyseq_launch_shard_combine(int kind, const int32_t* rowT, int h1, co
                                        hipStream_t st) {
     hipLaunchKernelGGL(anyseq::shard_combine_kernel, dim3(64), dim3(256), 0, st, kind, rowT, h1, rowB, h2, w, gap, lT,
                        sT, lB, sB, last, colT, colB, adj, out);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_aff_rowbest(const void* rowbest, int h, int32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(anyseq::aff_rowbest_kernel, dim3(1), dim3(1024), 0, st, (const int2*)rowbest, h, out);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_aff_edge_scan(const void* row, int w, const int32_t* col, int h, int nge, int rborder,
+                                       int cborder, int32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(anyseq::aff_edge_scan_kernel, dim3(1), dim3(1024), 0, st, (const int2*)row, w, col, h, nge,
+                       rborder, cborder, out);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, const int32_t* LH, const int32_t* LE,
+                                     const int32_t* RH, const int32_t* RE, int go, int ge, int32_t* splits,
+                                     int32_t* types, hipStream_t st) {
+    if (nparts > 0)
+        hipLaunchKernelGGL(anyseq::aff_hb_join_kernel, dim3(nparts), dim3(256), 0, st,
+                           (const anyseq::PartInfo*)parts, half, LH, LE, RH, RE, go, ge, splits, types);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_aff_pred(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
+                                  int match, int mismatch, int go, int ge, hipStream_t st) {
+    if (nblocks > 0)
+        hipLaunchKernelGGL(anyseq::aff_pred_kernel, dim3(nblocks), dim3(64), 0, st,
+                           (const anyseq::BlockInfo*)blocks, nblocks, Q, S, pred, match, mismatch, go, ge);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_aff_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
+                                  const uint8_t* pred, uint8_t* alq, uint8_t* als, hipStream_t st) {
+    if (nblocks > 0)
+        hipLaunchKernelGGL(anyseq::aff_walk_kernel, dim3((nblocks + 63) / 64), dim3(64), 0, st,
+                           (const anyseq::BlockInfo*)blocks, nblocks, Q, S, pred, alq, als);
     return hipGetLastError();
 }
 

@@ -1,0 +1,68 @@
+"""GPU parity of the build-defined affine construct (anyseq_construct with gap_open < 0).
+
+HIP path (C-ABI anyseq_construct) vs the oracle restatement
+(oracle_affine_construct): score and both sparse i+j+1 strings bit-exact.  The
+oracle itself is pinned by optimality/validity properties in
+tests/test_oracle_affine.py (affine gaps have no reference semantics).
+"""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ("global", "semiglobal", "local")
+SCHEMES = [(2, -1, -2, -1), (1, -3, -5, -2), (5, -4, -10, -1), (3, -2, -1, -3), (2, -1, -1, -1)]
+
+
+def rnd(rng, n, alphabet=b"ACGT"):
+    return bytes(rng.choice(alphabet) for _ in range(n))
+
+
+def same(anyseq, oracle, kind, q, s, sc):
+    g = anyseq.construct(kind, q, s, match=sc[0], mismatch=sc[1], gap_open=sc[2], gap_extend=sc[3])
+    o = oracle.affine_construct(kind, q, s, *sc)
+    assert g[0] == o[0], (kind, len(q), len(s), sc, "score", g[0], o[0])
+    assert g[1] == o[1] and g[2] == o[2], (kind, len(q), len(s), sc, "strings")
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_construct_random(anyseq, oracle, kind):
+    rng = random.Random(51)
+    for it in range(30):
+        sc = SCHEMES[it % len(SCHEMES)]
+        same(anyseq, oracle, kind, rnd(rng, rng.randint(1, 300)), rnd(rng, rng.randint(1, 700)), sc)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_construct_shapes(anyseq, oracle, kind):
+    rng = random.Random(52)
+    for n in (0, 1, 2, 63, 64, 65, 129, 300):
+        for m in (0, 1, 64, 127, 128, 129, 255, 256, 257, 700):
+            same(anyseq, oracle, kind, rnd(rng, n), rnd(rng, m), (2, -1, -2, -1))
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_construct_long_gaps(anyseq, oracle, kind):
+    rng = random.Random(53)
+    core = rnd(rng, 900)
+    ins = rnd(rng, 350)
+    q = core[:400] + core[700:]
+    s = core[:200] + ins + core[200:]
+    for sc in [(2, -1, -8, -1), (2, -1, -2, -1), (1, -1, -20, -1)]:
+        same(anyseq, oracle, kind, q, core, sc)
+        same(anyseq, oracle, kind, core, s, sc)
+        same(anyseq, oracle, kind, s, q, sc)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_construct_multi_group(anyseq, oracle, kind):
+    """Several workgroups per sub-problem, several Hirschberg levels, similar sequences."""
+    rng = random.Random(54)
+    base = rnd(rng, 3000)
+    mut = bytearray(base)
+    for _ in range(120):
+        mut[rng.randrange(len(mut))] = rng.choice(b"ACGT")
+    same(anyseq, oracle, kind, base, bytes(mut[100:2900]), (2, -1, -3, -1))
+    same(anyseq, oracle, kind, rnd(rng, 2500), rnd(rng, 2100), (2, -1, -2, -1))
+    same(anyseq, oracle, kind, rnd(rng, 60) + base[300:2000] + rnd(rng, 90), base, (1, -3, -5, -2))
