@@ -149,15 +149,31 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     // the affine fill has one row per lane and hands (G, F) pairs over (twice the row bytes)
     const int R = aff ? 1 : rows_per_lane(), NW = aff ? (g_tuning.NWa == 3 ? 3 : 4) : waves_per_group();
     const int vpc = aff ? 2 : 1;
-    size_t rowbuf_ints = 0, flag_words = 0;
+    // Persistent grid: at most `grid` groups are in flight, and a group finishes only after
+    // its predecessor in the same problem (it consumes that group's last chunk), so the
+    // groups of a problem in flight when group k starts are within [k-grid+1, k].  Hand-off
+    // rows therefore live in a ring of nslots >= 2*grid+2 rows per problem (group k writes
+    // slot k % nslots, the reader puts the sentinel back): O(grid * w) memory instead of
+    // O(h/64 * w), which is what makes genome-length matrices fit.
     int max_groups = 0;
+    size_t total_groups = 0;
     for (auto& P : probs) {
         P.nbands = (P.h + 64 * R - 1) / (64 * R);
         P.ngroups = (P.nbands + NW - 1) / NW;
         P.wpad = (P.w + 63) & ~63;
-        rowbuf_ints += (size_t)std::max(P.ngroups - 1, 0) * P.wpad * vpc;
-        flag_words += P.ngroups;
         max_groups = std::max(max_groups, P.ngroups);
+        total_groups += (size_t)P.ngroups;
+    }
+    int grid = aff ? (g_tuning.grida > 0 ? g_tuning.grida : E.num_cus) : (g_tuning.grid > 0 ? g_tuning.grid : E.num_cus);
+    if (grid_req > 0) grid = grid_req;
+    grid = (int)std::min<size_t>((size_t)grid, std::max<size_t>(total_groups, 1));
+    const int min_slots = 2 * grid + 2;
+    const int want_slots = std::max(g_tuning.ring_slots > 0 ? g_tuning.ring_slots : 2 * min_slots, min_slots);
+    size_t rowbuf_ints = 0, flag_words = 0;
+    for (auto& P : probs) {
+        P.nslots = std::max(1, std::min(P.ngroups - 1, want_slots));
+        rowbuf_ints += (size_t)(P.ngroups > 1 ? P.nslots : 0) * P.wpad * vpc;
+        flag_words += P.ngroups;
     }
     int32_t* rowbuf = (int32_t*)C.rowbuf.get(rowbuf_ints * 4);
     uint32_t* flags = (uint32_t*)C.flags.get((flag_words + 4) * 4);
@@ -165,7 +181,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     for (auto& P : probs) {
         P.rowbuf = rowbuf + ro;
         P.flags = flags + fo;
-        ro += (size_t)std::max(P.ngroups - 1, 0) * P.wpad * vpc;
+        ro += (size_t)(P.ngroups > 1 ? P.nslots : 0) * P.wpad * vpc;
         fo += P.ngroups;
     }
     // group table: round-robin over problems so every sub-problem progresses
@@ -190,9 +206,6 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     if (rowbuf_ints) HIPCHECK(hipMemsetAsync(rowbuf, aff ? 0x80 : 0xff, rowbuf_ints * 4, st));
     uint32_t* ctr = (uint32_t*)C.ctr.get(128);
     HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));  // ctr[0] = dequeue counter, ctr[1] = error word
-    int grid = aff ? (g_tuning.grida > 0 ? g_tuning.grida : E.num_cus) : (g_tuning.grid > 0 ? g_tuning.grid : E.num_cus);
-    if (grid_req > 0) grid = grid_req;
-    grid = std::min<int>(grid, (int)groups.size());
     FillParams fpl = fp;
     unsigned long long* dbg = nullptr;
     static DevBuf stamp_buf;
@@ -926,6 +939,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_waves_per_group") g_tuning.NWa = value;
     else if (n == "affine_grid") g_tuning.grida = value;
     else if (n == "affine_asm") g_tuning.affasm = value;
+    else if (n == "ring_slots") g_tuning.ring_slots = value;
     else return -1;
     return 0;
 }

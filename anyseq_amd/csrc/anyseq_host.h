@@ -52,6 +52,7 @@ struct Tuning {
     int NWa = 4;     // affine fill: compute waves per workgroup (3 or 4)
     int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
     int affasm = 1;  // affine fill: asm steady state (0 = C++ blocks only, diagnostics)
+    int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
 };
 extern Tuning g_tuning;
 

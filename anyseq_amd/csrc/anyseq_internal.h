@@ -28,10 +28,10 @@ struct DPProblem {
     int32_t nbands;        // ceil(h / (64*R))
     int32_t ngroups;       // ceil(nbands / NW)
     int32_t wpad;          // row-buffer pitch (multiple of 64, >= w)
-    int32_t pad0;
+    int32_t nslots;        // hand-off rows in the ring: group k writes slot k % nslots
     int32_t* out_col;      // optional: H[r][w-1] for r in [0,h)
     int32_t* out_row;      // optional: raw (kernel value space) bottom row, >= wpad ints
-    int32_t* rowbuf;       // (ngroups-1) * wpad ints: group -> group hand-off rows
+    int32_t* rowbuf;       // nslots * wpad ints: ring of group -> group hand-off rows
     uint32_t* flags;       // ngroups entries, chunk progress of each group's last band
     int32_t* best;         // optional (local): atomicMax of every cell
     int32_t* out_col_e;    // optional (affine): E[r][w-1] (H space) for r in [0,h)

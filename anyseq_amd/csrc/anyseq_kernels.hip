@@ -733,8 +733,12 @@ struct HandOff<int32_t> {
     __device__ static int32_t load(const int32_t* p) {
         return __hip_atomic_load(gmem(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __device__ static void store(int32_t* p, int32_t v) {
+        __hip_atomic_store(gmem(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __device__ static bool pending(int32_t v) { return v == -1; }
     __device__ static int32_t zero() { return 0; }
+    __device__ static int32_t sentinel() { return -1; }
 };
 template <>
 struct HandOff<int2> {
@@ -749,12 +753,13 @@ struct HandOff<int2> {
     }
     __device__ static bool pending(int2 v) { return v.x == (int)0x80808080; }
     __device__ static int2 zero() { return make_int2(0, 0); }
+    __device__ static int2 sentinel() { return make_int2((int)0x80808080, (int)0x80808080); }
 };
 
 template <int CH, bool SKEW, typename T = int32_t>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
                         uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
-                        uint32_t* cons0, uint32_t* err) {
+                        uint32_t* cons0, uint32_t* err, bool reset_in = false) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
     const int nchunks = (w + CH - 1) / CH;
@@ -843,6 +848,17 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                         const int col = c0 + i * 64 + lane;
                         if (col < c2) ring0[col & IRM] = v[i];
                     }
+                    // ring of hand-off rows (DPProblem::nslots < ngroups - 1): put the sentinel
+                    // back, so the group that reuses this slot 2*grid+2 groups later is polled
+                    // against fresh data
+                    if (reset_in) {
+                        T* gw = const_cast<T*>(g_in);
+#pragma unroll
+                        for (int i = 0; i < PER; ++i) {
+                            const int col = c0 + i * 64 + lane;
+                            if (col < c2 && col < w) HandOff<T>::store(gw + col, HandOff<T>::sentinel());
+                        }
+                    }
                     lds_st(prod0, (uint32_t)(in_next + ready));
                     in_next += ready;
                     progress = true;
@@ -900,14 +916,14 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
         // stores it there itself.
         int32_t* g_out = nullptr;
         if (last < P.nbands - 1)
-            g_out = P.rowbuf + (size_t)g.group * P.wpad;
+            g_out = P.rowbuf + (size_t)(g.group % P.nslots) * P.wpad;
         else if (P.out_row)
             g_out = P.out_row;
         if (wave == NW) {
-            const int32_t* g_in = g.group > 0 ? P.rowbuf + (size_t)(g.group - 1) * P.wpad : nullptr;
+            const int32_t* g_in = g.group > 0 ? P.rowbuf + (size_t)((g.group - 1) % P.nslots) * P.wpad : nullptr;
             io_wave<CH, R == 1 && X == 0 && CH == 32>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0],
                                                       &sh.s_filled, &sh.tail, g_in, sh.in_ring[0], &sh.prod[0],
-                                                      &sh.cons[0], err);
+                                                      &sh.cons[0], err, P.nslots < P.ngroups - 1);
         } else {
             const int band = first + wave;
             if (band <= last) {
@@ -1328,13 +1344,14 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
         int2* rows = reinterpret_cast<int2*>(P.rowbuf);
         int2* g_out = nullptr;
         if (last < P.nbands - 1)
-            g_out = rows + (size_t)gr.group * P.wpad;
+            g_out = rows + (size_t)(gr.group % P.nslots) * P.wpad;
         else if (P.out_row)
             g_out = reinterpret_cast<int2*>(P.out_row);
         if (wave == NW) {
-            const int2* g_in = gr.group > 0 ? rows + (size_t)(gr.group - 1) * P.wpad : nullptr;
+            const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
             io_wave<32, true, int2>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0], &sh.s_filled,
-                                    &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err);
+                                    &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
+                                    P.nslots < P.ngroups - 1);
         } else {
             const int band = first + wave;
             if (band <= last) {

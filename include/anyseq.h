@@ -84,7 +84,9 @@ void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid);
 
 /* Named tuning option: "rows_per_lane" (1,2,4), "chunk" (16,32 steps per block),
  * "waves_per_group" (3,4,7,8), "grid", "fronts" (1 or 2: score fill as one
- * front or two meeting fronts).
+ * front or two meeting fronts), "affine_waves_per_group" (3,4), "affine_grid",
+ * "ring_slots" (group hand-off rows kept per sub-problem; 0 = 4*grid+4, never
+ * fewer than 2*grid+2).
  * Returns 0, or -1 for an unknown name. */
 int anyseq_set_option(const char* name, int value);
 
