@@ -61,6 +61,9 @@ _lib.anyseq_score_device.argtypes = [_c_int, ctypes.POINTER(Scoring), _vp, _c_in
 _lib.anyseq_construct.restype = _c_int
 _lib.anyseq_construct.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _vp, _vp,
                                   ctypes.POINTER(_c_i64)]
+_lib.anyseq_construct_device.restype = _c_int
+_lib.anyseq_construct_device.argtypes = [_c_int, ctypes.POINTER(Scoring), _vp, _c_int, _vp, _c_int, _vp, _vp, _vp,
+                                         ctypes.POINTER(_c_i64)]
 _lib.anyseq_shard_score_local.restype = _c_int
 _lib.anyseq_shard_score_local.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _c_int,
                                           ctypes.POINTER(_c_i64)]
@@ -79,6 +82,8 @@ _lib.anyseq_set_tuning.argtypes = [_c_int, _c_int, _c_int]
 _lib.anyseq_set_option.restype = _c_int
 _lib.anyseq_set_option.argtypes = [_c_p, _c_int]
 _lib.anyseq_last_fill_timing.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int)]
+_lib.anyseq_last_fill_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int),
+                                        ctypes.POINTER(_c_i64)]
 _lib.anyseq_main_random_pair.argtypes = [_c_i64, _c_i64, _vp, ctypes.POINTER(_c_i64), _vp,
                                          ctypes.POINTER(_c_i64)]
 
@@ -182,6 +187,19 @@ def construct(kind, query, subject, match=2, mismatch=-1, gap_open=0, gap_extend
     return out.value, aq.raw[:L], as_.raw[:L]
 
 
+def construct_device(kind, q_ptr: int, n: int, s_ptr: int, m: int, alq_ptr: int, als_ptr: int, stream: int = 0,
+                     match=2, mismatch=-1, gap_open=0, gap_extend=-1) -> int:
+    """Construct on device-resident sequences into device strings (n+m bytes each);
+    returns the optimal score."""
+    out = _c_i64(0)
+    sc = _scoring(match, mismatch, gap_open, gap_extend)
+    if _lib.anyseq_construct_device(_kind(kind), ctypes.byref(sc), ctypes.c_void_p(q_ptr), n, ctypes.c_void_p(s_ptr),
+                                    m, ctypes.c_void_p(alq_ptr), ctypes.c_void_p(als_ptr),
+                                    ctypes.c_void_p(stream or None), ctypes.byref(out)) != 0:
+        raise AnySeqError(_err())
+    return out.value
+
+
 def shard_score_local(kind, query, subject, nshards: int, match=2, mismatch=-1, gap_open=0, gap_extend=-1) -> int:
     """Column-block sharded score with `nshards` shards in this process on one GPU
     (the same kernels, progress counters and chunked hand-off as the RCCL path,
@@ -214,6 +232,13 @@ def last_fill_timing():
     ms, n = ctypes.c_double(0.0), _c_int(0)
     _lib.anyseq_last_fill_timing(ctypes.byref(ms), ctypes.byref(n))
     return ms.value, n.value
+
+
+def last_fill_stats():
+    """(milliseconds, launches, DP cells) of the fill kernels since the previous call."""
+    ms, n, c = ctypes.c_double(0.0), _c_int(0), _c_i64(0)
+    _lib.anyseq_last_fill_stats(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(c))
+    return ms.value, n.value, c.value
 
 
 def main_random_pair(minlen: int, maxlen: int):

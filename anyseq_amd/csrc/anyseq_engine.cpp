@@ -62,6 +62,7 @@ constexpr int CPU_BLOCK_WIDTH = 1024;              // iteration_cpu.impala:1 (hb
 thread_local std::string g_last_error;
 thread_local double g_fill_ms = 0.0;
 thread_local int g_fill_launches = 0;
+thread_local int64_t g_fill_cells = 0;
 
 void set_last_error(const std::string& m) { g_last_error = m; }
 
@@ -170,7 +171,9 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     const int min_slots = 2 * grid + 2;
     const int want_slots = std::max(g_tuning.ring_slots > 0 ? g_tuning.ring_slots : 2 * min_slots, min_slots);
     size_t rowbuf_ints = 0, flag_words = 0;
+    C.cells = 0;
     for (auto& P : probs) {
+        C.cells += (int64_t)P.h * P.w;
         P.nslots = std::max(1, std::min(P.ngroups - 1, want_slots));
         rowbuf_ints += (size_t)(P.ngroups > 1 ? P.nslots : 0) * P.wpad * vpc;
         flag_words += P.ngroups;
@@ -252,6 +255,7 @@ void fill_finish(FillCtx& C) {
     HIPCHECK(hipEventElapsedTime(&ms, C.ev0, C.ev1));
     g_fill_ms += ms;
     g_fill_launches += 1;
+    g_fill_cells += C.cells;
     uint32_t err = 0;
     uint32_t* ctr = (uint32_t*)C.ctr.get(128);
     HIPCHECK(hipMemcpy(&err, ctr + 1, 4, hipMemcpyDeviceToHost));
@@ -486,24 +490,18 @@ struct HostSplits {  // traceback_lintime.impala:1-42 (logical index -1 at stora
     }
 };
 
-// Linear-space construct (traceback_lintime, align.impala:237-311) on the GPU.
-void construct_host(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m, char* alq,
-                    char* als) {
-    Engine& E = engine();
-    std::lock_guard<std::mutex> lk(E.mu);
-    hipStream_t st = E.stream;
+// Linear-space construct (traceback_lintime, align.impala:237-311) on the GPU, on
+// device-resident sequences, into device strings d_alq/d_als of n+m bytes (the
+// sparse i+j+1 layout, blanks first).  Enqueued on st; returns after the last
+// kernel has been enqueued (the level loop syncs on the split vector).
+void construct_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds, int m,
+                   uint8_t* d_alq, uint8_t* d_als, hipStream_t st) {
     const size_t L = (size_t)n + (size_t)m;
     if (L == 0) return;
-    if (m <= 0) {  // no 128-column block: the reference writes only blanks
-        memset(alq, ' ', L);
-        memset(als, ' ', L);
-        return;
-    }
+    HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
+    HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
+    if (m <= 0) return;  // no 128-column block: the reference writes only blanks
     const FillParams fp = make_params(kind, sc);
-    uint8_t* dq = (uint8_t*)E.q.get((size_t)std::max(n, 1));
-    uint8_t* ds = (uint8_t*)E.s.get((size_t)m);
-    if (n > 0) HIPCHECK(hipMemcpyAsync(dq, q, (size_t)n, hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemcpyAsync(ds, s, (size_t)m, hipMemcpyHostToDevice, st));
 
     HostSplits sp;
     sp.nb = (m + MIN_PART_WIDTH_HB - 1) / MIN_PART_WIDTH_HB;
@@ -586,12 +584,24 @@ void construct_host(int kind, const anyseq_scoring& sc, const char* q, int n, co
     BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
     HIPCHECK(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, st));
     uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
-    uint8_t* d_alq = (uint8_t*)E.alq.get(L);
-    uint8_t* d_als = (uint8_t*)E.als.get(L);
-    HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
-    HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
     HIPCHECK(anyseq_launch_pred(d_blocks, sp.nb, dq, ds, d_pred, &fp, st));
     HIPCHECK(anyseq_launch_walk(d_blocks, sp.nb, dq, ds, d_pred, kind, d_alq, d_als, st));
+}
+
+void construct_host(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m, char* alq,
+                    char* als) {
+    Engine& E = engine();
+    std::lock_guard<std::mutex> lk(E.mu);
+    hipStream_t st = E.stream;
+    const size_t L = (size_t)n + (size_t)m;
+    if (L == 0) return;
+    uint8_t* dq = (uint8_t*)E.q.get((size_t)std::max(n, 1));
+    uint8_t* ds = (uint8_t*)E.s.get((size_t)std::max(m, 1));
+    if (n > 0) HIPCHECK(hipMemcpyAsync(dq, q, (size_t)n, hipMemcpyHostToDevice, st));
+    if (m > 0) HIPCHECK(hipMemcpyAsync(ds, s, (size_t)m, hipMemcpyHostToDevice, st));
+    uint8_t* d_alq = (uint8_t*)E.alq.get(L);
+    uint8_t* d_als = (uint8_t*)E.als.get(L);
+    construct_dev(E, kind, sc, dq, n, ds, m, d_alq, d_als, st);
     HIPCHECK(hipMemcpyAsync(alq, d_alq, L, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(als, d_als, L, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -739,27 +749,21 @@ void aff_construct_rect(Engine& E, const anyseq_scoring& sc, const uint8_t* dq, 
     HIPCHECK(anyseq_launch_aff_walk(d_blocks, sp.nb, dq, ds, d_pred, d_alq, d_als, st));
 }
 
-int64_t construct_affine_host(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m,
-                              char* alq, char* als) {
-    Engine& E = engine();
-    std::lock_guard<std::mutex> lk(E.mu);
-    hipStream_t st = E.stream;
+// Affine construct on device-resident sequences into device strings (n+m bytes);
+// returns the optimal score.
+int64_t construct_affine_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n,
+                             const uint8_t* ds, int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st) {
     const size_t L = (size_t)n + (size_t)m;
     if (L == 0) return empty_score(kind, n, m, sc);
-    memset(alq, ' ', L);
-    memset(als, ' ', L);
+    HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
+    HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
     if (n <= 0 || m <= 0) {
-        if (kind == KIND_GLOBAL && m <= 0)   // all query rows against gaps, down the left border
-            for (int i = 0; i < n; ++i) {
-                alq[i] = q[i];
-                als[i] = '_';
-            }
+        if (kind == KIND_GLOBAL && m <= 0 && n > 0) {   // all query rows against gaps, down the left border
+            HIPCHECK(hipMemcpyAsync(d_alq, dq, (size_t)n, hipMemcpyDeviceToDevice, st));
+            HIPCHECK(hipMemsetAsync(d_als, '_', (size_t)n, st));
+        }
         if (kind != KIND_GLOBAL || m <= 0) return empty_score(kind, n, m, sc);
     }
-    uint8_t* dq = (uint8_t*)E.q.get((size_t)std::max(n, 1));
-    uint8_t* ds = (uint8_t*)E.s.get((size_t)std::max(m, 1));
-    if (n > 0) HIPCHECK(hipMemcpyAsync(dq, q, (size_t)n, hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemcpyAsync(ds, s, (size_t)m, hipMemcpyHostToDevice, st));
     int is = 0, ie = n - 1, js = 0, je = m - 1;
     int64_t score = 0;
     if (kind == KIND_GLOBAL) {
@@ -779,11 +783,24 @@ int64_t construct_affine_host(int kind, const anyseq_scoring& sc, const char* q,
         js = je - start.j;
     }
     const int n2 = ie - is + 1, m2 = je - js + 1;
+    aff_construct_rect(E, sc, dq + is, n2, ds + js, m2, d_alq + is + js, d_als + is + js, st);
+    return score;
+}
+
+int64_t construct_affine_host(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m,
+                              char* alq, char* als) {
+    Engine& E = engine();
+    std::lock_guard<std::mutex> lk(E.mu);
+    hipStream_t st = E.stream;
+    const size_t L = (size_t)n + (size_t)m;
+    if (L == 0) return empty_score(kind, n, m, sc);
+    uint8_t* dq = (uint8_t*)E.q.get((size_t)std::max(n, 1));
+    uint8_t* ds = (uint8_t*)E.s.get((size_t)std::max(m, 1));
+    if (n > 0) HIPCHECK(hipMemcpyAsync(dq, q, (size_t)n, hipMemcpyHostToDevice, st));
+    if (m > 0) HIPCHECK(hipMemcpyAsync(ds, s, (size_t)m, hipMemcpyHostToDevice, st));
     uint8_t* d_alq = (uint8_t*)E.alq.get(L);
     uint8_t* d_als = (uint8_t*)E.als.get(L);
-    HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
-    HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
-    aff_construct_rect(E, sc, dq + is, n2, ds + js, m2, d_alq + is + js, d_als + is + js, st);
+    const int64_t score = construct_affine_dev(E, kind, sc, dq, n, ds, m, d_alq, d_als, st);
     HIPCHECK(hipMemcpyAsync(alq, d_alq, L, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(als, d_als, L, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -898,6 +915,33 @@ int anyseq_construct(int kind, const anyseq_scoring* sc, const char* query, int 
     }
 }
 
+int anyseq_construct_device(int kind, const anyseq_scoring* sc, const uint8_t* d_query, int lenq,
+                            const uint8_t* d_subject, int lens, uint8_t* d_alQuery, uint8_t* d_alSubject, void* stream,
+                            int64_t* score) {
+    try {
+        const anyseq_scoring s = sc ? *sc : kAbiScoring;
+        check_scoring(kind, s);
+        if (lenq < 0 || lens < 0) fail("negative sequence length");
+        Engine& E = engine();
+        std::lock_guard<std::mutex> lk(E.mu);
+        hipStream_t st = stream ? (hipStream_t)stream : E.stream;
+        int64_t v;
+        if (s.gap_open != 0) {
+            v = construct_affine_dev(E, kind, s, d_query, lenq, d_subject, lens, d_alQuery, d_alSubject, st);
+        } else {
+            construct_dev(E, kind, s, d_query, lenq, d_subject, lens, d_alQuery, d_alSubject, st);
+            v = lenq > 0 && lens > 0 ? score_dev(E, kind, s, d_query, lenq, d_subject, lens, st)
+                                     : empty_score(kind, lenq, lens, s);
+        }
+        HIPCHECK(hipStreamSynchronize(st));
+        if (score) *score = v;
+        return 0;
+    } catch (const Failure& f) {
+        g_last_error = f.msg;
+        return -1;
+    }
+}
+
 int anyseq_set_device(int device) {
     std::lock_guard<std::mutex> lk(g_engines_mu);
     g_device = device;
@@ -945,10 +989,16 @@ int anyseq_set_option(const char* name, int value) {
 }
 
 void anyseq_last_fill_timing(double* ms, int* launches) {
+    anyseq_last_fill_stats(ms, launches, nullptr);
+}
+
+void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells) {
     if (ms) *ms = g_fill_ms;
     if (launches) *launches = g_fill_launches;
+    if (cells) *cells = g_fill_cells;
     g_fill_ms = 0.0;
     g_fill_launches = 0;
+    g_fill_cells = 0;
 }
 
 void anyseq_main_random_pair(int64_t minlen, int64_t maxlen, char* query, int64_t* lenq, char* subject,

@@ -68,6 +68,7 @@ struct FillCtx {
     DPProblem* d_probs = nullptr;
     GroupRef* d_groups = nullptr;
     int ngroups = 0, grid = 0;
+    int64_t cells = 0;                      // DP cells of the prepared launch (sum of h*w)
     FillParams fp{};
     hipStream_t st = nullptr;
     void init();

@@ -15,6 +15,13 @@ neighbouring ranks in 1024-row chunks with RCCL send/recv over xGMI while the
 fills run (libanyseq.so, anyseq_shard.cpp).  torch.distributed
 (gloo) is the control plane only: barrier, max-over-ranks time, RCCL ids.
 
+--config 2 (BASELINE.json configs[2], the north-star target): local (SW) affine
+alignment (+2/-1, open -2, extend -1) of the same 65536^2 pair, score + Hirschberg
+traceback: one step = anyseq_construct_device into device strings.
+--config 3 (configs[3]): semi-global affine linear-memory traceback of a 4.64 Mbp
+synthetic related-genome pair (the E. coli / S. boydii FASTAs are absent from the
+reference snapshot; anyseq_amd/genome.py), or of --fasta Q S (first records).
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -44,6 +51,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="run the RCCL column-block path even at N=1 (plumbing check; the N=1 line is single GPU)")
+    ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3],
+                    help="BASELINE.json configs index: 1 NW linear score, 2 SW affine score+traceback, "
+                         "3 genome semi-global affine traceback")
+    ap.add_argument("--fasta", nargs=2, metavar=("QUERY", "SUBJECT"), help="config 3: real genome files")
     ap.add_argument("--cpu-threads", type=int, default=4,
                     help="oracle threads (reference get_thread_count() = 4, backend_cpu.impala:13)")
     return ap.parse_args()
@@ -77,8 +88,102 @@ def cpu_baseline(q: bytes, s: bytes, kind: str, threads: int, expect: int):
                       f"scoring_cpu, 1024^2 tiles, {threads} threads), {dt:.2f} s"}
 
 
+AFFINE = dict(match=2, mismatch=-1, gap_open=-2, gap_extend=-1)
+
+
+def cpu_baseline_construct(q: bytes, s: bytes, kind: str, side: int):
+    """Oracle affine construct (single-threaded restatement) on a side x side prefix sample."""
+    from oracle import oracle as O   # bench.py's cpu_baseline leg is allowed to use the oracle
+    O.build()
+    qs, ss = q[:side], s[:side]
+    t = time.perf_counter()
+    O.affine_construct(kind, qs, ss, **AFFINE)
+    dt = time.perf_counter() - t
+    return {"value": round(len(qs) * len(ss) / dt / 1e9, 4), "unit": "GCUPS", "cores": 1, "kind": "port",
+            "sample": f"{len(qs)}x{len(ss)} prefix of the same pair, {kind} affine score + linear-memory "
+                      f"traceback (oracle_affine_construct, 1 thread), {dt:.2f} s"}
+
+
+def construct_bench(args):
+    """configs[2] / configs[3]: affine construct (score + Hirschberg traceback) on one GPU."""
+    import torch
+    import anyseq_amd as A
+    from anyseq_amd import genome
+    A.set_device(0)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    if args.config == 2:
+        kind = "local"
+        q, s = A.main_random_pair(args.n, args.m)
+        data = "synthetic: main.cpp `-r 65536 65536` generator (mt19937_64 default seed, uniform ACGT)"
+        workload = f"local (SW) affine alignment, score + Hirschberg traceback, {len(q)}x{len(s)}"
+    else:
+        kind = "semiglobal"
+        if args.fasta:
+            (_, q), (_, s) = genome.first_record(args.fasta[0]), genome.first_record(args.fasta[1])
+            data = f"FASTA first records: {os.path.basename(args.fasta[0])}, {os.path.basename(args.fasta[1])}"
+        else:
+            q, s = genome.synthetic_related_pair(4_641_652, 0.9)
+            data = ("synthetic related-genome pair (E. coli K-12 length, 90% identity; the reference's "
+                    "ecoli/sboydii FASTAs are absent)")
+        workload = f"semi-global affine alignment, linear-memory traceback, {len(q)}x{len(s)}"
+    n, m = len(q), len(s)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    dq = torch.frombuffer(bytearray(q), dtype=torch.uint8).to(dev)
+    ds = torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev)
+    alq = torch.empty(n + m, dtype=torch.uint8, device=dev)
+    als = torch.empty(n + m, dtype=torch.uint8, device=dev)
+
+    def step():
+        return A.construct_device(kind, dq.data_ptr(), n, ds.data_ptr(), m, alq.data_ptr(), als.data_ptr(),
+                                  stream=sh, **AFFINE)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    A.last_fill_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        score = step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    fill_ms, launches, fill_cells = A.last_fill_stats()
+    # the alignment re-scored on the host equals the fill's optimum (size-independent check)
+    rs = genome.affine_rescore(alq.cpu().numpy().tobytes(), als.cpu().numpy().tobytes(), **AFFINE)
+    if rs != score:
+        raise SystemExit(f"construct strings score {rs} != optimum {score}")
+    cells = n * m
+    gcups = cells * args.steps / elapsed / 1e9
+    achieved = fill_cells * BYTES_PER_CELL / (fill_ms * 1e-3) / 1e9 if fill_ms > 0 else None
+    traffic, traffic_src = load_traffic(f"fill_affine_kernel<{kind}> construct {n}x{m}")
+    out = {
+        "metric": "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; % of HBM roofline",
+        "value": round(gcups, 2), "unit": "GCUPS", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int32", "data": data,
+        "config": {"workload": workload, "baseline_config": args.config, "query_len": n, "subject_len": m,
+                   "scoring": "match +2, mismatch -1, gap open -2, extend -1", "parallelism": "single GPU",
+                   "score": int(score), "fill_cells_per_step": fill_cells // max(args.steps, 1),
+                   "fill_launches_per_step": launches // max(args.steps, 1)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": traffic, "kernel_ms": round(fill_ms / max(launches, 1), 4),
+                     "bytes_model": f"{BYTES_PER_CELL} B/cell x cells computed by the fill launches "
+                                    "(Hirschberg halves included) / their summed duration (SURVEY.md 8(d))",
+                     "traffic_source": traffic_src},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_construct(q, s, kind, 16384)
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.config != 1:
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            raise SystemExit("--config 2/3 run on one GPU (the column-block sharded path is config 1 / 4)")
+        return construct_bench(args)
     # the sharded path's fill + transport streams each need a hardware queue of their own
     # (anyseq_shard.cpp check_hw_queues); HIP reads this at its first call
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:

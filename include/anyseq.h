@@ -73,6 +73,13 @@ int anyseq_score_device(int kind, const anyseq_scoring* sc, const uint8_t* d_que
 int anyseq_construct(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject, int lens,
                      char* alQuery, char* alSubject, int64_t* score);
 
+/* anyseq_construct on device-resident sequences (device pointers of the current
+ * device) into device strings d_alQuery/d_alSubject of lenq+lens bytes each; runs
+ * on `stream` (NULL = the engine's own) and returns when the strings are complete. */
+int anyseq_construct_device(int kind, const anyseq_scoring* sc, const uint8_t* d_query, int lenq,
+                            const uint8_t* d_subject, int lens, uint8_t* d_alQuery, uint8_t* d_alSubject, void* stream,
+                            int64_t* score);
+
 /* Device selection (default: $ANYSEQ_DEVICE or 0) and diagnostics. */
 int anyseq_set_device(int device);
 int anyseq_get_device(void);
@@ -93,6 +100,9 @@ int anyseq_set_option(const char* name, int value);
 /* Timing of the most recent fill launch(es) of the calling thread, measured with
  * HIP events on the engine stream: total kernel milliseconds and launch count. */
 void anyseq_last_fill_timing(double* ms, int* launches);
+/* The same, plus the DP cells those launches computed (sum of h*w of their
+ * sub-problems).  Both reset the counters. */
+void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells);
 
 /* ---- column-block sharded score (build-defined) ----
  * Subject columns are split into contiguous blocks, block g = [g*m/N, (g+1)*m/N);
