@@ -20,7 +20,10 @@ $(SRC)/anyseq_engine.o: $(SRC)/anyseq_engine.cpp $(SRC)/anyseq_internal.h $(SRC)
 $(SRC)/anyseq_shard.o: $(SRC)/anyseq_shard.cpp $(SRC)/anyseq_internal.h $(SRC)/anyseq_host.h include/anyseq.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(SRC)/anyseq_kernels.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o
+$(SRC)/anyseq_io.o: $(SRC)/anyseq_io.cpp include/anyseq.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(SRC)/anyseq_kernels.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -L/opt/rocm/lib -lrccl
 
 oracle:

@@ -61,6 +61,10 @@ _lib.anyseq_score_device.argtypes = [_c_int, ctypes.POINTER(Scoring), _vp, _c_in
 _lib.anyseq_construct.restype = _c_int
 _lib.anyseq_construct.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _vp, _vp,
                                   ctypes.POINTER(_c_i64)]
+_lib.anyseq_alignment_dense.restype = _c_i64
+_lib.anyseq_alignment_dense.argtypes = [_c_p, _c_p, _c_i64, _vp, _vp]
+_lib.anyseq_alignment_cigar.restype = _c_i64
+_lib.anyseq_alignment_cigar.argtypes = [_c_p, _c_p, _c_i64, _vp, _c_i64]
 _lib.anyseq_construct_device.restype = _c_int
 _lib.anyseq_construct_device.argtypes = [_c_int, ctypes.POINTER(Scoring), _vp, _c_int, _vp, _c_int, _vp, _vp, _vp,
                                          ctypes.POINTER(_c_i64)]
@@ -251,25 +255,25 @@ def main_random_pair(minlen: int, maxlen: int):
 
 
 def dense(al_q: bytes, al_s: bytes):
-    """Sparse i+j+1 layout -> dense alignment (drop positions blank in both)."""
-    keep = [i for i in range(len(al_q)) if not (al_q[i] == 32 and al_s[i] == 32)]
-    return bytes(al_q[i] for i in keep), bytes(al_s[i] for i in keep)
+    """Sparse i+j+1 layout -> dense alignment (positions blank in both dropped);
+    anyseq_alignment_dense in the library."""
+    al_q, al_s = _b(al_q), _b(al_s)
+    n = min(len(al_q), len(al_s))
+    oq, os_ = ctypes.create_string_buffer(max(n, 1)), ctypes.create_string_buffer(max(n, 1))
+    k = _lib.anyseq_alignment_dense(al_q, al_s, n, oq, os_)
+    if k < 0:
+        raise AnySeqError("anyseq_alignment_dense failed")
+    return oq.raw[:k], os_.raw[:k]
 
 
 def cigar(al_q: bytes, al_s: bytes) -> str:
-    """Extended CIGAR (=, X, I, D) of a dense alignment; '_' is the gap symbol."""
-    ops = []
-    for a, b in zip(al_q, al_s):
-        if a == 95:
-            op = "D"       # gap in query: subject base consumed
-        elif b == 95:
-            op = "I"
-        elif a == b:
-            op = "="
-        else:
-            op = "X"
-        if ops and ops[-1][0] == op:
-            ops[-1][1] += 1
-        else:
-            ops.append([op, 1])
-    return "".join(f"{n}{o}" for o, n in ops)
+    """Extended CIGAR (=, X, I, D) of an alignment (sparse or dense; '_' is the gap
+    symbol); anyseq_alignment_cigar in the library."""
+    al_q, al_s = _b(al_q), _b(al_s)
+    n = min(len(al_q), len(al_s))
+    need = _lib.anyseq_alignment_cigar(al_q, al_s, n, None, 0)
+    if need < 0:
+        raise AnySeqError("anyseq_alignment_cigar failed")
+    out = ctypes.create_string_buffer(need + 1)
+    _lib.anyseq_alignment_cigar(al_q, al_s, n, out, need + 1)
+    return out.value.decode()

@@ -124,6 +124,18 @@ int anyseq_shard_finalize(void);
 int anyseq_shard_score_local(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
                              int lens, int nshards, int64_t* score);
 
+/* ---- alignment-output adapters (host only) ----
+ * The sparse i+j+1 layout of construct_* / anyseq_construct (len = lenq+lens):
+ * anyseq_alignment_dense drops the positions blank in both strings and writes the
+ * dense pair (either output may be NULL); returns its length.
+ * anyseq_alignment_cigar writes the extended CIGAR (=, X, I, D; '_' in alQuery ->
+ * D, '_' in alSubject -> I) NUL-terminated into out (at most cap bytes, truncated
+ * like snprintf) and returns its full length; out may be NULL to size it.
+ * Both return -1 on invalid arguments. */
+int64_t anyseq_alignment_dense(const char* alQuery, const char* alSubject, int64_t len, char* outQuery,
+                               char* outSubject);
+int64_t anyseq_alignment_cigar(const char* alQuery, const char* alSubject, int64_t len, char* out, int64_t cap);
+
 /* main.cpp's random input generator (main.cpp:90-120, 200-210): mt19937_64 with the
  * default seed, lengths uniform in [minlen, maxlen], bases uniform over ACGT.
  * query/subject must hold maxlen bytes; lengths are returned. */
