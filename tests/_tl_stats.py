@@ -24,3 +24,15 @@ for path in sys.argv[1:]:
               f"glob {np.median(d[glob]) if glob.any() else 0:.2f} | st->pub {np.median(pub[ok]-st[ok]):.2f} | "
               f"pub->next lds {np.median(pd[ok2 & ~glob]) if (ok2 & ~glob).any() else 0:.2f} "
               f"glob {np.median(pd[ok2 & glob]) if (ok2 & glob).any() else 0:.2f}")
+
+# band duration by wave slot in its workgroup (which SIMD neighbours the I/O wave)
+for path in sys.argv[1:]:
+    rows = [l.split() for l in open(path) if not l.startswith("#")]
+    a = np.array([[float(x) for x in r] for r in rows])
+    band = (a[:, 0] % 2048).astype(int)
+    dur = a[:, 3] - a[:, 1]
+    ok = a[:, 3] > 0
+    print(" duration by wave slot:", " ".join(f"w{k}={np.median(dur[ok & (band % NW == k)]):.1f}" for k in range(NW)))
+    mid = ok & (band > 64) & (band < 448)
+    print(" mid-chain bands, start-to-start lag by slot:",
+          " ".join(f"w{k}={np.median(np.diff(np.sort(a[mid & (band % NW == k), 1]))):.2f}" for k in range(NW)))
