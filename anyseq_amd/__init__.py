@@ -49,7 +49,9 @@ _c_i64, _c_int, _c_p, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_char_p, ctype
 for _n in ("global_alignment_score", "semiglobal_alignment_score", "local_alignment_score"):
     getattr(_lib, _n).restype = _c_i64
     getattr(_lib, _n).argtypes = [_c_p, _c_int, _c_p, _c_int]
-for _n in ("construct_global_alignment", "construct_semiglobal_alignment", "construct_local_alignment"):
+for _n in ("construct_global_alignment", "construct_semiglobal_alignment", "construct_local_alignment",
+           "construct_global_alignment_fulltb", "construct_semiglobal_alignment_fulltb",
+           "construct_local_alignment_fulltb"):
     getattr(_lib, _n).restype = _c_i64
     getattr(_lib, _n).argtypes = [_c_p, _c_int, _c_p, _c_int, _vp, _vp]
 _lib.anyseq_score.restype = _c_int
@@ -149,6 +151,21 @@ def construct_semiglobal_alignment(query, subject):
 
 def construct_local_alignment(query, subject):
     return _construct_abi(_lib.construct_local_alignment, query, subject)
+
+
+def construct_global_alignment_fulltb(query, subject):
+    """Undeclared reference export (export.impala:37-53): full-matrix traceback."""
+    return _construct_abi(_lib.construct_global_alignment_fulltb, query, subject)
+
+
+def construct_semiglobal_alignment_fulltb(query, subject):
+    """export.impala:93-109 -- runs the GLOBAL scheme, as the reference does."""
+    return _construct_abi(_lib.construct_semiglobal_alignment_fulltb, query, subject)
+
+
+def construct_local_alignment_fulltb(query, subject):
+    """export.impala:150-166 -- runs the GLOBAL scheme, as the reference does."""
+    return _construct_abi(_lib.construct_local_alignment_fulltb, query, subject)
 
 
 # ---- extended API ---------------------------------------------------------

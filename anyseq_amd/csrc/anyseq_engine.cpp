@@ -40,6 +40,9 @@ hipError_t anyseq_launch_pred(const void* blocks, int nblocks, const uint8_t* Q,
                               const FillParams* fp, hipStream_t st);
 hipError_t anyseq_launch_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
                               const uint8_t* pred, int kind, uint8_t* alq, uint8_t* als, hipStream_t st);
+hipError_t anyseq_launch_fulltb(const uint8_t* Q, int n, const uint8_t* S, int m, uint8_t* pred, int32_t* cols,
+                                uint32_t* ticket, uint32_t* err, int match, int mismatch, int gap, uint8_t* alq,
+                                uint8_t* als, hipStream_t st);
 hipError_t anyseq_launch_aff_rowbest(const void* rowbest, int h, int32_t* out, hipStream_t st);
 hipError_t anyseq_launch_aff_edge_scan(const void* row, int w, const int32_t* col, int h, int nge, int rborder,
                                        int cborder, int32_t* out, hipStream_t st);
@@ -807,6 +810,47 @@ int64_t construct_affine_host(int kind, const anyseq_scoring& sc, const char* q,
     return score;
 }
 
+// construct_*_alignment_fulltb: full-matrix predecessors + one walk (align.impala:190-216),
+// global scheme for all three exports (export.impala:52,108,165).  Returns H[n-1][m-1].
+int64_t construct_fulltb_host(const anyseq_scoring& sc, const char* q, int n, const char* s, int m, char* alq,
+                              char* als) {
+    if (sc.gap_open != 0) fail("fulltb: linear gaps only (the reference's traceback_full)");
+    Engine& E = engine();
+    std::lock_guard<std::mutex> lk(E.mu);
+    hipStream_t st = E.stream;
+    const size_t L = (size_t)n + (size_t)m;
+    if (L == 0) return 0;
+    const int nstrips = (m + 127) / 128;
+    const size_t pred_bytes = (size_t)nstrips * (size_t)(n + 127) * 128;
+    if (pred_bytes > ((size_t)16 << 30))
+        fail("fulltb: %d x %d needs %.1f GB of predecessors (limit 16 GB; the reference's own limit is "
+             "n*m < 2^31, use construct_* for long sequences)", n, m, pred_bytes / 1e9);
+    uint8_t* dq = (uint8_t*)E.q.get((size_t)std::max(n, 1));
+    uint8_t* ds = (uint8_t*)E.s.get((size_t)std::max(m, 1));
+    if (n > 0) HIPCHECK(hipMemcpyAsync(dq, q, (size_t)n, hipMemcpyHostToDevice, st));
+    if (m > 0) HIPCHECK(hipMemcpyAsync(ds, s, (size_t)m, hipMemcpyHostToDevice, st));
+    uint8_t* d_pred = (uint8_t*)E.pred.get(std::max<size_t>(pred_bytes, 16));
+    const size_t col_ints = (size_t)std::max(nstrips - 1, 1) * (size_t)std::max(n, 1);
+    int32_t* cols = (int32_t*)E.outcol.get(col_ints * 4);
+    HIPCHECK(hipMemsetAsync(cols, 0x80, col_ints * 4, st));
+    uint32_t* ctr = (uint32_t*)E.fc.ctr.get(128) + 8;   // [0] ticket, [1] error word
+    HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));
+    uint8_t* d_alq = (uint8_t*)E.alq.get(L);
+    uint8_t* d_als = (uint8_t*)E.als.get(L);
+    HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
+    HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
+    HIPCHECK(anyseq_launch_fulltb(dq, n, ds, m, d_pred, cols, ctr, ctr + 1, sc.match, sc.mismatch, sc.gap_extend,
+                                  d_alq, d_als, st));
+    HIPCHECK(hipMemcpyAsync(alq, d_alq, L, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(als, d_als, L, hipMemcpyDeviceToHost, st));
+    uint32_t err = 0;
+    HIPCHECK(hipMemcpyAsync(&err, ctr + 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (err) fail("fulltb kernel reported error %u (spin timeout)", err);
+    if (n <= 0 || m <= 0) return empty_score(KIND_GLOBAL, n, m, sc);
+    return score_dev(E, KIND_GLOBAL, sc, dq, n, ds, m, st);
+}
+
 const anyseq_scoring kAbiScoring = {2, -1, 0, -1};  // linear_scoring_scheme(2,-1,-1)
 
 int64_t abi_score(int kind, const char* q, int n, const char* s, int m) {
@@ -863,6 +907,30 @@ int64_t construct_semiglobal_alignment(const char* query, int lenq, const char* 
 int64_t construct_local_alignment(const char* query, int lenq, const char* subject, int lens, char* alQuery,
                                   char* alSubject) {
     return abi_construct(KIND_LOCAL, query, lenq, subject, lens, alQuery, alSubject);
+}
+
+// The reference's undeclared *_fulltb exports (export.impala:37-53,93-109,150-166):
+// all three run the GLOBAL scheme (export.impala:52,108,165) -- reproduced as is.
+static int64_t abi_fulltb(const char* q, int n, const char* s, int m, char* alq, char* als) {
+    try {
+        return construct_fulltb_host(kAbiScoring, q, n, s, m, alq, als);
+    } catch (const Failure& f) {
+        g_last_error = f.msg;
+        fprintf(stderr, "anyseq: %s\n", f.msg.c_str());
+        return INT64_MIN;
+    }
+}
+int64_t construct_global_alignment_fulltb(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                          char* alSubject) {
+    return abi_fulltb(query, lenq, subject, lens, alQuery, alSubject);
+}
+int64_t construct_semiglobal_alignment_fulltb(const char* query, int lenq, const char* subject, int lens,
+                                              char* alQuery, char* alSubject) {
+    return abi_fulltb(query, lenq, subject, lens, alQuery, alSubject);
+}
+int64_t construct_local_alignment_fulltb(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                         char* alSubject) {
+    return abi_fulltb(query, lenq, subject, lens, alQuery, alSubject);
 }
 
 int anyseq_score(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject, int lens,

@@ -1669,6 +1669,102 @@ __global__ void walk_kernel(const BlockInfo* __restrict__ blocks, int nblocks, c
     }
 }
 
+// ----------------------------------------------------------------- fulltb --
+// construct_*_alignment_fulltb (export.impala:37-53,93-109,150-166; all three use
+// global_scheme, export.impala:52,108,165): traceback_full (align.impala:190-216)
+// = one fill of the whole matrix writing every predecessor, then traceback_offset
+// from (n-1, m-1).  The matrix is cut into 128-column strips; one wave per strip,
+// lane l owns strip columns 2l and 2l+1 and sweeps anti-diagonals exactly like
+// pred_kernel, with the GLOBAL top border and the left column H[r][oj-1] polled
+// from the strip on the left (which stores its last column as it goes, sentinel
+// 0x80808080, 64 rows per poll).  Strips are taken by ticket, so a strip only
+// waits on a strip that is already running.  Predecessors are anti-diagonal-major
+// per strip: pred[k*(n+127)*128 + (i+jl)*128 + jl].
+__global__ __launch_bounds__(64) void fulltb_strip_kernel(const uint8_t* __restrict__ Q, int n,
+                                                          const uint8_t* __restrict__ S, int m, uint8_t* pred,
+                                                          int32_t* cols, uint32_t* ticket, uint32_t* err, int match,
+                                                          int mismatch, int gap) {
+    const int lane = threadIdx.x;
+    int k = 0;
+    if (lane == 0) k = (int)atomicAdd(ticket, 1u);
+    k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
+    const int nstrips = (m + 127) / 128;
+    if (k >= nstrips) return;
+    const int oj = k * 128, w = min(128, m - oj);
+    const int32_t* left_in = k > 0 ? cols + (size_t)(k - 1) * n : nullptr;
+    int32_t* right_out = (k < nstrips - 1) ? cols + (size_t)k * n : nullptr;
+    auto init = [&](int i) { return (i + 1) * gap; };   // init_scores_global, align.impala:85
+    const int jA = 2 * lane, jB = 2 * lane + 1;
+    const int sA = jA < w ? (int)S[oj + jA] : 0x100;
+    const int sB = jB < w ? (int)S[oj + jB] : 0x100;
+    int A = init(oj + jA), Bv = init(oj + jB), A_old = A;
+    int leftA_prev = init(oj - 1);   // H[-1][oj-1]: the corner of this strip
+    uint16_t* out16 = reinterpret_cast<uint16_t*>(pred + (size_t)k * (size_t)(n + 127) * 128);
+    int lchunk = 0;                  // left-column values of rows d & ~63 .. +63 (lane r holds row base + r)
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const int nsteps = n + 127;
+    for (int d = 0; d < nsteps; ++d) {
+        if (left_in && (d & 63) == 0 && d < n) {
+            const int r = d + lane;
+            uint32_t it = 0;
+            for (;;) {
+                lchunk = r < n ? __hip_atomic_load(gmem(left_in) + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0;
+                if (__ballot(r < n && lchunk == kShardSentinel) == 0) break;
+                __builtin_amdgcn_s_sleep(2);
+                if ((++it & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
+                    atomicOr(err, ERR_SPIN_TIMEOUT | 16u);
+                    return;
+                }
+            }
+        }
+        const int lv = left_in ? __shfl(lchunk, d & 63) : init(d);   // H[d][oj-1] for lane 0 (row iA = d)
+        const int iA = d - jA, iB = d - jB;
+        const int leftA = wave_shr1(lv, Bv);
+        const int diagA = leftA_prev;
+        leftA_prev = leftA;
+        const bool actA = (iA >= 0) && (iA < n) && (jA < w);
+        const bool actB = (iB >= 0) && (iB < n) && (jB < w);
+        const int qA = (iA >= 0 && iA < n) ? (int)Q[iA] : 0x200;
+        const int qB = (iB >= 0 && iB < n) ? (int)Q[iB] : 0x200;
+        int pA = 0, pB = 0;
+        const int nB = relax_pred(KIND_GLOBAL, A_old, A, Bv, qB == sB ? match : mismatch, gap, pB);
+        const int nA = relax_pred(KIND_GLOBAL, diagA, leftA, A, qA == sA ? match : mismatch, gap, pA);
+        if (actB) Bv = nB;
+        A_old = A;
+        if (actA) A = nA;
+        if (right_out && actB && jB == 127)
+            __hip_atomic_store(gmem(right_out) + iB, nB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        out16[(size_t)d * 64 + lane] = (uint16_t)((actA ? pA : 0) | ((actB ? pB : 0) << 8));
+    }
+}
+
+// One thread: traceback_offset (traceback.impala:47-80) from (n-1, m-1) over the
+// strips, global border predecessors (predecessors.impala:17-18, align.impala:88-90).
+__global__ void fulltb_walk_kernel(const uint8_t* __restrict__ Q, int n, const uint8_t* __restrict__ S, int m,
+                                   const uint8_t* __restrict__ pred, uint8_t* alq, uint8_t* als) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const size_t strip = (size_t)(n + 127) * 128;
+    auto P = [&](int i, int j) -> int {
+        if (i < 0 && j < 0) return 0;
+        if (i < 0) return 1;   // row -1: GAP_Q
+        if (j < 0) return 2;   // column -1: GAP_S
+        const int jl = j & 127;
+        return pred[(size_t)(j >> 7) * strip + (size_t)(i + jl) * 128 + jl];
+    };
+    int i = n - 1, j = m - 1;
+    int p = P(i, j);
+    while (p != 0) {
+        uint8_t sq = '_', ss = '_';
+        const int pos = i + j + 1;
+        if (p == 3 || p == 2) sq = Q[i--];
+        if (p == 3 || p == 1) ss = S[j--];
+        alq[pos] = sq;
+        als[pos] = ss;
+        p = P(i, j);
+    }
+}
+
 // ======================================================= affine construct --
 // Build-defined linear-space affine alignment (semantics =
 // oracle_affine_construct in oracle/anyseq_oracle.c).
@@ -2123,6 +2219,17 @@ hipError_t anyseq_launch_walk(const void* blocks, int nblocks, const uint8_t* Q,
     if (nblocks > 0)
         hipLaunchKernelGGL(anyseq::walk_kernel, dim3((nblocks + 63) / 64), dim3(64), 0, st,
                            (const anyseq::BlockInfo*)blocks, nblocks, Q, S, pred, kind, alq, als);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_fulltb(const uint8_t* Q, int n, const uint8_t* S, int m, uint8_t* pred, int32_t* cols,
+                                uint32_t* ticket, uint32_t* err, int match, int mismatch, int gap, uint8_t* alq,
+                                uint8_t* als, hipStream_t st) {
+    const int nstrips = (m + 127) / 128;
+    if (n > 0 && m > 0)
+        hipLaunchKernelGGL(anyseq::fulltb_strip_kernel, dim3(nstrips), dim3(64), 0, st, Q, n, S, m, pred, cols,
+                           ticket, err, match, mismatch, gap);
+    hipLaunchKernelGGL(anyseq::fulltb_walk_kernel, dim3(1), dim3(64), 0, st, Q, n, S, m, pred, alq, als);
     return hipGetLastError();
 }
 

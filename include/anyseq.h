@@ -48,6 +48,18 @@ int64_t global_alignment_score(const char* query, int lenq, const char* subject,
 int64_t semiglobal_alignment_score(const char* query, int lenq, const char* subject, int lens);
 int64_t local_alignment_score(const char* query, int lenq, const char* subject, int lens);
 
+/* ---- reference exports not declared in import.h: export.impala:37-53, 93-109,
+ * 150-166.  Full-matrix traceback (traceback_full, align.impala:190-216): every
+ * predecessor of the n x m matrix, walked from (n-1, m-1).  As in the reference,
+ * ALL THREE use the global scheme (export.impala:52,108,165).  Same sparse output
+ * layout as construct_*; returns H[n-1][m-1].  Memory O(n*m) (limit 16 GB). ---- */
+int64_t construct_global_alignment_fulltb(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                          char* alSubject);
+int64_t construct_semiglobal_alignment_fulltb(const char* query, int lenq, const char* subject, int lens,
+                                              char* alQuery, char* alSubject);
+int64_t construct_local_alignment_fulltb(const char* query, int lenq, const char* subject, int lens, char* alQuery,
+                                         char* alSubject);
+
 /* ---- extended API (build-defined; not part of the reference) ---- */
 enum { ANYSEQ_GLOBAL = 0, ANYSEQ_SEMIGLOBAL = 1, ANYSEQ_LOCAL = 2 };
 

@@ -602,6 +602,60 @@ int64_t oracle_construct_local_alignment(const char* q, int n, const char* s, in
     return oracle_construct(SCHEME_LOCAL, q, n, s, m, 2, -1, -1, aq, as_, NULL, 0);
 }
 
+/* construct_*_alignment_fulltb (export.impala:37-53, 93-109, 150-166): all three
+ * pass global_scheme(linear_scoring_scheme(2,-1,-1)) (export.impala:52,108,165),
+ * so each is traceback_full (align.impala:190-216) of the GLOBAL scheme: one fill of
+ * the whole matrix writing every predecessor into a full (n+1) x (m+1) matrix with
+ * the scheme's border predecessors (full_predecessors, predecessors.impala:11-34),
+ * then traceback_offset (traceback.impala:47-80) from get_score_pos() = (n-1, m-1)
+ * (scoring.impala:34) over blank-filled outputs (traceback.impala:14-44).  Returns
+ * get_score() = H[n-1][m-1] (the scoring object IS relaxed here, unlike
+ * traceback_lintime's).  Memory O(n*m): test sizes only. */
+int64_t oracle_construct_fulltb(const char* qc, int n, const char* sc_, int m, int match, int mismatch, int gap,
+                                char* alq, char* als) {
+    const uint8_t* Q = (const uint8_t*)qc;
+    const uint8_t* S = (const uint8_t*)sc_;
+    Scheme sc = make_scheme(SCHEME_GLOBAL, match, mismatch, gap);
+    g_error = 0;
+    const size_t W = (size_t)m + 1;
+    uint8_t* P = (uint8_t*)malloc(((size_t)n + 1) * W);
+    Score* row = (Score*)malloc(W * sizeof(Score));
+    if (!P || !row) { free(P); free(row); g_error = 1; return 0; }
+#define PF(i, j) P[((size_t)(i) + 1) * W + (size_t)(j) + 1]
+    for (Index j = -1; j < m; ++j) { PF(-1, j) = init_predc_cols(&sc, j); row[j + 1] = init_scores(&sc, j); }
+    for (Index i = 0; i < n; ++i) {
+        PF(i, -1) = init_predc_rows(&sc, i);
+        Score diag = row[0];                 /* H[i-1][-1] */
+        row[0] = init_scores(&sc, i);        /* H[i][-1] */
+        for (Index j = 0; j < m; ++j) {
+            Pred pr;
+            const Score v = relax(&sc, Q[i], S[j], diag, row[j], row[j + 1], &pr);
+            diag = row[j + 1];
+            row[j + 1] = v;
+            PF(i, j) = pr;
+        }
+    }
+    const int64_t score = (n > 0 && m > 0) ? row[m] : (n > 0 ? init_scores(&sc, n - 1) : init_scores(&sc, m - 1));
+    const size_t L = (size_t)n + (size_t)m;
+    memset(alq, ' ', L);
+    memset(als, ' ', L);
+    Index i = n - 1, j = m - 1;
+    Pred pr = PF(i, j);
+    while (pr != PRED_NONE) {
+        char sq = '_', ss = '_';
+        const Index pos = i + j + 1;
+        if (pr == PRED_NO_GAP || pr == PRED_GAP_S) { sq = (char)Q[i]; --i; }
+        if (pr == PRED_NO_GAP || pr == PRED_GAP_Q) { ss = (char)S[j]; --j; }
+        alq[pos] = sq;
+        als[pos] = ss;
+        pr = PF(i, j);
+    }
+#undef PF
+    free(P);
+    free(row);
+    return (n == 0 && m == 0) ? 0 : score;
+}
+
 /* ===================================================================== */
 /* Build-defined affine gap (Gotoh).  NO reference semantics exist        */
 /* (affine_scoring_scheme, align.impala:153-166, is dead and broken):     */

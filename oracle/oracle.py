@@ -48,6 +48,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_affine_construct.restype = c_i64
         L.oracle_affine_construct.argtypes = [c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_int,
                                               c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_construct_fulltb.restype = c_i64
+        L.oracle_construct_fulltb.argtypes = [c_p, c_int, c_p, c_int, c_int, c_int, c_int,
+                                              ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_affine_rect.restype = c_int
         L.oracle_affine_rect.argtypes = [c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_int, c_int,
                                          i32p, ctypes.POINTER(c_i64)]
@@ -90,6 +93,17 @@ def construct(kind, q, s, match=2, mismatch=-1, gap=-1, with_splits=False):
     if with_splits:
         out = out + (list(spl)[:nb],)
     return out
+
+
+def construct_fulltb(q, s, match=2, mismatch=-1, gap=-1):
+    """construct_*_alignment_fulltb (all three: global scheme, full-matrix traceback,
+    export.impala:37-53,93-109,150-166): (H[n-1][m-1], alQuery, alSubject)."""
+    q, s = _b(q), _b(s)
+    n, m = len(q), len(s)
+    aq = ctypes.create_string_buffer(max(n + m, 1))
+    as_ = ctypes.create_string_buffer(max(n + m, 1))
+    r = lib().oracle_construct_fulltb(q, n, s, m, match, mismatch, gap, aq, as_)
+    return r, aq.raw[: n + m], as_.raw[: n + m]
 
 
 def affine_score(kind, q, s, match=2, mismatch=-1, gap_open=-2, gap_extend=-1, with_pos=False):
