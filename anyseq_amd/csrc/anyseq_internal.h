@@ -42,6 +42,8 @@ struct DPProblem {
     // + left_shift.  progress: bands whose out_col rows are complete, bumped in
     // band order with a system-scope release (the transport stream waits on it).
     const int32_t* left_in;
+    const int32_t* left_in_e;   // affine: E[r][-1] (H space), polled like left_in
+    int32_t* out_f_last;        // affine shard: F of the last row at the last column (H space)
     int32_t left_shift;
     // Affine global sub-problems of the affine construct: border
     // mode of the top-left corner.  0: the scheme's borders; 1 (E_FREE): the path

@@ -408,6 +408,24 @@ __device__ __forceinline__ bool poll_left(const DPProblem& P, int row, int32_t& 
     return true;
 }
 
+// Affine shard: this lane's E[row][-1] from left_in_e (sentinel-polled like poll_left).
+__device__ __forceinline__ bool poll_left_e(const DPProblem& P, int row, int32_t& e1, uint32_t* err) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t it = 0;
+    for (;;) {
+        const bool has1 = row < P.h;
+        e1 = has1 ? __hip_atomic_load(gmem(P.left_in_e) + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        if (__ballot(has1 && e1 == kShardSentinel) == 0) break;
+        __builtin_amdgcn_s_sleep(4);
+        if ((++it & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
+            atomicOr(err, ERR_SPIN_TIMEOUT | 2u);
+            return false;
+        }
+    }
+    e1 += P.left_shift;
+    return true;
+}
+
 // After a band has stored its out_col rows: publish "band + 1 bands complete" in
 // band order (waits for the band above to publish first), system scope, so the
 // transport stream's hipStreamWaitValue32 and the kernel that sends the rows see
@@ -1142,6 +1160,11 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     constexpr bool VIRT = KIND == KIND_GLOBAL && !PARTIAL && !FINOUT;
     constexpr bool ASM = !PARTIAL && !FINOUT && !TRACK;
     const int h = P.h, w = P.w, go = k.go, nge = k.nge;
+    // column-block shard: the left border column (H and E of column
+    // -1, H space, sender's frame + left_shift) arrives from the neighbour shard;
+    // such a band runs the masked prologue on the received values
+    const bool shard_left = P.left_in != nullptr;
+    const bool virt = VIRT && !shard_left;
     // border values (G space): corner, top row (c >= 0), left column (r >= 0); the
     // affine construct's global sub-problems change them by border mode (bmode)
     const int bm = KIND == KIND_GLOBAL ? P.bmode : BM_NORMAL;
@@ -1160,7 +1183,18 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(q)::"memory");
     int g, e = kAffNeg, hg, fdn = kAffNeg, dg;
     int2 tf;
-    if (VIRT) {
+    if (shard_left) {
+        int32_t lh1 = 0, lh0 = 0, le1 = 0;
+        if (!poll_left(P, row, lh1, lh0, err)) return;
+        if (!poll_left_e(P, row, le1, err)) return;
+        // H space -> G space at column -1: G = H + (r + 1) (-ge); row -1 is the corner,
+        // the scheme's border in every shard frame (global: go, else 0)
+        g = lh1 + (row + 1) * nge;
+        e = le1 + (row + 1) * nge;
+        hg = g + go;
+        dg = row == 0 ? (KIND == KIND_GLOBAL ? go : 0) : lh0 + row * nge;
+        tf = make_int2(__shfl(dg, 0), kAffNeg);
+    } else if (virt) {
         g = kAffNeg;
         hg = kAffNeg;
         dg = kAffNeg;
@@ -1197,7 +1231,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
         if constexpr (ASM) {
-            if ((VIRT || t0 >= 64) && b < fe && !(k.flags & 1)) {
+            if ((virt || t0 >= 64) && b < fe && !(k.flags & 1)) {
                 uint32_t bb = (uint32_t)b;
                 uint32_t z = (uint32_t)((rb + t0 + 1) * nge);
                 const int role = (io.in_border ? 3 : 0) + (io.out_lds ? 1 : (io.gout ? 2 : 0));
@@ -1257,13 +1291,16 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         int og[CH], of[CH];
         const int c0 = t0 - 1 - lane;
         const int z = (rb + t0 + 1) * nge;
-        const bool full = (VIRT || t0 >= 64) && b < fe;
+        const bool full = (virt || t0 >= 64) && b < fe;
         if (TRACK)
             aff_block<KIND, true, PARTIAL, FINOUT, VIRT, true>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg,
                                                                best, og, of, k, &bcol);
         else if (full)
             aff_block<KIND, false, PARTIAL, FINOUT, VIRT>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg, best,
                                                     og, of, k);
+        else if (VIRT && shard_left)   // a shard's prologue: real border column, no virtual lanes
+            aff_block<KIND, true, PARTIAL, FINOUT, false>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg,
+                                                    best, og, of, k);
         else
             aff_block<KIND, true, PARTIAL, FINOUT, VIRT>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg, best,
                                                    og, of, k);
@@ -1302,8 +1339,11 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     if (!dead) {
         if (P.out_col) gmem(P.out_col)[row] = aff_to_h(g, row, w - 1, nge);
         if (P.out_col_e) gmem(P.out_col_e)[row] = aff_to_h(e, row, w - 1, nge);
+        // shard: F of the last row at the last column (the combine pairs it across shards)
+        if (lastrow && P.out_f_last) *gmem(P.out_f_last) = aff_to_h(fdn, row, w - 1, nge);
         if (TRACK) P.rowbest[row] = make_int2(best, bcol);
     }
+    if (P.progress && !publish_progress(P, band, lane, err)) return;
     if (KIND == KIND_LOCAL && P.best && !TRACK) {
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
@@ -1510,6 +1550,60 @@ __global__ void shard_combine_kernel(int kind, const int32_t* __restrict__ rowT,
         if (colB)
             for (int i = threadIdx.x + blockIdx.x * blockDim.x; i < h2; i += blockDim.x * gridDim.x)
                 best = max(best, colB[i]);
+    }
+    for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, best);
+}
+
+// Affine shard combine: aff_reduce_kernel's two-front split-row join over this
+// shard's columns (true-score units via adj), with the split column left of the
+// block paired through the received left column (H[h1-1], F of the last row at
+// lTf) and the one right of it through the bottom front's received column.
+__global__ void shard_aff_combine_kernel(int kind, const int2* __restrict__ rowT, int h1, const int2* __restrict__ rowB,
+                                         int h2, int w, int go, int ge, const int32_t* __restrict__ lT,
+                                         const int32_t* __restrict__ lTf, int sT, const int32_t* __restrict__ lB,
+                                         const int32_t* __restrict__ lBf, int sB, int last,
+                                         const int32_t* __restrict__ colT, const int32_t* __restrict__ colB, int adj,
+                                         int32_t* out) {
+    auto toh = [&](int v, int r, int c) { return v + (r + c + 2) * ge; };
+    const int NEG2 = 2 * kAffNeg;
+    int best = kind == KIND_SEMIGLOBAL ? 0 : -2147483647;
+    const int bt = kind == KIND_GLOBAL ? go + h1 * ge : 0;   // H[h1-1][-1] of the whole matrix
+    const int bb = kind == KIND_GLOBAL ? go + h2 * ge : 0;
+    const int jend = last ? w : w - 1;
+    const int tid = threadIdx.x + blockIdx.x * blockDim.x, nth = blockDim.x * gridDim.x;
+    for (int j = tid - 1; j < jend; j += nth) {
+        int Ht, Ft, Hb, Fb;
+        if (j >= 0) {
+            const int2 t = rowT[j];
+            Ht = toh(t.x, h1 - 1, j);
+            Ft = toh(t.y, h1 - 1, j);
+        } else if (lT) {
+            Ht = lT[h1 - 1] + sT;
+            Ft = *lTf + sT;
+        } else {
+            Ht = bt;
+            Ft = kind == KIND_GLOBAL ? bt : kAffNeg;
+        }
+        const int jb = w - 2 - j;
+        if (jb >= 0) {
+            const int2 t = rowB[jb];
+            Hb = toh(t.x, h2 - 1, jb);
+            Fb = toh(t.y, h2 - 1, jb);
+        } else if (lB) {
+            Hb = lB[h2 - 1] + sB;
+            Fb = *lBf + sB;
+        } else {
+            Hb = bb;
+            Fb = kind == KIND_GLOBAL ? bb : kAffNeg;
+        }
+        best = max(best, max(Ht + Hb, max(Ft + Fb - go, NEG2)) + adj);
+    }
+    if (kind == KIND_SEMIGLOBAL) {
+        if (colT)
+            for (int i = tid; i < h1; i += nth) best = max(best, colT[i]);
+        if (colB)
+            for (int i = tid; i < h2; i += nth) best = max(best, colB[i]);
     }
     for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
     if ((threadIdx.x & 63) == 0) atomicMax(out, best);
@@ -2219,6 +2313,15 @@ hipError_t anyseq_launch_walk(const void* blocks, int nblocks, const uint8_t* Q,
     if (nblocks > 0)
         hipLaunchKernelGGL(anyseq::walk_kernel, dim3((nblocks + 63) / 64), dim3(64), 0, st,
                            (const anyseq::BlockInfo*)blocks, nblocks, Q, S, pred, kind, alq, als);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_shard_aff_combine(int kind, const void* rowT, int h1, const void* rowB, int h2, int w, int go,
+                                           int ge, const int32_t* lT, const int32_t* lTf, int sT, const int32_t* lB,
+                                           const int32_t* lBf, int sB, int last, const int32_t* colT,
+                                           const int32_t* colB, int adj, int32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(anyseq::shard_aff_combine_kernel, dim3(64), dim3(256), 0, st, kind, (const int2*)rowT, h1,
+                       (const int2*)rowB, h2, w, go, ge, lT, lTf, sT, lB, lBf, sB, last, colT, colB, adj, out);
     return hipGetLastError();
 }
 

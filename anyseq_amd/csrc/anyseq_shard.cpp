@@ -37,6 +37,11 @@
 
 #include "anyseq_host.h"
 
+extern "C" hipError_t anyseq_launch_shard_aff_combine(int kind, const void* rowT, int h1, const void* rowB, int h2,
+                                                      int w, int go, int ge, const int32_t* lT, const int32_t* lTf,
+                                                      int sT, const int32_t* lB, const int32_t* lBf, int sB, int last,
+                                                      const int32_t* colT, const int32_t* colB, int adj, int32_t* out,
+                                                      hipStream_t st);
 extern "C" hipError_t anyseq_launch_shard_combine(int kind, const int32_t* rowT, int h1, const int32_t* rowB, int h2,
                                                   int w, int gap, const int32_t* lT, int sT, const int32_t* lB,
                                                   int sB, int last, const int32_t* colT, const int32_t* colB, int adj,
@@ -64,7 +69,10 @@ bool use_direct() { return env_int("ANYSEQ_SHARD_DIRECT", 0) != 0; }
 
 
 struct Front {
-    DevBuf out_col, left_in, out_row;
+    // affine: out_col_e / left_in_e hold E of the last column, h rows, plus [h] = F of
+    // the last row at the last column (the combine's vertical-gap join)
+    DevBuf out_col, left_in, out_row, out_col_e, left_in_e;
+    bool aff = false;
     uint32_t* progress = nullptr;     // device view of the counter (what the kernel bumps)
     uint32_t* progress_h = nullptr;   // host view (pinned, coherent) -- host-poll transport
     uint32_t* progress_sig = nullptr; // signal memory -- hipStreamWaitValue32 transport
@@ -81,10 +89,13 @@ struct Shard {
     DevBuf res;
     const int32_t* lT = nullptr;   // where the fronts read their received columns (combine reads them too)
     const int32_t* lB = nullptr;
+    const int32_t* lTe = nullptr;  // affine: received E columns (+ [h] = F of the last row)
+    const int32_t* lBe = nullptr;
     void init() {
         if (st) return;
         // polled across kernels / XCDs: never L2-cached (see DevBuf::uncached)
-        for (Front* f : {&top, &bot}) f->out_col.uncached = f->left_in.uncached = true;
+        for (Front* f : {&top, &bot})
+            f->out_col.uncached = f->left_in.uncached = f->out_col_e.uncached = f->left_in_e.uncached = true;
         HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
         HIPCHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
         for (Front* f : {&top, &bot}) {
@@ -161,10 +172,25 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     const int wpad = (w + 63) & ~63;
     const bool has_left = g > 0, has_right = g < N - 1;
     const int ng = -sc.gap_extend;
+    const bool aff = sc.gap_open != 0;
     S.top.h = h1;
     S.bot.h = h2;
-    int32_t* rowT = (int32_t*)S.top.out_row.get((size_t)wpad * 4);
-    int32_t* rowB = (int32_t*)S.bot.out_row.get((size_t)wpad * 4);
+    S.top.aff = S.bot.aff = aff;
+    // rows: (G, F) pairs for affine
+    int32_t* rowT = (int32_t*)S.top.out_row.get((size_t)wpad * (aff ? 8 : 4));
+    int32_t* rowB = (int32_t*)S.bot.out_row.get((size_t)wpad * (aff ? 8 : 4));
+    int32_t* colTe = aff ? (int32_t*)S.top.out_col_e.get((size_t)(h1 + 1) * 4) : nullptr;
+    int32_t* colBe = aff ? (int32_t*)S.bot.out_col_e.get((size_t)(h2 + 1) * 4) : nullptr;
+    int32_t* inTe = aff && has_left ? (int32_t*)S.top.left_in_e.get((size_t)(h1 + 1) * 4) : nullptr;
+    int32_t* inBe = aff && has_right ? (int32_t*)S.bot.left_in_e.get((size_t)(h2 + 1) * 4) : nullptr;
+    if (inTe) HIPCHECK(hipMemsetAsync(inTe, 0x80, (size_t)(h1 + 1) * 4, S.st));
+    if (inBe) HIPCHECK(hipMemsetAsync(inBe, 0x80, (size_t)(h2 + 1) * 4, S.st));
+    if (direct && aff) {
+        HIPCHECK(hipMemsetAsync(colTe, 0x80, (size_t)(h1 + 1) * 4, S.st));
+        HIPCHECK(hipMemsetAsync(colBe, 0x80, (size_t)(h2 + 1) * 4, S.st));
+    }
+    S.lTe = inTe;
+    S.lBe = inBe;
     // out_col: sent downstream; also the semiglobal end column on the edge shards
     int32_t* colT = (int32_t*)S.top.out_col.get((size_t)h1 * 4);
     int32_t* colB = (int32_t*)S.bot.out_col.get((size_t)h2 * 4);
@@ -200,6 +226,9 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     P.out_row = rowT;
     P.out_col = colT;
     P.left_in = inT;
+    P.left_in_e = inTe;
+    P.out_col_e = colTe;
+    P.out_f_last = colTe ? colTe + h1 : nullptr;
     S.lT = inT;
     S.lB = inB;
     P.left_shift = shT * ng;
@@ -213,6 +242,9 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     P.out_row = rowB;
     P.out_col = colB;
     P.left_in = inB;
+    P.left_in_e = inBe;
+    P.out_col_e = colBe;
+    P.out_f_last = colBe ? colBe + h2 : nullptr;
     P.left_shift = shB * ng;
     P.progress = S.bot.progress;
     probs.push_back(P);
@@ -229,6 +261,7 @@ struct Xfer {
     int device = 0;
     Front* src = nullptr;
     int32_t* dst = nullptr;         // local transport: the neighbour's left_in
+    int32_t* dst_e = nullptr;       // affine: the neighbour's left_in_e (RCCL: receive E into it)
     ncclComm_t comm = nullptr;      // RCCL transport
     int peer = -1;
     bool recv = false;              // RCCL: receive into dst instead of sending
@@ -242,8 +275,13 @@ void run_xfer(Xfer* x) {
         const int CR = chunk_rows();
         for (int r0 = 0; r0 < x->h; r0 += CR) {
             const int r1 = std::min(x->h, r0 + CR);
+            // affine: E rows follow the H rows; the last chunk's E carries one more
+            // element, [h] = F of the last row at the last column
+            const size_t ne = (size_t)(r1 - r0) + (r1 == x->h ? 1 : 0);
             if (x->recv) {
                 NCCLCHECK(ncclRecv(x->dst + r0, (size_t)(r1 - r0), ncclInt32, x->peer, x->comm, x->src->s_recv));
+                if (x->src->aff)
+                    NCCLCHECK(ncclRecv(x->dst_e + r0, ne, ncclInt32, x->peer, x->comm, x->src->s_recv));
                 continue;
             }
             const uint32_t need = bands_for_rows(r1);
@@ -259,11 +297,16 @@ void run_xfer(Xfer* x) {
                 }
             }
             const int32_t* src = (const int32_t*)x->src->out_col.p + r0;
-            if (x->comm)
+            const int32_t* src_e = x->src->aff ? (const int32_t*)x->src->out_col_e.p + r0 : nullptr;
+            if (x->comm) {
                 NCCLCHECK(ncclSend(src, (size_t)(r1 - r0), ncclInt32, x->peer, x->comm, x->src->s_send));
-            else
+                if (src_e) NCCLCHECK(ncclSend(src_e, ne, ncclInt32, x->peer, x->comm, x->src->s_send));
+            } else {
                 HIPCHECK(hipMemcpyAsync(x->dst + r0, src, (size_t)(r1 - r0) * 4, hipMemcpyDeviceToDevice,
                                         x->src->s_send));
+                if (src_e)
+                    HIPCHECK(hipMemcpyAsync(x->dst_e + r0, src_e, ne * 4, hipMemcpyDeviceToDevice, x->src->s_send));
+            }
         }
     } catch (const Failure& f) {
         x->error = f.msg;
@@ -301,6 +344,7 @@ std::vector<Xfer> local_xfers(std::vector<Shard>& shards, int N, int device) {
             x.device = device;
             x.src = &S.top;
             x.dst = (int32_t*)shards[g + 1].top.left_in.p;
+            x.dst_e = (int32_t*)shards[g + 1].top.left_in_e.p;
             x.h = S.top.h;
             xs.push_back(x);
         }
@@ -309,6 +353,7 @@ std::vector<Xfer> local_xfers(std::vector<Shard>& shards, int N, int device) {
             x.device = device;
             x.src = &S.bot;
             x.dst = (int32_t*)shards[g - 1].bot.left_in.p;
+            x.dst_e = (int32_t*)shards[g - 1].bot.left_in_e.p;
             x.h = S.bot.h;
             xs.push_back(x);
         }
@@ -330,6 +375,7 @@ std::vector<Xfer> rccl_xfers(RcclState& R, int device) {
         x.peer = peer;
         x.comm = c;
         x.dst = recv ? (int32_t*)f->left_in.p : nullptr;
+        x.dst_e = recv ? (int32_t*)f->left_in_e.p : nullptr;
         x.h = f->h;
         xs.push_back(x);
     };
@@ -354,6 +400,13 @@ void enqueue_combine(Shard& S, int N, int kind, const anyseq_scoring& sc, int m,
     const int adj = kind == KIND_GLOBAL ? (m - w) * gap : 0;
     const int32_t* colT = (kind == KIND_SEMIGLOBAL && g == N - 1) ? (const int32_t*)S.top.out_col.p : nullptr;
     const int32_t* colB = (kind == KIND_SEMIGLOBAL && g == 0) ? (const int32_t*)S.bot.out_col.p : nullptr;
+    if (sc.gap_open != 0) {
+        HIPCHECK(anyseq_launch_shard_aff_combine(kind, S.top.out_row.p, h1, S.bot.out_row.p, h2, w, sc.gap_open, gap,
+                                                 S.lT, S.lTe ? S.lTe + h1 : nullptr, shT, S.lB,
+                                                 S.lBe ? S.lBe + h2 : nullptr, shB, g == N - 1 ? 1 : 0, colT, colB, adj,
+                                                 res, S.st));
+        return;
+    }
     HIPCHECK(anyseq_launch_shard_combine(kind, (const int32_t*)S.top.out_row.p, h1, (const int32_t*)S.bot.out_row.p,
                                          h2, w, gap, S.lT, shT, S.lB, shB,
                                          g == N - 1 ? 1 : 0, colT, colB, adj, res, S.st));
@@ -361,7 +414,6 @@ void enqueue_combine(Shard& S, int N, int kind, const anyseq_scoring& sc, int m,
 
 void check_shard_shape(int kind, const anyseq_scoring& sc, int n, int m, int N) {
     check_scoring(kind, sc);
-    if (sc.gap_open != 0) fail("sharded fill: affine gaps are not supported yet (linear only)");
     if (N < 1) fail("sharded fill: need at least one shard");
     if (n < 2) fail("sharded fill: need at least 2 query rows (two fronts), got %d", n);
     if (m < N) fail("sharded fill: %d columns cannot be split over %d shards", m, N);
@@ -413,6 +465,10 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
         for (int g = 0; g < N; ++g) {
             if (g > 0) shards[g].lT = probs[g][0].left_in = (const int32_t*)shards[g - 1].top.out_col.p;
             if (g + 1 < N) shards[g].lB = probs[g][1].left_in = (const int32_t*)shards[g + 1].bot.out_col.p;
+            if (sc.gap_open != 0) {
+                if (g > 0) shards[g].lTe = probs[g][0].left_in_e = (const int32_t*)shards[g - 1].top.out_col_e.p;
+                if (g + 1 < N) shards[g].lBe = probs[g][1].left_in_e = (const int32_t*)shards[g + 1].bot.out_col_e.p;
+            }
             for (int k = 0; k < N; ++k)
                 if (k != g) HIPCHECK(hipStreamWaitEvent(shards[g].st, shards[k].ready, 0));
         }

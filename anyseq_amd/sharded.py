@@ -4,7 +4,8 @@ SURVEY.md §8(e) / DESIGN.md §6.  Rank g owns subject columns
 ``shard_plan.block(g, world, m)``; the boundary columns travel between
 neighbouring ranks with RCCL ncclSend/ncclRecv over xGMI inside
 libanyseq.so (anyseq_shard.cpp) while the fills run; the per-rank split
-candidates are reduced with one MAX all-reduce.  torch.distributed (any backend,
+candidates are reduced with one MAX all-reduce.  Linear and affine gaps (the
+affine boundary column carries (H, E) plus F of the last row).  torch.distributed (any backend,
 ``gloo`` is enough) only broadcasts the RCCL unique ids.
 """
 from __future__ import annotations
@@ -52,9 +53,11 @@ def finalize() -> None:
     _lib.anyseq_shard_finalize()
 
 
-def make_weak_step(dist, rank: int, world: int, kind: str, rows: int = 65536, cols_per_rank: int = 65536):
+def make_weak_step(dist, rank: int, world: int, kind: str, rows: int = 65536, cols_per_rank: int = 65536,
+                   gap_open: int = 0):
     """bench.py's weak-scaling workload: `rows` x (cols_per_rank * world) cells, each
-    rank owning one block of cols_per_rank columns (main.cpp generator inputs)."""
+    rank owning one block of cols_per_rank columns (main.cpp generator inputs);
+    gap_open != 0 runs the affine fill (+2/-1, open gap_open, extend -1)."""
     L = cols_per_rank * world
     q, s = main_random_pair(max(L, rows), max(L, rows))
     q, s = q[:rows], s[:L]
@@ -62,7 +65,7 @@ def make_weak_step(dist, rank: int, world: int, kind: str, rows: int = 65536, co
     load(q, s, rank, world)
 
     def step():
-        return score(kind)
+        return score(kind, gap_open=gap_open, gap_extend=-1)
 
     par = f"column blocks x{world} (RCCL boundary columns over xGMI)"
     return step, rows, cols_per_rank, par

@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3],
                     help="BASELINE.json configs index: 1 NW linear score, 2 SW affine score+traceback, "
                          "3 genome semi-global affine traceback")
+    ap.add_argument("--gap-open", type=int, default=0,
+                    help="config 1 only: affine gap open (extend -1); 0 = the reference's linear scheme")
     ap.add_argument("--fasta", nargs=2, metavar=("QUERY", "SUBJECT"), help="config 3: real genome files")
     ap.add_argument("--cpu-threads", type=int, default=4,
                     help="oracle threads (reference get_thread_count() = 4, backend_cpu.impala:13)")
@@ -74,18 +76,23 @@ def load_traffic(kernel_tag: str):
     return None, None
 
 
-def cpu_baseline(q: bytes, s: bytes, kind: str, threads: int, expect: int):
+def cpu_baseline(q: bytes, s: bytes, kind: str, threads: int, expect: int, gap_open: int = 0):
     from oracle import oracle as O   # bench.py's cpu_baseline leg is allowed to use the oracle
     O.build()
     O.set_threads(threads)
     t = time.perf_counter()
-    v = O.score(kind, q, s)
+    if gap_open:
+        v = O.affine_score(kind, q, s, 2, -1, gap_open, -1)   # single-threaded restatement
+        threads = 1
+    else:
+        v = O.score(kind, q, s)
     dt = time.perf_counter() - t
     if v != expect:
         raise SystemExit(f"cpu baseline disagrees with GPU: {v} != {expect}")
+    what = (f"affine (open {gap_open}) score (oracle_affine_score, 1 thread)" if gap_open else
+            f"linear score (oracle restatement of iteration_cpu/scoring_cpu, 1024^2 tiles, {threads} threads)")
     return {"value": round(len(q) * len(s) / dt / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
-            "sample": f"full {len(q)}x{len(s)} {kind} linear score (oracle restatement of iteration_cpu/"
-                      f"scoring_cpu, 1024^2 tiles, {threads} threads), {dt:.2f} s"}
+            "sample": f"full {len(q)}x{len(s)} {kind} {what}, {dt:.2f} s"}
 
 
 AFFINE = dict(match=2, mismatch=-1, gap_open=-2, gap_extend=-1)
@@ -210,7 +217,8 @@ def main():
     parallelism = "single GPU"
     if dist:
         from anyseq_amd import sharded
-        step, n, m, parallelism = sharded.make_weak_step(dist, rank, world, kind, rows=args.n, cols_per_rank=args.m)
+        step, n, m, parallelism = sharded.make_weak_step(dist, rank, world, kind, rows=args.n, cols_per_rank=args.m,
+                                                         gap_open=args.gap_open)
         q = s = None
     else:
         q, s = A.main_random_pair(args.n, args.m)
@@ -221,7 +229,8 @@ def main():
         ds = torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev)
 
         def step():
-            return A.score_device(kind, dq.data_ptr(), n, ds.data_ptr(), m, stream=sh)
+            return A.score_device(kind, dq.data_ptr(), n, ds.data_ptr(), m, stream=sh, gap_open=args.gap_open,
+                                  gap_extend=-1)
 
     for _ in range(args.warmup):
         score = step()
@@ -251,7 +260,7 @@ def main():
     kernel_ms = fill_ms / max(launches, 1)
     cells_per_launch = n * m
     achieved = cells_per_launch * BYTES_PER_CELL / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
-    tag = f"fill_kernel<{kind}> {n}x{m}"
+    tag = f"fill_kernel<{kind}> {n}x{m}" if not args.gap_open else f"fill_affine_kernel<{kind}> {n}x{m}"
     traffic, traffic_src = load_traffic(tag)
 
     if rank == 0:
@@ -268,7 +277,9 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic: main.cpp `-r 65536 65536` generator (mt19937_64 default seed, uniform ACGT)",
-            "config": {"workload": f"{kind} alignment score, linear gap (+2/-1/-1), {n}x{m} cells per GPU",
+            "config": {"workload": f"{kind} alignment score, "
+                                   + (f"affine gap (+2/-1, open {args.gap_open}, extend -1)" if args.gap_open
+                                      else "linear gap (+2/-1/-1)") + f", {n}x{m} cells per GPU",
                        "query_len": n, "subject_len": m,
                        "parallelism": parallelism,
                        "score": int(score)},
@@ -282,7 +293,7 @@ def main():
                          "traffic_source": traffic_src},
         }
         if world == 1 and not dist and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(q, s, kind, args.cpu_threads, int(score))
+            out["cpu_baseline"] = cpu_baseline(q, s, kind, args.cpu_threads, int(score), args.gap_open)
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

@@ -119,7 +119,8 @@ void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells);
 /* ---- column-block sharded score (build-defined) ----
  * Subject columns are split into contiguous blocks, block g = [g*m/N, (g+1)*m/N);
  * the boundary columns of the two fill fronts travel between neighbouring shards
- * in row chunks while the fills run.  Linear gaps only.
+ * in row chunks while the fills run.  Linear and affine gaps (affine: the column
+ * carries H and E, plus F of the front's last row).
  *
  * One process per GPU over RCCL: rank 0 calls anyseq_shard_unique_ids (count = 4),
  * the bytes (count * 128) are broadcast out of band, every rank calls
