@@ -69,3 +69,16 @@ def make_weak_step(dist, rank: int, world: int, kind: str, rows: int = 65536, co
 
     par = f"column blocks x{world} (RCCL boundary columns over xGMI)"
     return step, rows, cols_per_rank, par
+
+
+def make_strong_step(dist, rank: int, world: int, query, subject, kind: str, gap_open: int = 0):
+    """bench.py --config 4: ONE fixed matrix (strong scaling), rank g owning subject
+    block g of `world`; the inputs must be identical on every rank."""
+    init(dist, rank, world)
+    load(query, subject, rank, world)
+
+    def step():
+        return score(kind, gap_open=gap_open, gap_extend=-1)
+
+    par = f"column blocks x{world} (RCCL boundary columns over xGMI)"
+    return step, len(_b(query)), len(_b(subject)), par

@@ -51,9 +51,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="run the RCCL column-block path even at N=1 (plumbing check; the N=1 line is single GPU)")
-    ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3],
+    ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
                     help="BASELINE.json configs index: 1 NW linear score, 2 SW affine score+traceback, "
-                         "3 genome semi-global affine traceback")
+                         "3 genome semi-global affine traceback, 4 genome semi-global affine score "
+                         "column-blocked over the ranks (strong scaling)")
     ap.add_argument("--gap-open", type=int, default=0,
                     help="config 1 only: affine gap open (extend -1); 0 = the reference's linear scheme")
     ap.add_argument("--fasta", nargs=2, metavar=("QUERY", "SUBJECT"), help="config 3: real genome files")
@@ -187,10 +188,14 @@ def construct_bench(args):
 
 def main():
     args = parse()
-    if args.config != 1:
+    if args.config in (2, 3):
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             raise SystemExit("--config 2/3 run on one GPU (the column-block sharded path is config 1 / 4)")
         return construct_bench(args)
+    genome = args.config == 4
+    if genome:   # configs[4]: semi-global affine, one genome-length matrix split over the ranks
+        args.kind, args.sharded = "semiglobal", True
+        args.gap_open = args.gap_open or -2
     # the sharded path's fill + transport streams each need a hardware queue of their own
     # (anyseq_shard.cpp check_hw_queues); HIP reads this at its first call
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
@@ -215,7 +220,14 @@ def main():
 
     kind = args.kind
     parallelism = "single GPU"
-    if dist:
+    if dist and genome:
+        from anyseq_amd import sharded, genome as G
+        if args.fasta:
+            (_, q), (_, s) = G.first_record(args.fasta[0]), G.first_record(args.fasta[1])
+        else:
+            q, s = G.synthetic_related_pair(4_641_652, 0.9)
+        step, n, m, parallelism = sharded.make_strong_step(dist, rank, world, q, s, kind, gap_open=args.gap_open)
+    elif dist:
         from anyseq_amd import sharded
         step, n, m, parallelism = sharded.make_weak_step(dist, rank, world, kind, rows=args.n, cols_per_rank=args.m,
                                                          gap_open=args.gap_open)
@@ -254,11 +266,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    cells_per_step = n * m * world          # weak scaling: each rank owns n x m cells
+    if genome:   # strong scaling: one n x m matrix, rank 0's launch covers its column block
+        from anyseq_amd import shard_plan
+        cells_per_step = n * m
+        cells_per_launch = n * shard_plan.block(0, world, m)[1]
+    else:        # weak scaling: each rank owns n x m cells
+        cells_per_step = n * m * world
+        cells_per_launch = n * m
     ms_per_step = elapsed * 1e3 / args.steps
     gcups = cells_per_step * args.steps / elapsed / 1e9
     kernel_ms = fill_ms / max(launches, 1)
-    cells_per_launch = n * m
     achieved = cells_per_launch * BYTES_PER_CELL / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
     tag = f"fill_kernel<{kind}> {n}x{m}" if not args.gap_open else f"fill_affine_kernel<{kind}> {n}x{m}"
     traffic, traffic_src = load_traffic(tag)
@@ -273,13 +290,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if genome else "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic: main.cpp `-r 65536 65536` generator (mt19937_64 default seed, uniform ACGT)",
+            "data": ("synthetic related-genome pair (E. coli K-12 length, 90% identity; the reference's "
+                     "ecoli/sboydii FASTAs are absent)" if genome and not args.fasta else
+                     "FASTA first records" if genome else
+                     "synthetic: main.cpp `-r 65536 65536` generator (mt19937_64 default seed, uniform ACGT)"),
             "config": {"workload": f"{kind} alignment score, "
                                    + (f"affine gap (+2/-1, open {args.gap_open}, extend -1)" if args.gap_open
-                                      else "linear gap (+2/-1/-1)") + f", {n}x{m} cells per GPU",
+                                      else "linear gap (+2/-1/-1)")
+                                   + (f", one {n}x{m} matrix column-blocked over {world} GPU(s)" if genome
+                                      else f", {n}x{m} cells per GPU"),
+                       "baseline_config": args.config,
                        "query_len": n, "subject_len": m,
                        "parallelism": parallelism,
                        "score": int(score)},
@@ -294,6 +317,11 @@ def main():
         }
         if world == 1 and not dist and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(q, s, kind, args.cpu_threads, int(score), args.gap_open)
+        elif world == 1 and genome and not args.no_cpu_baseline:
+            qs, ss = q[:16384], s[:16384]
+            v = A.score(kind, qs, ss, gap_open=args.gap_open, gap_extend=-1)
+            out["cpu_baseline"] = cpu_baseline(qs, ss, kind, 1, v, args.gap_open)
+            out["cpu_baseline"]["sample"] = "16384x16384 prefix of the pair: " + out["cpu_baseline"]["sample"]
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
