@@ -306,7 +306,6 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.gap_extend = sc.gap_extend;
     fp.affine = sc.gap_open != 0;
     fp.dbg = nullptr;
-    fp.io_border = g_tuning.io_border >= 0 ? g_tuning.io_border : env_int("ANYSEQ_IO_BORDER", 1);
     fp.pad = (g_tuning.affasm & 1) ? (g_tuning.affasm & 2) : (1 | (g_tuning.affasm & 2));  // affine_asm bit0: asm steady state, bit1: scalar row stores (diagnostics)
     return fp;
 }
@@ -1053,7 +1052,6 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_grid") g_tuning.grida = value;
     else if (n == "affine_asm") g_tuning.affasm = value;
     else if (n == "ring_slots") g_tuning.ring_slots = value;
-    else if (n == "io_border") g_tuning.io_border = value;
     else return -1;
     return 0;
 }

@@ -53,7 +53,6 @@ struct Tuning {
     int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
     int affasm = 1;  // affine fill: asm steady state (0 = C++ blocks only, diagnostics)
     int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
-    int io_border = -1;  // 1: the I/O wave generates band 0's top border (-1: $ANYSEQ_IO_BORDER, default 1)
 };
 extern Tuning g_tuning;
 

@@ -73,7 +73,6 @@ struct FillParams {
     int32_t gap_open, gap_extend;     // affine (gap_open <= 0, gap_extend < 0)
     int32_t affine;
     int32_t pad;                      // affine: bit 0 = C++ steady state only (diagnostics)
-    int32_t io_border;                // 1: the I/O wave writes band 0's top border into its ring
     unsigned long long* dbg;          // diagnostic build only (ANYSEQ_STAMPS): per-launch stamp sums
 };
 

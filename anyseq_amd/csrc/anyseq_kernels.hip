@@ -774,24 +774,19 @@ struct HandOff<int2> {
     __device__ static int2 sentinel() { return make_int2((int)0x80808080, (int)0x80808080); }
 };
 
-// Border: functor column -> the scheme's top border value (row -1) in ring format.
-template <int CH, bool SKEW, typename T, typename Border>
+template <int CH, bool SKEW, typename T = int32_t>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
                         uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
-                        uint32_t* cons0, uint32_t* err, bool reset_in, bool gen_border, Border border) {
+                        uint32_t* cons0, uint32_t* err, bool reset_in = false) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
     const int nchunks = (w + CH - 1) / CH;
     const bool need_in = g_in != nullptr;
-    // the problem's first group: band 0's input row is the scheme's top border, which
-    // this wave writes into wave 0's ring ahead of it (band 0 then runs the same
-    // consumer path as every other band, off the LDS write -> read round trip)
-    const bool gen = gen_border && !need_in;
     const GLOBAL_AS uint8_t* sg = gmem(s);
     int s_next = 0, sk_next = 0, in_next = 0;
     uint32_t idle = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    while (s_next < nchunks || (SKEW && sk_next < nchunks) || ((need_in || gen) && in_next < nchunks)) {
+    while (s_next < nchunks || (SKEW && sk_next < nchunks) || (need_in && in_next < nchunks)) {
         bool progress = false;
         if (s_next < nchunks) {
             const uint32_t tl = lds_ld(tail);
@@ -837,15 +832,6 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             if (lim > sk_next) {
                 lds_st(s_filled, (uint32_t)lim);
                 sk_next = lim;
-                progress = true;
-            }
-        }
-        if (gen && in_next < nchunks) {
-            const int lim = min((int)lds_ld(cons0) + kSlots, nchunks);
-            if (lim > in_next) {
-                for (int col = in_next * CH + lane; col < lim * CH; col += 64) ring0[col & IRM] = border(col);
-                lds_st(prod0, (uint32_t)lim);
-                in_next = lim;
                 progress = true;
             }
         }
@@ -919,7 +905,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     CellK ck;
     ck.ng = -fp.gap;
-    const bool io_border = fp.io_border != 0;
     if (KIND == KIND_LOCAL) {
         ck.wm = fp.match - fp.gap;
         ck.wx = fp.mismatch - fp.gap;
@@ -954,16 +939,14 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
             g_out = P.out_row;
         if (wave == NW) {
             const int32_t* g_in = g.group > 0 ? P.rowbuf + (size_t)((g.group - 1) % P.nslots) * P.wpad : nullptr;
-            const int ngv = ck.ng;
-            io_wave<CH, R == 1 && X == 0 && CH == 32, int32_t>(
-                lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0], &sh.s_filled, &sh.tail, g_in,
-                sh.in_ring[0], &sh.prod[0], &sh.cons[0], err, P.nslots < P.ngroups - 1, io_border,
-                [=](int c) { return border_top<KIND>(c, ngv); });
+            io_wave<CH, R == 1 && X == 0 && CH == 32>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0],
+                                                      &sh.s_filled, &sh.tail, g_in, sh.in_ring[0], &sh.prod[0],
+                                                      &sh.cons[0], err, P.nslots < P.ngroups - 1);
         } else {
             const int band = first + wave;
             if (band <= last) {
                 WaveIO io;
-                io.in_border = band == 0 && !io_border;
+                io.in_border = band == 0;
                 io.trailing = band == last;
                 io.my_ring = sh.in_ring[wave];
                 io.my_prod = &sh.prod[wave];
@@ -1381,10 +1364,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
     k.wm = fp.match + 2 * k.nge;
     k.wx = fp.mismatch + 2 * k.nge;
     k.flags = fp.pad;
-    // The I/O-wave border is off for the affine fill: with it on, the 20000^2 semiglobal
-    // affine construct faulted on the box (tests/test_gpu_device_api.py), cause not found
-    // yet.  Band 0 writes its own border here, as before.
-    const bool io_border = false;
     for (;;) {
         if (threadIdx.x == 0) {
             sh.group = (int32_t)atomicAdd(dq, 1u);
@@ -1410,22 +1389,14 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
             g_out = reinterpret_cast<int2*>(P.out_row);
         if (wave == NW) {
             const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
-            // top border (G, G + go) of column c, with the construct's border modes (run_band_aff's topv)
-            const int bm = KIND == KIND_GLOBAL ? P.bmode : BM_NORMAL;
-            const int cg = bm == BM_NORMAL ? 0 : kAffNeg, tg = bm == BM_EFREE ? 0 : k.go;
-            const int go = k.go, nge = k.nge;
             io_wave<32, true, int2>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0], &sh.s_filled,
                                     &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
-                                    P.nslots < P.ngroups - 1, io_border, [=](int c) {
-                                        const int bv = KIND == KIND_GLOBAL ? (c < 0 ? cg : tg)
-                                                                            : aff_border<KIND>(c, go, nge);
-                                        return make_int2(bv, bv + go);
-                                    });
+                                    P.nslots < P.ngroups - 1);
         } else {
             const int band = first + wave;
             if (band <= last) {
                 AffIO io;
-                io.in_border = band == 0 && !io_border;
+                io.in_border = band == 0;
                 io.trailing = band == last;
                 io.my_ring = sh.in_ring[wave];
                 io.my_prod = &sh.prod[wave];
