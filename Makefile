@@ -35,15 +35,6 @@ anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_stamps.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl
 
-# timing experiments (ANYSEQ_EXP bits, see anyseq_kernels.hip); wrong results by design
-anyseq_amd/libanyseq_e%.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_io.o $(SRC)/anyseq_internal.h
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_EXP=$* -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_e$*.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_e$*.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl
-
-anyseq_amd/libanyseq_se%.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_io.o $(SRC)/anyseq_internal.h
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -DANYSEQ_EXP=$* -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_se$*.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_se$*.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl
-
 clean:
 	rm -f $(SRC)/*.o $(LIB) anyseq_amd/libanyseq_*.so
 	$(MAKE) -s -C oracle clean

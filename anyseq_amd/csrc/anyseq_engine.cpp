@@ -191,7 +191,8 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
         fo += P.ngroups;
     }
     // group table: round-robin over problems so every sub-problem progresses
-    std::vector<GroupRef> groups;
+    std::vector<GroupRef>& groups = C.h_groups;
+    groups.clear();
     for (int k = 0; k < max_groups; ++k)
         for (size_t p = 0; p < probs.size(); ++p)
             if (k < probs[p].ngroups) groups.push_back(GroupRef{(int32_t)p, k});
@@ -204,7 +205,8 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     }
     DPProblem* d_probs = (DPProblem*)C.probs.get(probs.size() * sizeof(DPProblem));
     GroupRef* d_groups = (GroupRef*)C.groups.get(groups.size() * sizeof(GroupRef));
-    HIPCHECK(hipMemcpyAsync(d_probs, probs.data(), probs.size() * sizeof(DPProblem), hipMemcpyHostToDevice, st));
+    C.h_probs = probs;
+    HIPCHECK(hipMemcpyAsync(d_probs, C.h_probs.data(), probs.size() * sizeof(DPProblem), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(d_groups, groups.data(), groups.size() * sizeof(GroupRef), hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemsetAsync(flags, 0, flag_words * 4, st));
     // group -> group hand-off rows start as a sentinel (the consumer polls the data):
@@ -574,7 +576,8 @@ void construct_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t*
     }
 
     // final level: blockwise predecessors + per-block walk (align.impala:292-311)
-    std::vector<BlockInfo> blocks((size_t)sp.nb);
+    std::vector<BlockInfo>& blocks = E.host_blocks;   // outlives the async upload
+    blocks.assign((size_t)sp.nb, BlockInfo{});
     int64_t pred_bytes = 0;
     for (int b = 0; b < sp.nb; ++b) {
         BlockInfo& bi = blocks[b];
@@ -731,7 +734,8 @@ void aff_construct_rect(Engine& E, const anyseq_scoring& sc, const uint8_t* dq, 
         pw /= 2;
         sp.bpp /= 2;
     }
-    std::vector<BlockInfo> blocks((size_t)sp.nb);
+    std::vector<BlockInfo>& blocks = E.host_blocks;   // outlives the async upload
+    blocks.assign((size_t)sp.nb, BlockInfo{});
     int64_t pred_bytes = 0;
     for (int b = 0; b < sp.nb; ++b) {
         BlockInfo& bi = blocks[b];

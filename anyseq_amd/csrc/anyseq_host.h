@@ -71,6 +71,10 @@ struct FillCtx {
     int64_t cells = 0;                      // DP cells of the prepared launch (sum of h*w)
     FillParams fp{};
     hipStream_t st = nullptr;
+    // host sources of the launch's uploads: hipMemcpyAsync may read pageable host
+    // memory after it returns, so they live as long as the context, not the call
+    std::vector<DPProblem> h_probs;
+    std::vector<GroupRef> h_groups;
     void init();
 };
 
@@ -83,6 +87,7 @@ struct Engine {
     DevBuf q, s, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq, als;
     DevBuf LE, RE, typ, rowbest, pos;   // affine construct
     std::vector<int32_t> host_i32;
+    std::vector<BlockInfo> host_blocks;
     explicit Engine(int dev);
 };
 

@@ -45,6 +45,14 @@ struct DPProblem {
     const int32_t* left_in_e;   // affine: E[r][-1] (H space), polled like left_in
     int32_t* out_f_last;        // affine shard: F of the last row at the last column (H space)
     int32_t left_shift;
+    // Chunk-ready flags of left_in / left_in_e (transported columns): the transport
+    // writes flag k (0 -> 1) in stream order after chunk k's rows [k*left_chunk,
+    // (k+1)*left_chunk) have landed.  A copy engine may write a chunk's bytes in any
+    // order, so the data words themselves are never polled (a sentinel word can be
+    // seen half overwritten).  Null: left_in is written by kernel dword stores (local
+    // direct mode) and polled against kShardSentinel.
+    const uint32_t* left_flag;
+    int32_t left_chunk;
     // Affine global sub-problems of the affine construct: border
     // mode of the top-left corner.  0: the scheme's borders; 1 (E_FREE): the path
     // continues a horizontal gap (corner and left column -inf, top row without the

@@ -90,11 +90,6 @@ __device__ __forceinline__ int to_h(int v, int r, int c, int ng) {
     return KIND == KIND_LOCAL ? v : v - (r + c + 2) * ng;
 }
 
-// Diagnostic experiments (timing builds only, results are wrong): bit 1 skips the
-// subject reads, bit 2 the bottom-row writes, bit 4 the hand-scheduled block.
-#ifndef ANYSEQ_EXP
-#define ANYSEQ_EXP 0
-#endif
 
 constexpr int kSlots = 16;     // in-ring depth in chunks
 constexpr int kSRing = 4096;   // shared subject ring bytes per workgroup (+64 mirrored)
@@ -386,17 +381,41 @@ __device__ __forceinline__ void load_sbytes(const uint8_t* s_ring, int p, uint32
     for (int i = 0; i < CH / 4; ++i) out[i] = __builtin_amdgcn_alignbit(d[i + 1], d[i], sh);
 }
 
-// Column-block sharding: this lane's left-border values H[row][-1] and H[row-1][-1]
-// from the problem's left_in buffer (sentinel-polled; row -1 is the corner, whose
-// value is the scheme's border in every shard frame).  Returns false on timeout.
+// Column-block sharding: wait until the transported left column holds every row
+// this band reads (rows rb-1 .. min(rb+63, h-1), rb = lane 0's row): the chunk
+// flag of the band's last row (flags are set in chunk order, DPProblem::left_flag).
+// Without flags (local direct mode) the kernel-written words themselves are polled
+// against the sentinel.  Returns false on timeout.
+__device__ __forceinline__ bool wait_left(const DPProblem& P, int row, uint32_t* err) {
+    if (!P.left_flag) return true;
+    const int rb = __builtin_amdgcn_readfirstlane(row);
+    const int last = min(rb + 63, P.h - 1);
+    if (last < 0) return true;
+    uint32_t* f = const_cast<uint32_t*>(P.left_flag) + last / P.left_chunk;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t it = 0;
+    while (__hip_atomic_load(gmem(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        __builtin_amdgcn_s_sleep(4);
+        if ((++it & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
+            atomicOr(err, ERR_SPIN_TIMEOUT | 2u);
+            return false;
+        }
+    }
+    return true;
+}
+
+// This lane's left-border values H[row][-1] and H[row-1][-1] from the problem's
+// left_in buffer (row -1 is the corner, whose value is the scheme's border in
+// every shard frame).  Returns false on timeout.
 __device__ __forceinline__ bool poll_left(const DPProblem& P, int row, int32_t& v1, int32_t& v0, uint32_t* err) {
+    if (!wait_left(P, row, err)) return false;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t it = 0;
     for (;;) {
         const bool has1 = row < P.h, has0 = row >= 1 && row - 1 < P.h;
         v1 = has1 ? __hip_atomic_load(gmem(P.left_in) + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
         v0 = has0 ? __hip_atomic_load(gmem(P.left_in) + row - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        if (__ballot((has1 && v1 == kShardSentinel) || (has0 && v0 == kShardSentinel)) == 0) break;
+        if (P.left_flag || __ballot((has1 && v1 == kShardSentinel) || (has0 && v0 == kShardSentinel)) == 0) break;
         __builtin_amdgcn_s_sleep(4);
         if ((++it & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
             atomicOr(err, ERR_SPIN_TIMEOUT | 2u);
@@ -408,14 +427,15 @@ __device__ __forceinline__ bool poll_left(const DPProblem& P, int row, int32_t& 
     return true;
 }
 
-// Affine shard: this lane's E[row][-1] from left_in_e (sentinel-polled like poll_left).
+// Affine shard: this lane's E[row][-1] from left_in_e (after poll_left: with flags
+// the chunk has landed; without, the words are sentinel-polled like poll_left).
 __device__ __forceinline__ bool poll_left_e(const DPProblem& P, int row, int32_t& e1, uint32_t* err) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t it = 0;
     for (;;) {
         const bool has1 = row < P.h;
         e1 = has1 ? __hip_atomic_load(gmem(P.left_in_e) + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        if (__ballot(has1 && e1 == kShardSentinel) == 0) break;
+        if (P.left_flag || __ballot(has1 && e1 == kShardSentinel) == 0) break;
         __builtin_amdgcn_s_sleep(4);
         if ((++it & 63) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
             atomicOr(err, ERR_SPIN_TIMEOUT | 2u);
@@ -516,7 +536,7 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
     uint32_t sw[R][CH / 4];
 
     // the hand-scheduled steady-state block reads its top-row values itself
-    constexpr bool ASM = R == 1 && X == 0 && CH == 32 && !PARTIAL && !(ANYSEQ_EXP & 16);
+    constexpr bool ASM = R == 1 && X == 0 && CH == 32 && !PARTIAL;
 
     // Acquire block bb's inputs: wait for the top-row chunk bb (in-ring) and the
     // subject bytes, load the subject bytes of every row and (unless the asm block
@@ -538,16 +558,9 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
             }
         }
         if (!asm_blk) {
-            if (ANYSEQ_EXP & 2) {
 #pragma unroll
-                for (int k = 0; k < R; ++k)
-#pragma unroll
-                    for (int q = 0; q < CH / 4; ++q) sw[k][q] = (uint32_t)(tb * 0x01010101 + lane + k + q);
-            } else {
-#pragma unroll
-                for (int k = 0; k < R; ++k)
-                    load_sbytes<CH>(io.s_ring, (tb - BASE - S * lane - k) & (kSRing - 1), sw[k]);
-            }
+            for (int k = 0; k < R; ++k)
+                load_sbytes<CH>(io.s_ring, (tb - BASE - S * lane - k) & (kSRing - 1), sw[k]);
         }
         if (bb < nchunks) {
             if (io.in_border) {
@@ -591,7 +604,7 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         la.lid4 = 4u * lane;
         la.bvb = (uint32_t)border_top<KIND>(lane, ng);
         la.bvs = (uint32_t)(border_top<KIND>(1, ng) - border_top<KIND>(0, ng));
-        la.fl = (io.in_border ? 1u : 0u) | (io.trailing ? 2u : 0u) | (io.out_lds && !(ANYSEQ_EXP & 4) ? 4u : 0u) |
+        la.fl = (io.in_border ? 1u : 0u) | (io.trailing ? 2u : 0u) | (io.out_lds ? 4u : 0u) |
                 (io.gout ? 8u : 0u);
         la.gp = (uint64_t)(size_t)io.gout;
     }
@@ -599,7 +612,7 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         const int t0 = b * CH;
         const bool full = (virt || t0 >= D) && (t0 + CH <= w + BASE);
         if constexpr (ASM) {
-            if (full && !(ANYSEQ_EXP & 32)) {
+            if (full) {
 #ifdef ANYSEQ_STAMPS
                 if (b == 0 && dbg && lane == 0 && band < 2048) dbg[16 + 4 * (band + (P.q_step < 0 ? 2048 : 0))] = __builtin_amdgcn_s_memrealtime();
                 STAMP(tl0);
@@ -659,7 +672,7 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
         }
         if (ASM && full) {
             if constexpr (ASM) {
-                const bool st = pub && !(ANYSEQ_EXP & 4);
+                const bool st = pub;
                 const uint32_t pa = st && lane >= 32 ? lds_addr(io.next_ring + ((j * CH) & IRM) + (lane - 32))
                                                      : lds_addr(io.dummy + lane);
                 const uint64_t pm = 0;
@@ -677,7 +690,7 @@ __device__ void run_band(const DPProblem& P, int band, int lane, const WaveIO& i
                 band_block<KIND, R, X, CH, true, PARTIAL, false>(t0, lane, w, top_first, rv, sw, qv, dead, cur, prev,
                                                                  upc, dg, outv, best, ck);
             top_first = rv[CH - 1];
-            if (pub && lane == 63 && !(ANYSEQ_EXP & 4)) {
+            if (pub && lane == 63) {
                 int4* dst = reinterpret_cast<int4*>(io.next_ring + ((j * CH) & IRM));
 #pragma unroll
                 for (int q = 0; q < CH / 4; ++q)

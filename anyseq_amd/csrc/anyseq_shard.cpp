@@ -72,6 +72,7 @@ struct Front {
     // affine: out_col_e / left_in_e hold E of the last column, h rows, plus [h] = F of
     // the last row at the last column (the combine's vertical-gap join)
     DevBuf out_col, left_in, out_row, out_col_e, left_in_e;
+    DevBuf left_flag;   // chunk-ready flags of left_in / left_in_e (DPProblem::left_flag)
     bool aff = false;
     uint32_t* progress = nullptr;     // device view of the counter (what the kernel bumps)
     uint32_t* progress_h = nullptr;   // host view (pinned, coherent) -- host-poll transport
@@ -95,7 +96,8 @@ struct Shard {
         if (st) return;
         // polled across kernels / XCDs: never L2-cached (see DevBuf::uncached)
         for (Front* f : {&top, &bot})
-            f->out_col.uncached = f->left_in.uncached = f->out_col_e.uncached = f->left_in_e.uncached = true;
+            f->out_col.uncached = f->left_in.uncached = f->out_col_e.uncached = f->left_in_e.uncached =
+                f->left_flag.uncached = true;
         HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
         HIPCHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
         for (Front* f : {&top, &bot}) {
@@ -198,6 +200,18 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     int32_t* inB = has_right ? (int32_t*)S.bot.left_in.get((size_t)h2 * 4) : nullptr;
     if (inT) HIPCHECK(hipMemsetAsync(inT, 0x80, (size_t)h1 * 4, S.st));
     if (inB) HIPCHECK(hipMemsetAsync(inB, 0x80, (size_t)h2 * 4, S.st));
+    // chunk-ready flags of the received columns (the transport sets flag k after chunk k)
+    const int CR = chunk_rows();
+    uint32_t* flT = nullptr;
+    uint32_t* flB = nullptr;
+    if (inT && !direct) {
+        flT = (uint32_t*)S.top.left_flag.get((size_t)((h1 + CR - 1) / CR) * 4);
+        HIPCHECK(hipMemsetAsync(flT, 0, (size_t)((h1 + CR - 1) / CR) * 4, S.st));
+    }
+    if (inB && !direct) {
+        flB = (uint32_t*)S.bot.left_flag.get((size_t)((h2 + CR - 1) / CR) * 4);
+        HIPCHECK(hipMemsetAsync(flB, 0, (size_t)((h2 + CR - 1) / CR) * 4, S.st));
+    }
     if (direct) {   // local direct mode: the neighbours poll these columns themselves
         HIPCHECK(hipMemsetAsync(colT, 0x80, (size_t)h1 * 4, S.st));
         HIPCHECK(hipMemsetAsync(colB, 0x80, (size_t)h2 * 4, S.st));
@@ -227,6 +241,8 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     P.out_col = colT;
     P.left_in = inT;
     P.left_in_e = inTe;
+    P.left_flag = flT;
+    P.left_chunk = CR;
     P.out_col_e = colTe;
     P.out_f_last = colTe ? colTe + h1 : nullptr;
     S.lT = inT;
@@ -243,6 +259,7 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     P.out_col = colB;
     P.left_in = inB;
     P.left_in_e = inBe;
+    P.left_flag = flB;
     P.out_col_e = colBe;
     P.out_f_last = colBe ? colBe + h2 : nullptr;
     P.left_shift = shB * ng;
@@ -262,6 +279,7 @@ struct Xfer {
     Front* src = nullptr;
     int32_t* dst = nullptr;         // local transport: the neighbour's left_in
     int32_t* dst_e = nullptr;       // affine: the neighbour's left_in_e (RCCL: receive E into it)
+    uint32_t* flag = nullptr;       // the receiver's chunk-ready flags (set after each chunk's data)
     ncclComm_t comm = nullptr;      // RCCL transport
     int peer = -1;
     bool recv = false;              // RCCL: receive into dst instead of sending
@@ -282,6 +300,8 @@ void run_xfer(Xfer* x) {
                 NCCLCHECK(ncclRecv(x->dst + r0, (size_t)(r1 - r0), ncclInt32, x->peer, x->comm, x->src->s_recv));
                 if (x->src->aff)
                     NCCLCHECK(ncclRecv(x->dst_e + r0, ne, ncclInt32, x->peer, x->comm, x->src->s_recv));
+                // in stream order after the chunk's data: the only word the fill polls
+                HIPCHECK(hipMemsetD32Async(x->flag + r0 / CR, 1u, 1, x->src->s_recv));
                 continue;
             }
             const uint32_t need = bands_for_rows(r1);
@@ -306,6 +326,7 @@ void run_xfer(Xfer* x) {
                                         x->src->s_send));
                 if (src_e)
                     HIPCHECK(hipMemcpyAsync(x->dst_e + r0, src_e, ne * 4, hipMemcpyDeviceToDevice, x->src->s_send));
+                HIPCHECK(hipMemsetD32Async(x->flag + r0 / CR, 1u, 1, x->src->s_send));
             }
         }
     } catch (const Failure& f) {
@@ -345,6 +366,7 @@ std::vector<Xfer> local_xfers(std::vector<Shard>& shards, int N, int device) {
             x.src = &S.top;
             x.dst = (int32_t*)shards[g + 1].top.left_in.p;
             x.dst_e = (int32_t*)shards[g + 1].top.left_in_e.p;
+            x.flag = (uint32_t*)shards[g + 1].top.left_flag.p;
             x.h = S.top.h;
             xs.push_back(x);
         }
@@ -354,6 +376,7 @@ std::vector<Xfer> local_xfers(std::vector<Shard>& shards, int N, int device) {
             x.src = &S.bot;
             x.dst = (int32_t*)shards[g - 1].bot.left_in.p;
             x.dst_e = (int32_t*)shards[g - 1].bot.left_in_e.p;
+            x.flag = (uint32_t*)shards[g - 1].bot.left_flag.p;
             x.h = S.bot.h;
             xs.push_back(x);
         }
@@ -376,6 +399,7 @@ std::vector<Xfer> rccl_xfers(RcclState& R, int device) {
         x.comm = c;
         x.dst = recv ? (int32_t*)f->left_in.p : nullptr;
         x.dst_e = recv ? (int32_t*)f->left_in_e.p : nullptr;
+        x.flag = recv ? (uint32_t*)f->left_flag.p : nullptr;
         x.h = f->h;
         xs.push_back(x);
     };
@@ -410,6 +434,47 @@ void enqueue_combine(Shard& S, int N, int kind, const anyseq_scoring& sc, int m,
     HIPCHECK(anyseq_launch_shard_combine(kind, (const int32_t*)S.top.out_row.p, h1, (const int32_t*)S.bot.out_row.p,
                                          h2, w, gap, S.lT, shT, S.lB, shB,
                                          g == N - 1 ? 1 : 0, colT, colB, adj, res, S.st));
+}
+
+// Diagnostics (ANYSEQ_SHARD_DUMP=<path>): every combine input of the last local
+// sharded call, plus each shard's combine alone, written as text.
+void dump_arr(FILE* f, const char* name, const void* d, size_t n) {
+    std::vector<int32_t> h(n);
+    if (d && n) (void)hipMemcpy(h.data(), d, n * 4, hipMemcpyDeviceToHost);
+    fprintf(f, "%s:", name);
+    if (!d) fprintf(f, " null");
+    for (size_t i = 0; d && i < n; ++i) fprintf(f, " %d", h[i]);
+    fprintf(f, "\n");
+}
+
+void dump_shards(const char* path, std::vector<Shard>& shards, int N, int kind, const anyseq_scoring& sc, int m, int h1,
+                 int h2, int32_t v) {
+    FILE* f = fopen(path, "w");
+    if (!f) return;
+    const bool aff = sc.gap_open != 0;
+    fprintf(f, "kind %d N %d m %d h1 %d h2 %d result %d\n", kind, N, m, h1, h2, v);
+    static DevBuf one;
+    int32_t* r1 = (int32_t*)one.get(64);
+    for (int g = 0; g < N; ++g) {
+        Shard& S = shards[g];
+        fprintf(f, "shard %d c0 %d w %d\n", g, S.c0, S.w);
+        dump_arr(f, "rowT", S.top.out_row.p, (size_t)S.w * (aff ? 2 : 1));
+        dump_arr(f, "rowB", S.bot.out_row.p, (size_t)S.w * (aff ? 2 : 1));
+        dump_arr(f, "colT", S.top.out_col.p, (size_t)h1);
+        dump_arr(f, "colB", S.bot.out_col.p, (size_t)h2);
+        if (aff) dump_arr(f, "colTe", S.top.out_col_e.p, (size_t)h1 + 1);
+        if (aff) dump_arr(f, "colBe", S.bot.out_col_e.p, (size_t)h2 + 1);
+        dump_arr(f, "lT", S.lT, (size_t)h1);
+        dump_arr(f, "lB", S.lB, (size_t)h2);
+        if (aff) dump_arr(f, "lTe", S.lTe, (size_t)h1 + 1);
+        if (aff) dump_arr(f, "lBe", S.lBe, (size_t)h2 + 1);
+        HIPCHECK(hipMemset(r1, kind == KIND_LOCAL ? 0 : 0x80, 4));
+        HIPCHECK(hipDeviceSynchronize());
+        enqueue_combine(S, N, kind, sc, m, h1, h2, r1);
+        HIPCHECK(hipStreamSynchronize(S.st));
+        dump_arr(f, "combine", r1, 1);
+    }
+    fclose(f);
 }
 
 void check_shard_shape(int kind, const anyseq_scoring& sc, int n, int m, int N) {
@@ -482,7 +547,7 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
             }
     static DevBuf stage_buf;
     uint32_t* stage = nullptr;
-    const int nbmax = (n + 63) / 64 + 1;
+    const int nbmax = std::max((n + 63) / 64 + 1, 128);
     if (env_int("ANYSEQ_SHARD_DEBUG", 0)) {
         stage = (uint32_t*)stage_buf.get((size_t)N * 2 * nbmax * 4);
         HIPCHECK(hipMemset(stage, 0, (size_t)N * 2 * nbmax * 4));
@@ -543,6 +608,19 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
     int32_t v = 0;
     for (int g = 0; g < N; ++g) HIPCHECK(hipStreamSynchronize(shards[g].st));
     HIPCHECK(hipMemcpy(&v, res, 4, hipMemcpyDeviceToHost));
+    if (const char* dump = getenv("ANYSEQ_SHARD_DUMP")) {
+        dump_shards(dump, shards, N, kind, sc, m, h1, h2, v);
+        if (stage) {
+            FILE* f = fopen(dump, "a");
+            for (int g = 0; f && g < N; ++g)
+                for (int fr = 0; fr < 2; ++fr) {
+                    char name[64];
+                    snprintf(name, sizeof name, "probe shard %d front %d", g, fr);
+                    dump_arr(f, name, stage + (g * 2 + fr) * nbmax + 64, 32);
+                }
+            if (f) fclose(f);
+        }
+    }
     return v;
 }
 

@@ -115,9 +115,9 @@ def test_fronts_and_chunk(anyseq, oracle, fronts, CH):
         for kind in KINDS:
             for n, m in [(513, 700), (2000, 1999), (4096, 64), (6001, 3000), (1024, 1)]:
                 q, s = rnd(rng, n), rnd(rng, m)
-                assert abi_score(anyseq, kind, q, s) == oracle.score(kind, q, s), (fronts, X, kind, n, m)
+                assert abi_score(anyseq, kind, q, s) == oracle.score(kind, q, s), (fronts, CH, kind, n, m)
             q, s = rnd(rng, 2500), rnd(rng, 1800)
-            assert abi_construct(anyseq, kind, q, s) == oracle.construct(kind, q, s), (fronts, X, kind)
+            assert abi_construct(anyseq, kind, q, s) == oracle.construct(kind, q, s), (fronts, CH, kind)
     finally:
         anyseq.set_option("fronts", 2)
         anyseq.set_option("chunk", 32)

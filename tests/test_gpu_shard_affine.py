@@ -58,3 +58,24 @@ def test_shard_affine_matches_single_gpu(anyseq, kind):
     ref = anyseq.score(kind, q, s, gap_open=-2, gap_extend=-1)
     for ns in (2, 4):
         assert anyseq.shard_score_local(kind, q, s, ns, gap_open=-2, gap_extend=-1) == ref, (kind, ns)
+
+
+def test_shard_received_column_never_torn(anyseq, oracle):
+    """Regression (round 2): the transport's small device copies land byte by byte, and
+    the fill used to poll the received words against a sentinel, so it could accept a
+    half-overwritten word (seen on the box: 0x80FFFFFD = sentinel high byte + the low
+    bytes of -3).  The fill now waits on per-chunk ready flags the transport writes
+    after each chunk.  This repeats the failing sequence (local, 4 shards, 3 x 40,
+    scheme (1,-3,-5,-2) after the other small cases), which mismatched about once in
+    twelve passes before the fix."""
+    for _ in range(4):
+        for ns in (1, 2, 3, 4):
+            for kind in KINDS:
+                rng = random.Random(200 + ns)
+                for it, (n, m) in enumerate([(2, 9), (3, 40), (130, 200), (700, 901)]):
+                    if m < ns:
+                        continue
+                    sc = SCHEMES[it % len(SCHEMES)]
+                    q, s = rnd(rng, n), rnd(rng, m)
+                    assert shard(anyseq, kind, q, s, ns, sc) == oracle.affine_score(kind, q, s, *sc), (kind, ns, n, m)
+                    assert anyseq.shard_score_local(kind, q, s, ns) == oracle.score(kind, q, s), (kind, ns, n, m)
