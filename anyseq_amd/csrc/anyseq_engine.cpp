@@ -43,13 +43,10 @@ hipError_t anyseq_launch_walk(const void* blocks, int nblocks, const uint8_t* Q,
 hipError_t anyseq_launch_fulltb(const uint8_t* Q, int n, const uint8_t* S, int m, uint8_t* pred, int32_t* cols,
                                 uint32_t* ticket, uint32_t* err, int match, int mismatch, int gap, uint8_t* alq,
                                 uint8_t* als, hipStream_t st);
-hipError_t anyseq_launch_aff_rowbest(const void* rowbest, int h, int32_t* out, hipStream_t st);
-hipError_t anyseq_launch_aff_edge_scan(const void* row, int w, const int32_t* col, int h, int nge, int rborder,
-                                       int cborder, int32_t* out, hipStream_t st);
 hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, const int32_t* LH, const int32_t* LE,
-                                     const int32_t* RH, const int32_t* RE, int go, int ge, int32_t* splits,
-                                     int32_t* types, hipStream_t st);
-hipError_t anyseq_launch_aff_pred(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
+                                     const int32_t* RH, const int32_t* RE, const int32_t* pbest, int go, int ge,
+                                     int32_t* splits, int32_t* types, int32_t* score, hipStream_t st);
+hipError_t anyseq_launch_aff_pred(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
                                   int match, int mismatch, int go, int ge, hipStream_t st);
 hipError_t anyseq_launch_aff_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
                                   const uint8_t* pred, uint8_t* alq, uint8_t* als, hipStream_t st);
@@ -312,6 +309,11 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     return fp;
 }
 
+void set_aff_kind(DPProblem& P, int kind) {
+    P.bmode = kind == KIND_GLOBAL ? BM_NORMAL : kind == KIND_SEMIGLOBAL ? BM_FREE_SEMI_OPEN : BM_FREE_LOCAL;
+    P.amode = kind == KIND_LOCAL ? (AM_CLAMP | AM_BEST_ALL) : 0;
+}
+
 void check_scoring(int kind, const anyseq_scoring& sc) {
     if (kind < 0 || kind > 2) fail("invalid alignment kind %d", kind);
     if (sc.gap_extend >= 0) fail("gap_extend must be negative (got %d)", sc.gap_extend);
@@ -425,6 +427,7 @@ int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const ui
     P.q_step = 1;
     P.s_step = 1;
     P.w = m;
+    set_aff_kind(P, kind);
     const int h1 = two ? n / 2 : n, h2 = n - h1;
     int32_t* rows = (int32_t*)E.outrow.get((size_t)2 * 2 * wpad * 4);
     int32_t* cols = kind != KIND_LOCAL ? (int32_t*)E.outcol.get((size_t)n * 4) : nullptr;
@@ -615,23 +618,13 @@ void construct_host(int kind, const anyseq_scoring& sc, const char* q, int n, co
 
 // ------------------------------------------------------ affine construct --
 // Build-defined linear-space affine alignment (semantics =
-// oracle_affine_construct).  Step 1 finds the aligned rectangle (global: the
-// matrix; local / semiglobal: end cell from a forward fill, start cell from a
-// GLOBAL fill of the reversed prefixes anchored at the end), step 2 aligns it
-// globally by the column-split Hirschberg of construct_host, carrying the
-// crossing state (H or E) of every split, step 3 walks the final 128-column
-// blocks.  Returns the optimal score.
-struct RectPos {
-    int32_t v, i, j;
-};
-
-RectPos read_pos(Engine& E, hipStream_t st) {
-    RectPos r;
-    HIPCHECK(hipMemcpyAsync(&r, E.pos.p, sizeof r, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
-    return r;
-}
-
+// oracle_affine_construct): ONE column-split Hirschberg over the whole matrix.
+// Every split boundary carries a row and a type (T_H / T_E crossings, T_BEFORE:
+// the path ended left of it, T_AFTER: it starts right of it), so local and
+// semiglobal ends are found by the levels themselves (a part's start or end is
+// free until a level pins it) instead of by separate end / start searches.  Each
+// level is ONE fill launch over every part's two halves, whatever their border
+// modes (fill_affine_kernel reads them per problem), then one join launch.
 DPProblem aff_problem(const uint8_t* dq, int q_off, int q_step, int h, const uint8_t* ds, int s_off, int s_step, int w) {
     DPProblem P;
     memset(&P, 0, sizeof P);
@@ -646,79 +639,87 @@ DPProblem aff_problem(const uint8_t* dq, int q_off, int q_step, int h, const uin
     return P;
 }
 
-// Position search fills (single front).  mode 0: TRACK (row-major first max of
-// all cells), 1: edge scan of the last row / column (semiglobal rule).
-RectPos aff_search(Engine& E, int kind, const anyseq_scoring& sc, DPProblem P, int mode, hipStream_t st) {
-    FillParams fp = make_params(kind, sc);
-    int32_t* pos = (int32_t*)E.pos.get(64);
-    std::vector<DPProblem> probs;
-    const int wpad = (P.w + 63) & ~63;
-    if (mode == 0) {
-        P.rowbest = (int2*)E.rowbest.get((size_t)P.h * 8);
-        probs.push_back(P);
-        run_fill(E, probs, fp, st);
-        HIPCHECK(anyseq_launch_aff_rowbest(P.rowbest, P.h, pos, st));
-    } else {
-        P.out_row = (int32_t*)E.outrow.get((size_t)wpad * 8);
-        P.out_col = (int32_t*)E.outcol.get((size_t)P.h * 4);
-        probs.push_back(P);
-        run_fill(E, probs, fp, st);
-        const int nge = -sc.gap_extend;
-        // index -1 of the row / column: the scheme's left / top border cell
-        const int rb = kind == KIND_GLOBAL ? sc.gap_open + P.h * sc.gap_extend : 0;
-        const int cb = kind == KIND_GLOBAL ? sc.gap_open + P.w * sc.gap_extend : 0;
-        HIPCHECK(anyseq_launch_aff_edge_scan(P.out_row, P.w, P.out_col, P.h, nge, rb, cb, pos, st));
-    }
-    return read_pos(E, st);
+// Border mode of a free start / end (oracle free_bm): local clamps everywhere,
+// semiglobal opens the side border only at the matrix edge.
+int free_bm(int kind, bool at_edge) {
+    return kind == KIND_LOCAL ? BM_FREE_LOCAL : (at_edge ? BM_FREE_SEMI_OPEN : BM_FREE_SEMI);
 }
 
-// Global affine Hirschberg of the rectangle dq[0..n) x ds[0..m) into d_alq/d_als
-// (already offset to the rectangle's i+j+1 origin).
-void aff_construct_rect(Engine& E, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds, int m,
-                        uint8_t* d_alq, uint8_t* d_als, hipStream_t st) {
+// Hirschberg levels + final blocks into d_alq / d_als (n+m bytes, already blank).
+// Returns the level-1 join value (the optimal score) or INT64_MIN if m <= 128
+// (no level).  kind != global with a level-1 value <= 0 stops there (empty
+// alignment).
+int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds,
+                         int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st) {
     const FillParams fp = make_params(KIND_GLOBAL, sc);
+    const bool local = kind == KIND_LOCAL;
     HostSplits sp;
     sp.nb = (m + MIN_PART_WIDTH_HB - 1) / MIN_PART_WIDTH_HB;
     sp.v.assign((size_t)sp.nb + 1, SPLIT_UNSET);
-    std::vector<int32_t> typ((size_t)sp.nb + 1, 0);
+    std::vector<int32_t> typ((size_t)sp.nb + 1, T_H);
     int pw = next_pow_2(m);
     sp.bpp = pw / MIN_PART_WIDTH_HB;
     sp.v[0] = 0;
     sp.v[sp.nb] = n;
+    if (kind != KIND_GLOBAL) {
+        typ[0] = T_AFTER;
+        typ[sp.nb] = T_BEFORE;
+    }
     int32_t* d_spl = (int32_t*)E.spl.get(sp.v.size() * 4);
     int32_t* d_typ = (int32_t*)E.typ.get(typ.size() * 4);
     HIPCHECK(hipMemcpyAsync(d_spl, sp.v.data(), sp.v.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemcpyAsync(d_typ, typ.data(), typ.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipStreamSynchronize(st));   // the host vectors change below
     const size_t nn = (size_t)std::max(n, 1) * 4;
     int32_t *LH = (int32_t*)E.L.get(nn), *LE = (int32_t*)E.LE.get(nn);
     int32_t *RH = (int32_t*)E.R.get(nn), *RE = (int32_t*)E.RE.get(nn);
+    int32_t* d_score = (int32_t*)E.pos.get(64);
     auto tp = [&](int idx) { return typ[idx + 1]; };
+    int64_t score = INT64_MIN;
+    bool level1 = true;
     while (pw > MIN_PART_WIDTH_HB) {
         const int half = pw / 2;
         const int parts = (m + half - 1) / pw;
+        int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * parts * 4);
+        HIPCHECK(hipMemsetD32Async(pbest, kAffNegH, (size_t)2 * parts, st));
         std::vector<DPProblem> probs;
-        std::vector<PartInfo> pinfo;
+        std::vector<PartInfo>& pinfo = E.host_parts;
+        pinfo.assign((size_t)parts, PartInfo{});
         for (int p = 0; p < parts; ++p) {
+            const int sb = p * sp.bpp - 1, eb = std::min((p + 1) * sp.bpp - 1, sp.nb - 1);
+            PartInfo& pi = pinfo[p];
+            pi.split_index = p * sp.bpp + sp.bpp / 2 - 1;
+            const int ts = tp(sb), te = tp(eb);
+            if (ts == T_BEFORE || te == T_AFTER) {   // empty part: so are both halves
+                pi.flags = 4;
+                pi.empty_type = ts == T_BEFORE ? T_BEFORE : T_AFTER;
+                pi.off = sp.at(sb);
+                continue;
+            }
             int off, len;
             sp.dims(p, off, len);
-            const int sb = p * sp.bpp - 1, eb = std::min((p + 1) * sp.bpp - 1, sp.nb - 1);
             const int hoj_l = p * pw, hoj_r = p * pw + half;
             const int hw = std::min(half, m - hoj_r);
-            PartInfo pi;
+            const bool sfree = ts == T_AFTER, efree = te == T_BEFORE;
             pi.off = off;
             pi.len = len;
             pi.rhw = hw;
-            pi.split_index = p * sp.bpp + sp.bpp / 2 - 1;
-            pi.smode = tp(sb) ? BM_EFREE : BM_NORMAL;
-            pinfo.push_back(pi);
+            pi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, hoj_l == 0);
+            pi.emode = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : free_bm(kind, hoj_r + hw == m);
+            pi.flags = (sfree ? 1 : 0) | (efree ? 2 : 0);
             if (len <= 0) continue;
+            const int best_bits = local ? AM_BEST_ALL : AM_BEST_LAST;
             DPProblem P = aff_problem(dq, off, 1, len, ds, hoj_l, 1, half);
             P.bmode = pi.smode;
+            P.amode = (pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0);
+            P.best = efree ? pbest + 2 * p : nullptr;
             P.out_col = LH + off;
             P.out_col_e = LE + off;
             probs.push_back(P);
             P = aff_problem(dq, off + len - 1, -1, len, ds, hoj_r + hw - 1, -1, hw);
-            P.bmode = tp(eb) ? BM_EPAID : BM_NORMAL;
+            P.bmode = pi.emode;
+            P.amode = (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0);
+            P.best = sfree ? pbest + 2 * p + 1 : nullptr;
             P.out_col = RH + off;
             P.out_col_e = RE + off;
             probs.push_back(P);
@@ -726,34 +727,48 @@ void aff_construct_rect(Engine& E, const anyseq_scoring& sc, const uint8_t* dq, 
         if (!probs.empty()) run_fill(E, probs, fp, st);
         PartInfo* d_parts = (PartInfo*)E.parts.get(pinfo.size() * sizeof(PartInfo));
         HIPCHECK(hipMemcpyAsync(d_parts, pinfo.data(), pinfo.size() * sizeof(PartInfo), hipMemcpyHostToDevice, st));
-        HIPCHECK(anyseq_launch_aff_hb_join(d_parts, parts, half, LH, LE, RH, RE, sc.gap_open, sc.gap_extend, d_spl,
-                                           d_typ, st));
+        HIPCHECK(anyseq_launch_aff_hb_join(d_parts, parts, half, LH, LE, RH, RE, pbest, sc.gap_open, sc.gap_extend,
+                                           d_spl, d_typ, level1 ? d_score : nullptr, st));
         HIPCHECK(hipMemcpyAsync(sp.v.data(), d_spl, sp.v.size() * 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipMemcpyAsync(typ.data(), d_typ, typ.size() * 4, hipMemcpyDeviceToHost, st));
+        int32_t s32 = 0;
+        if (level1) HIPCHECK(hipMemcpyAsync(&s32, d_score, 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        if (level1) {
+            // semiglobal: the empty alignment (a border cell, 0) is a candidate too
+            score = kind == KIND_SEMIGLOBAL ? std::max(s32, 0) : s32;
+            level1 = false;
+            if (kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
+        }
         pw /= 2;
         sp.bpp /= 2;
     }
     std::vector<BlockInfo>& blocks = E.host_blocks;   // outlives the async upload
-    blocks.assign((size_t)sp.nb, BlockInfo{});
+    blocks.clear();
     int64_t pred_bytes = 0;
     for (int b = 0; b < sp.nb; ++b) {
-        BlockInfo& bi = blocks[b];
+        const int ts = tp(b - 1), te = tp(b);
+        if (ts == T_BEFORE || te == T_AFTER) continue;   // the path does not touch the block
+        BlockInfo bi{};
         bi.oi = sp.at(b - 1);
         bi.h = sp.at(b) - bi.oi;
         bi.oj = b * MIN_PART_WIDTH_HB;
         bi.w = std::min(MIN_PART_WIDTH_HB, m - bi.oj);
         bi.pred_base = pred_bytes;
-        bi.smode = tp(b - 1) ? BM_EFREE : BM_NORMAL;
-        bi.e_end = tp(b);
+        bi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, bi.oj == 0);
+        bi.e_end = te == T_H ? 0 : te == T_E ? 1 : 2;
+        bi.flags = (local ? 1 : 0) | (bi.oj + bi.w == m ? 2 : 0);
         if (bi.h > 0) pred_bytes += (int64_t)(bi.h + 127) * 128;
+        blocks.push_back(bi);
     }
+    if (blocks.empty()) return score;
     BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
     HIPCHECK(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, st));
     uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
-    HIPCHECK(anyseq_launch_aff_pred(d_blocks, sp.nb, dq, ds, d_pred, sc.match, sc.mismatch, sc.gap_open,
-                                    sc.gap_extend, st));
-    HIPCHECK(anyseq_launch_aff_walk(d_blocks, sp.nb, dq, ds, d_pred, d_alq, d_als, st));
+    HIPCHECK(anyseq_launch_aff_pred(d_blocks, (int)blocks.size(), dq, ds, d_pred, sc.match, sc.mismatch,
+                                    sc.gap_open, sc.gap_extend, st));
+    HIPCHECK(anyseq_launch_aff_walk(d_blocks, (int)blocks.size(), dq, ds, d_pred, d_alq, d_als, st));
+    return score;
 }
 
 // Affine construct on device-resident sequences into device strings (n+m bytes);
@@ -771,27 +786,13 @@ int64_t construct_affine_dev(Engine& E, int kind, const anyseq_scoring& sc, cons
         }
         if (kind != KIND_GLOBAL || m <= 0) return empty_score(kind, n, m, sc);
     }
-    int is = 0, ie = n - 1, js = 0, je = m - 1;
-    int64_t score = 0;
-    if (kind == KIND_GLOBAL) {
-        score = n > 0 ? score_dev(E, kind, sc, dq, n, ds, m, st) : empty_score(kind, n, m, sc);
-    } else {
-        const RectPos end = aff_search(E, kind, sc, aff_problem(dq, 0, 1, n, ds, 0, 1, m),
-                                       kind == KIND_LOCAL ? 0 : 1, st);
-        score = end.v;
-        if (end.i < 0 || end.j < 0 || (kind == KIND_LOCAL && end.v <= 0)) return score;   // empty alignment
-        ie = end.i;
-        je = end.j;
-        // GLOBAL fill of the reversed prefixes anchored at the end cell
-        const RectPos start = aff_search(E, KIND_GLOBAL, sc, aff_problem(dq, ie, -1, ie + 1, ds, je, -1, je + 1),
-                                         kind == KIND_LOCAL ? 0 : 1, st);
-        if (start.v != end.v) fail("affine construct: start search found %d, end search %d", start.v, end.v);
-        is = ie - start.i;
-        js = je - start.j;
+    if (m <= MIN_PART_WIDTH_HB) {   // no Hirschberg level: the score from a (small) fill
+        const int64_t score = score_dev(E, kind, sc, dq, n, ds, m, st);
+        if (kind != KIND_GLOBAL && score <= 0) return score;
+        aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st);
+        return score;
     }
-    const int n2 = ie - is + 1, m2 = je - js + 1;
-    aff_construct_rect(E, sc, dq + is, n2, ds + js, m2, d_alq + is + js, d_als + is + js, st);
-    return score;
+    return aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st);
 }
 
 int64_t construct_affine_host(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m,

@@ -17,6 +17,7 @@ namespace anyseq {
 namespace host {
 
 constexpr int32_t SCORE_MIN_VALUE = -2147483647;  // align.impala:16
+constexpr int32_t kAffNegH = -(1 << 29);          // affine "minus infinity" (the kernels' kAffNeg)
 
 struct Failure {
     std::string msg;
@@ -85,9 +86,10 @@ struct Engine {
     std::mutex mu;
     FillCtx fc;
     DevBuf q, s, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq, als;
-    DevBuf LE, RE, typ, rowbest, pos;   // affine construct
+    DevBuf LE, RE, typ, pos;   // affine construct
     std::vector<int32_t> host_i32;
     std::vector<BlockInfo> host_blocks;
+    std::vector<PartInfo> host_parts;
     explicit Engine(int dev);
 };
 
@@ -96,6 +98,9 @@ int rows_per_lane();
 int waves_per_group();
 
 FillParams make_params(int kind, const anyseq_scoring& sc);
+// An affine problem of kind `kind` over the whole matrix (or a shard of it): its
+// border mode and clamp / best bits (DPProblem::bmode / amode).
+void set_aff_kind(DPProblem& P, int kind);
 void check_scoring(int kind, const anyseq_scoring& sc);
 
 // Enqueues one batched fill over `probs` on `st` (the problems' nbands/ngroups/

@@ -53,18 +53,28 @@ struct DPProblem {
     // direct mode) and polled against kShardSentinel.
     const uint32_t* left_flag;
     int32_t left_chunk;
-    // Affine global sub-problems of the affine construct: border
-    // mode of the top-left corner.  0: the scheme's borders; 1 (E_FREE): the path
-    // continues a horizontal gap (corner and left column -inf, top row without the
-    // open); 2 (E_PAID): the path starts with a horizontal gap that pays its open.
+    // Affine fill: border mode (BM_*) and kind bits
+    // (bit 0 the local clamp; bits 1-2 the best cell into *best, 1: every cell,
+    // 2: the last row; H space).
     int32_t bmode;
+    int32_t amode;
     uint32_t* progress;
     uint32_t* stage;       // diagnostics (ANYSEQ_SHARD_DEBUG): per-band stage reached
-    // Affine position search: (best H of the row, first column reaching it) per row.
-    int2* rowbest;
 };
 
-enum : int32_t { BM_NORMAL = 0, BM_EFREE = 1, BM_EPAID = 2 };
+// Affine border modes (H space; oracle bm_corner / bm_top / bm_left):
+//   NORMAL     the scheme's global borders (corner 0, gaps paid from it);
+//   EFREE      the path continues a horizontal gap (corner and left -inf, top
+//              row without the open);
+//   EPAID      the path starts with a horizontal gap that pays its open (corner
+//              and left -inf, top row with the open);
+//   FREE_LOCAL local: every border 0 (with the clamp, amode bit 0);
+//   FREE_SEMI  semiglobal inside the matrix: top 0, left -inf;
+//   FREE_SEMI_OPEN semiglobal at the matrix's left edge: top and left 0.
+enum : int32_t { BM_NORMAL = 0, BM_EFREE = 1, BM_EPAID = 2, BM_FREE_LOCAL = 3, BM_FREE_SEMI = 4, BM_FREE_SEMI_OPEN = 5 };
+enum : int32_t { AM_CLAMP = 1, AM_BEST_ALL = 2, AM_BEST_LAST = 4 };
+// Split boundary types of the affine construct (oracle T_*).
+enum : int32_t { T_H = 0, T_E = 1, T_BEFORE = 2, T_AFTER = 3 };
 
 // Sentinel of a not-yet-received left-border value (memset byte 0x80): no H value
 // of a supported problem reaches it.
@@ -90,7 +100,10 @@ struct PartInfo {
     int32_t len;          // rows of the part
     int32_t rhw;          // right-half width
     int32_t split_index;  // logical index into splits set by set_split_position
-    int32_t smode;        // affine construct: border mode of the part's start (left half)
+    int32_t smode;        // affine construct: border mode of the left half (the part's start)
+    int32_t emode;        // affine construct: border mode of the reversed right half (the part's end)
+    int32_t flags;        // affine construct: bit 0 free start, bit 1 free end, bit 2 empty part
+    int32_t empty_type;   // affine construct, empty part: the type its split inherits
 };
 
 // One final-level 128-column block (iteration_*:121-173).
@@ -98,8 +111,10 @@ struct BlockInfo {
     int32_t oi, h;        // rows [oi, oi+h)
     int32_t oj, w;        // cols [oj, oj+w)
     int64_t pred_base;    // byte offset of the block's anti-diagonal-major predecessor slab
-    int32_t smode;        // affine construct: start border mode (BM_NORMAL / BM_EFREE)
-    int32_t e_end;        // affine construct: the path ends in a horizontal gap (E state)
+    int32_t smode;        // affine construct: start border mode (BM_*)
+    int32_t e_end;        // affine construct: end at the bottom-right in H (0) or E (1), or free (2)
+    int32_t flags;        // affine construct: bit 0 local (free end = any cell), bit 1 holds the last column
+    int32_t xi, xj;       // affine construct, free end: the exit cell (written by aff_pred_kernel)
 };
 
 // Device-side error codes written to the error word.

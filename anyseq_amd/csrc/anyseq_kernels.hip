@@ -995,15 +995,15 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
 
 // ------------------------------------------------------------- affine fill --
 // Gotoh (build-defined: affine_scoring_scheme, align.impala:153-166, is dead in the
-// reference; semantics = oracle_affine_score in oracle/anyseq_oracle.c):
+// reference; semantics = oracle_affine_score / aff_fill in oracle/anyseq_oracle.c):
 //   E[r][c] = max(E[r][c-1] + ge, H[r][c-1] + go + ge)   (horizontal, left)
 //   F[r][c] = max(F[r-1][c] + ge, H[r-1][c] + go + ge)   (vertical, up)
-//   H[r][c] = max(H[r-1][c-1] + sub, E, F)               (local: max(., 0))
-// All kinds run in G-space, X_G = X - (r+c+2)*ge for X in {H,E,F}: every gap
+//   H[r][c] = max(H[r-1][c-1] + sub, E, F)               (clamped: max(., 0))
+// All problems run in G-space, X_G = X - (r+c+2)*ge for X in {H,E,F}: every gap
 // extension is free there, so
 //   E_G = max(E_G, G_left + go),  F_G = max(F_G, G_up + go),
 //   G   = max3(G_diag + sub - 2 ge, E_G, F_G),
-// and local's clamp H >= 0 becomes G >= Z_t = (r+c+2)(-ge), which is the SAME for
+// and the local clamp H >= 0 becomes G >= Z_t = (r+c+2)(-ge), which is the SAME for
 // every lane of a step (r + c = rb + t - 1 on the anti-diagonal): one v_max with a
 // wave-uniform bound.  Same geometry as fill_kernel (R = 1, X = 0, CH = 32): lane l
 // owns row rb + l of a 64-row band and processes column t - 1 - l at step t.  From
@@ -1011,6 +1011,15 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
 // diagonal) and F[r][c] ("F-down" of the row above); lane 0 reads both from the
 // band's input ring (int2 per column).  G + go is computed once per cell and
 // serves both the F-down of this cell and the E of the next column.
+//
+// The kind of a problem is runtime data, so ONE launch can mix the sub-problems of
+// a Hirschberg level whose ends are anchored or free:
+//   DPProblem::bmode  borders (BM_*: the scheme corner / a continuing or paid gap /
+//                     free local / free semiglobal borders),
+//   DPProblem::amode  bit 0 the local clamp, bits 1-2 the best-cell output into
+//                     *best (1: every cell, 2: the last row), H space.
+// Problems with amode 0 run the plain steady-state loop (11 VALU per step), the
+// others the clamp + best loop (14).
 constexpr int kAffNeg = -(1 << 29);   // "minus infinity" of the E/F states (the oracle's AFF_NEG_INF)
 
 struct AffK {
@@ -1020,12 +1029,23 @@ struct AffK {
     int flags;    // bit 0: no asm steady state (diagnostics)
 };
 
-// Border cell G[-1][i] / G[i][-1], i >= -1 (G space).
-template <int KIND>
-__device__ __forceinline__ int aff_border(int i, int go, int nge) {
-    if (KIND == KIND_GLOBAL) return i < 0 ? 0 : go;
-    return (i + 1) * nge;   // semiglobal / local: H border 0
-}
+// Borders of a problem in G space (H border values by border mode, see
+// bm_corner / bm_top / bm_left in oracle/anyseq_oracle.c):
+//   corner G[-1][-1] = cg;  top G[-1][c] = tfree ? (c+1)(-ge) : tg;  left likewise.
+struct AffBorder {
+    int cg, tg, lg;
+    bool tfree, lfree;
+    __device__ AffBorder(int bm, int go) {
+        const bool neg_corner = bm == BM_EFREE || bm == BM_EPAID;
+        cg = neg_corner ? kAffNeg : 0;
+        tfree = bm >= BM_FREE_LOCAL;
+        tg = bm == BM_EFREE ? 0 : go;
+        lfree = bm == BM_FREE_LOCAL || bm == BM_FREE_SEMI_OPEN;
+        lg = bm == BM_NORMAL ? go : kAffNeg;
+    }
+    __device__ int top(int c, int nge) const { return c < 0 ? cg : (tfree ? (c + 1) * nge : tg); }
+    __device__ int left(int r, int nge) const { return r < 0 ? cg : (lfree ? (r + 1) * nge : lg); }
+};
 __device__ __forceinline__ int aff_to_h(int v, int r, int c, int nge) { return v - (r + c + 2) * nge; }
 
 template <int NW>
@@ -1057,15 +1077,16 @@ struct AffIO {
 
 // 32 steps in C++ (prologue / epilogue / partial bands; the steady state is the asm
 // loop below).  c0 = this lane's column at the first step, tf = top row at column
-// t0 - 1, rv[u] = top row at column t0 + u, z = local clamp bound of the first step.
+// t0 - 1, rv[u] = top row at column t0 + u, zc / zb = clamp bound / true Z_t of the
+// first step (zc is far below zb when the problem does not clamp).
 // MASK: some lanes are outside [0, w).  PARTIAL: rows >= h pass the row above
 // through.  FINOUT: the problem's last row publishes F[h-1][c] (not F-down), as
 // the two-front combine needs.  og/of: this lane's (G, F-out) after each step
 // (lane 63's are the band's bottom row).
-template <int KIND, bool MASK, bool PARTIAL, bool FINOUT, bool VIRT, bool TRACK = false>
+template <bool MASK, bool PARTIAL, bool FINOUT, bool VIRT>
 __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&rv)[32], const uint32_t (&sw)[8], int q,
-                                          bool dead, bool lastrow, int z, int& g, int& e, int& hg, int& fdn, int& dg,
-                                          int& best, int (&og)[32], int (&of)[32], const AffK k, int* bcol = nullptr) {
+                                          bool dead, bool lastrow, int zc, int zb, int& g, int& e, int& hg, int& fdn,
+                                          int& dg, int& best, int (&og)[32], int (&of)[32], const AffK k) {
 #pragma unroll
     for (int u = 0; u < 32; ++u) {
         const int2 top = u == 0 ? tf : rv[u - 1];
@@ -1075,7 +1096,7 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
         const int wgt = q == sb ? k.wm : k.wx;
         const int en = max(e, hg);
         int v = max(max(dg + wgt, en), fin);
-        if (KIND == KIND_LOCAL) v = max(v, z + u * k.nge);
+        v = max(v, zc + u * k.nge);
         const int hn = v + k.go;
         int fn = max(fin, hn);
         if (PARTIAL && dead) {
@@ -1090,16 +1111,7 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
         g = act ? v : g;
         hg = act ? hn : hg;
         fdn = act ? fn : fdn;
-        if (TRACK) {
-            // row-major first maximum: this lane's row, first column reaching its best H
-            const int hv = v - (z + u * k.nge);
-            if (act && !dead && (unsigned)(c0 + u) < (unsigned)w && hv > best) {
-                best = hv;
-                *bcol = c0 + u;
-            }
-        } else if (KIND == KIND_LOCAL) {
-            best = act ? max(best, v - (z + u * k.nge)) : best;
-        }
+        best = act ? max(best, v - (zb + u * k.nge)) : best;
         dg = upg;
         og[u] = g;
         of[u] = fdn;
@@ -1115,18 +1127,19 @@ struct AffLoopArgs {
 #define AFF_ASM(NAME)                                                                                           \
     asm volatile(NAME                                                                                          \
                  : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
-                   [hg] "+v"(hg), [best] "+v"(best), [z] "+s"(z), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf),      \
-                   [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3), \
-                   [x4] "=&s"(x4)                                                                              \
+                   [hg] "+v"(hg), [best] "+v"(best), [z] "+s"(z), [zb] "+s"(zb), [b] "+s"(b), [sp] "+s"(sp),     \
+                   [sf] "+s"(sf), [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), \
+                   [x3] "=&s"(x3), [x4] "=&s"(x4)                                                              \
                  : [be] "s"(be), [q] "v"(q), [wm] "v"(k.wm), [wx] "v"(k.wx), [go] "v"(k.go), [nge] "s"(nge),     \
                    [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp),          \
                    [anc] "v"(la.anc), [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo),  \
                    [lid8] "v"(la.lid8), [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp)            \
                  : ANYSEQ_AFF_ASM_CLOBBERS, "memory")
-template <int KIND, bool BORDER, int PUB>
+// L: the clamp + best loop (any amode != 0), else the plain loop.
+template <bool L, bool BORDER, int PUB>
 __device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                  const AffLoopArgs& la, int q, int& g, int& fdn, int& dg, int2& tf,
-                                                 int& e, int& hg, int& best, uint32_t& z, const AffK& k) {
+                                                 int& e, int& hg, int& best, uint32_t& z, uint32_t& zb, const AffK& k) {
     uint32_t st, x0, x1, x2, x3, x4;
     const uint64_t hm = 0xffffffff00000000ull;
 #define RFL(x) __builtin_amdgcn_readfirstlane(x)
@@ -1136,11 +1149,12 @@ __device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint3
     sc = RFL(sc);
     be = RFL(be);
     z = RFL(z);
+    zb = RFL(zb);
     const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), nge = RFL(k.nge);
     const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
 #undef RFL
     int tfg = tf.x, tff = tf.y;
-    if constexpr (KIND == KIND_LOCAL) {
+    if constexpr (L) {
         if constexpr (BORDER && PUB == 0) AFF_ASM(ANYSEQ_AFF_L_B1_NONE);
         if constexpr (BORDER && PUB == 1) AFF_ASM(ANYSEQ_AFF_L_B1_LDS);
         if constexpr (BORDER && PUB == 2) AFF_ASM(ANYSEQ_AFF_L_B1_GLOB);
@@ -1160,32 +1174,29 @@ __device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint3
 }
 #undef AFF_ASM
 
-template <int KIND, bool PARTIAL, bool FINOUT, bool TRACK = false>
+template <bool PARTIAL, bool FINOUT>
 __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k) {
     constexpr int CH = 32;
     constexpr int IRM = kSlots * CH - 1;
     constexpr int LAG = 2;   // lane 63 finishes column c at step c + 64: chunk j is complete after block j + 2
-    // VIRT (global): lanes left of column 0 compute virtual cells from "minus
-    // infinity" states; lane 0's top value at column -1 is (G[rb-1][-1], go), so
-    // column -1 computes G = F = go, the left border, and E at column 0 = 2 go, as
-    // the oracle's.  The prologue then runs in the asm loop.  Semiglobal / local
-    // borders grow with the row and keep the masked C++ prologue.
-    constexpr bool VIRT = KIND == KIND_GLOBAL && !PARTIAL && !FINOUT;
-    constexpr bool ASM = !PARTIAL && !FINOUT && !TRACK;
     const int h = P.h, w = P.w, go = k.go, nge = k.nge;
+    const int bm = __builtin_amdgcn_readfirstlane(P.bmode);
+    const int amode = __builtin_amdgcn_readfirstlane(P.amode);
+    const bool clamp = amode & 1;
+    const int bestmode = (amode >> 1) & 3;
+    const AffBorder B(bm, go);
     // column-block shard: the left border column (H and E of column
     // -1, H space, sender's frame + left_shift) arrives from the neighbour shard;
     // such a band runs the masked prologue on the received values
     const bool shard_left = P.left_in != nullptr;
-    const bool virt = VIRT && !shard_left;
-    // border values (G space): corner, top row (c >= 0), left column (r >= 0); the
-    // affine construct's global sub-problems change them by border mode (bmode)
-    const int bm = KIND == KIND_GLOBAL ? P.bmode : BM_NORMAL;
-    const int cg = bm == BM_NORMAL ? 0 : kAffNeg;
-    const int tg = bm == BM_EFREE ? 0 : go;
-    const int lg = bm == BM_NORMAL ? go : kAffNeg;
-    auto topv = [&](int c) { return KIND == KIND_GLOBAL ? (c < 0 ? cg : tg) : aff_border<KIND>(c, go, nge); };
-    auto leftv = [&](int r) { return KIND == KIND_GLOBAL ? (r < 0 ? cg : lg) : aff_border<KIND>(r, go, nge); };
+    // VIRT (the scheme's borders): lanes left of column 0 compute virtual cells from
+    // "minus infinity" states; lane 0's top value at column -1 is (G[rb-1][-1], go),
+    // so column -1 computes G = F = go, the left border, and E at column 0 = 2 go, as
+    // the oracle's.  The prologue then runs in the asm loop.  Other borders keep the
+    // masked C++ prologue.
+    constexpr bool VIRT_OK = !PARTIAL && !FINOUT;
+    // (not with a best-cell output: the virtual border column would count as a cell)
+    const bool virt = VIRT_OK && bm == BM_NORMAL && !shard_left && !(amode & (AM_BEST_ALL | AM_BEST_LAST));
     const int rb = band * 64;
     const int row = rb + lane;
     const bool dead = row >= h;
@@ -1200,32 +1211,33 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         int32_t lh1 = 0, lh0 = 0, le1 = 0;
         if (!poll_left(P, row, lh1, lh0, err)) return;
         if (!poll_left_e(P, row, le1, err)) return;
-        // H space -> G space at column -1: G = H + (r + 1) (-ge); row -1 is the corner,
-        // the scheme's border in every shard frame (global: go, else 0)
+        // H space -> G space at column -1: G = H + (r + 1) (-ge); row -1 is the top
+        // border of the shard frame (the scheme's: global go, free 0)
         g = lh1 + (row + 1) * nge;
         e = le1 + (row + 1) * nge;
         hg = g + go;
-        dg = row == 0 ? (KIND == KIND_GLOBAL ? go : 0) : lh0 + row * nge;
+        dg = row == 0 ? (bm == BM_NORMAL ? go : 0) : lh0 + row * nge;
         tf = make_int2(__shfl(dg, 0), kAffNeg);
     } else if (virt) {
         g = kAffNeg;
         hg = kAffNeg;
         dg = kAffNeg;
-        tf = make_int2(leftv(rb - 1), rb == 0 ? cg + go : lg);
+        tf = make_int2(B.left(rb - 1, nge), rb == 0 ? B.cg + go : B.lg);
     } else {
-        g = leftv(row);
+        g = B.left(row, nge);
         hg = g + go;   // the next column's E candidate: G[r][-1] + go
-        dg = leftv(row - 1);
-        tf = make_int2(leftv(rb - 1), kAffNeg);
+        dg = B.left(row - 1, nge);
+        tf = make_int2(B.left(rb - 1, nge), kAffNeg);
     }
-    int best = TRACK ? -2147483647 : 0;
-    int bcol = -1;
+    int best = kAffNeg;
     const int nchunks = (w + CH - 1) / CH;
     const int nblocks = nchunks + LAG;
     const int fe = w >= CH - 1 ? (w - (CH - 1)) / CH + 1 : 0;   // full blocks: 32b + 30 < w
     uint32_t seen_prod = 0, seen_sfill = 0, seen_cons = 0;
+    // clamp bound far below any cell when the problem does not clamp
+    const int zoff = clamp ? 0 : 2 * kAffNeg;
     AffLoopArgs la;
-    if constexpr (ASM) {
+    if constexpr (VIRT_OK) {
         la.rb = lds_addr(io.my_ring);
         la.nb = io.out_lds ? lds_addr(io.next_ring) : 0u;
         la.apr = lds_addr(io.my_prod);
@@ -1237,28 +1249,40 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         la.skb = lds_addr(io.skew) + 4u * lane;
         la.lo = 8u * (lane - 32);
         la.lid8 = 8u * lane;
-        la.bvb = (uint32_t)topv(lane);
-        la.bvs = (uint32_t)(topv(1) - topv(0));
+        la.bvb = (uint32_t)B.top(lane, nge);
+        la.bvs = (uint32_t)(B.top(1, nge) - B.top(0, nge));
         la.gp = (uint64_t)(size_t)io.gout;
     }
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
-        if constexpr (ASM) {
+        if constexpr (VIRT_OK) {
             if ((virt || t0 >= 64) && b < fe && !(k.flags & 1)) {
                 uint32_t bb = (uint32_t)b;
-                uint32_t z = (uint32_t)((rb + t0 + 1) * nge);
+                uint32_t zb = (uint32_t)((rb + t0 + 1) * nge);
+                uint32_t z = zb + (uint32_t)zoff;
                 const int role = (io.in_border ? 3 : 0) + (io.out_lds ? 1 : (io.gout ? 2 : 0));
                 uint32_t st = 0;
-#define AF_CALL(BD, PB)                                                                                    \
-    st = aff_loop_asm<KIND, BD, PB>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, q, g, fdn, dg, tf, e, \
-                                    hg, best, z, k)
-                switch (role) {
-                    case 0: AF_CALL(false, 0); break;
-                    case 1: AF_CALL(false, 1); break;
-                    case 2: AF_CALL(false, 2); break;
-                    case 3: AF_CALL(true, 0); break;
-                    case 4: AF_CALL(true, 1); break;
-                    default: AF_CALL(true, 2); break;
+#define AF_CALL(LV, BD, PB)                                                                                    \
+    st = aff_loop_asm<LV, BD, PB>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, q, g, fdn, dg, tf, e, \
+                                  hg, best, z, zb, k)
+                if (amode) {
+                    switch (role) {
+                        case 0: AF_CALL(true, false, 0); break;
+                        case 1: AF_CALL(true, false, 1); break;
+                        case 2: AF_CALL(true, false, 2); break;
+                        case 3: AF_CALL(true, true, 0); break;
+                        case 4: AF_CALL(true, true, 1); break;
+                        default: AF_CALL(true, true, 2); break;
+                    }
+                } else {
+                    switch (role) {
+                        case 0: AF_CALL(false, false, 0); break;
+                        case 1: AF_CALL(false, false, 1); break;
+                        case 2: AF_CALL(false, false, 2); break;
+                        case 3: AF_CALL(false, true, 0); break;
+                        case 4: AF_CALL(false, true, 1); break;
+                        default: AF_CALL(false, true, 2); break;
+                    }
                 }
 #undef AF_CALL
                 if (st) {
@@ -1277,7 +1301,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         int2 rv[CH];
         if (b < nchunks) {
             if (io.in_border) {
-                const int bv = topv(t0 + lane);
+                const int bv = B.top(t0 + lane, nge);
                 io.my_ring[(t0 + lane) & IRM] = make_int2(bv, bv + go);
             } else if (seen_prod < (uint32_t)(b + 1)) {
                 if (!(seen_prod = spin_lds_ge(io.my_prod, (uint32_t)(b + 1), err))) return;
@@ -1303,20 +1327,23 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         }
         int og[CH], of[CH];
         const int c0 = t0 - 1 - lane;
-        const int z = (rb + t0 + 1) * nge;
+        const int zb = (rb + t0 + 1) * nge;
+        const int zc = zb + zoff;
         const bool full = (virt || t0 >= 64) && b < fe;
-        if (TRACK)
-            aff_block<KIND, true, PARTIAL, FINOUT, VIRT, true>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg,
-                                                               best, og, of, k, &bcol);
-        else if (full)
-            aff_block<KIND, false, PARTIAL, FINOUT, VIRT>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg, best,
-                                                    og, of, k);
-        else if (VIRT && shard_left)   // a shard's prologue: real border column, no virtual lanes
-            aff_block<KIND, true, PARTIAL, FINOUT, false>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg,
+        if (full) {
+            if (virt)
+                aff_block<false, PARTIAL, FINOUT, true>(c0, w, tf, rv, sw, q, dead, lastrow, zc, zb, g, e, hg, fdn,
+                                                        dg, best, og, of, k);
+            else
+                aff_block<false, PARTIAL, FINOUT, false>(c0, w, tf, rv, sw, q, dead, lastrow, zc, zb, g, e, hg, fdn,
+                                                         dg, best, og, of, k);
+        } else if (virt) {
+            aff_block<true, PARTIAL, FINOUT, true>(c0, w, tf, rv, sw, q, dead, lastrow, zc, zb, g, e, hg, fdn, dg,
+                                                   best, og, of, k);
+        } else {   // masked prologue / epilogue (also a shard's received border column)
+            aff_block<true, PARTIAL, FINOUT, false>(c0, w, tf, rv, sw, q, dead, lastrow, zc, zb, g, e, hg, fdn, dg,
                                                     best, og, of, k);
-        else
-            aff_block<KIND, true, PARTIAL, FINOUT, VIRT>(c0, w, tf, rv, sw, q, dead, lastrow, z, g, e, hg, fdn, dg, best,
-                                                   og, of, k);
+        }
         tf = rv[CH - 1];
         if (pub && lane == 63) {
             int4* dst = reinterpret_cast<int4*>(io.next_ring + ((j * CH) & IRM));
@@ -1354,17 +1381,18 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         if (P.out_col_e) gmem(P.out_col_e)[row] = aff_to_h(e, row, w - 1, nge);
         // shard: F of the last row at the last column (the combine pairs it across shards)
         if (lastrow && P.out_f_last) *gmem(P.out_f_last) = aff_to_h(fdn, row, w - 1, nge);
-        if (TRACK) P.rowbest[row] = make_int2(best, bcol);
     }
     if (P.progress && !publish_progress(P, band, lane, err)) return;
-    if (KIND == KIND_LOCAL && P.best && !TRACK) {
+    if (bestmode && P.best) {
+        // the lane's best covers its row; last-row mode keeps the problem's last row only
+        if (dead || (bestmode == 2 && !lastrow)) best = kAffNeg;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
         if (lane == 0) atomicMax(P.best, best);
     }
 }
 
-template <int KIND, int NW>
+template <int NW>
 __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProblem* __restrict__ probs,
                                                                      const GroupRef* __restrict__ groups,
                                                                      int ngroups_total, uint32_t* dq, uint32_t* err,
@@ -1425,15 +1453,12 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                 io.gout = band < last ? nullptr : g_out;
                 const bool partial = (band + 1) * 64 > P.h;
                 const bool finout = band == P.nbands - 1 && P.out_row != nullptr;
-                if (KIND != KIND_SEMIGLOBAL && P.rowbest) {   // position search (no out_row)
-                    if (partial) run_band_aff<KIND, true, false, true>(P, band, lane, io, err, k);
-                    else run_band_aff<KIND, false, false, true>(P, band, lane, io, err, k);
-                } else if (partial) {
-                    if (finout) run_band_aff<KIND, true, true>(P, band, lane, io, err, k);
-                    else run_band_aff<KIND, true, false>(P, band, lane, io, err, k);
+                if (partial) {
+                    if (finout) run_band_aff<true, true>(P, band, lane, io, err, k);
+                    else run_band_aff<true, false>(P, band, lane, io, err, k);
                 } else {
-                    if (finout) run_band_aff<KIND, false, true>(P, band, lane, io, err, k);
-                    else run_band_aff<KIND, false, false>(P, band, lane, io, err, k);
+                    if (finout) run_band_aff<false, true>(P, band, lane, io, err, k);
+                    else run_band_aff<false, false>(P, band, lane, io, err, k);
                 }
             }
         }
@@ -1874,120 +1899,67 @@ __global__ void fulltb_walk_kernel(const uint8_t* __restrict__ Q, int n, const u
 
 // ======================================================= affine construct --
 // Build-defined linear-space affine alignment (semantics =
-// oracle_affine_construct in oracle/anyseq_oracle.c).
+// oracle_affine_construct in oracle/anyseq_oracle.c): one column-split Hirschberg
+// over the whole matrix whose parts may have free starts / ends.
 
-// Position scans.  Rows' (best H, first column) of a TRACK fill -> the row-major
-// first maximum: out = {value, row, col}.
-__global__ __launch_bounds__(1024) void aff_rowbest_kernel(const int2* __restrict__ rb, int h, int32_t* out) {
-    __shared__ int sv[1024], sr[1024];
-    int best = -2147483647, row = 0x7fffffff;
-    for (int r = threadIdx.x; r < h; r += blockDim.x)
-        if (rb[r].x > best) {
-            best = rb[r].x;
-            row = r;
-        }
-    sv[threadIdx.x] = best;
-    sr[threadIdx.x] = row;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            const int v2 = sv[threadIdx.x + o], r2 = sr[threadIdx.x + o];
-            if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && r2 < sr[threadIdx.x])) {
-                sv[threadIdx.x] = v2;
-                sr[threadIdx.x] = r2;
-            }
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        out[0] = sv[0];
-        out[1] = sr[0];
-        out[2] = sr[0] < h ? rb[sr[0]].y : -1;
-    }
+// H-space top border of a half at column c (oracle bm_top).
+__device__ __forceinline__ int aff_top_h(int bm, int c, int go, int ge) {
+    if (bm == BM_NORMAL || bm == BM_EPAID) return go + (c + 1) * ge;
+    if (bm == BM_EFREE) return (c + 1) * ge;
+    return 0;
 }
 
-// First maximum of a sequence with index -1 = `border` and indices 0..n-1 = the
-// values (a raw (G, F) row converted to H at row `r`, or an H column).
-__device__ void first_max(bool raw, const int2* row, const int32_t* col, int n, int r, int nge, int border, int& bv,
-                          int& bi, int* sv, int* si) {
-    int best = border, idx = -1;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        const int v = raw ? row[j].x - (r + j + 2) * nge : col[j];
-        if (v > best) {
-            best = v;
-            idx = j;
-        }
-    }
-    sv[threadIdx.x] = best;
-    si[threadIdx.x] = idx;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            const int v2 = sv[threadIdx.x + o], i2 = si[threadIdx.x + o];
-            if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && i2 < si[threadIdx.x])) {
-                sv[threadIdx.x] = v2;
-                si[threadIdx.x] = i2;
-            }
-        }
-        __syncthreads();
-    }
-    bv = sv[0];
-    bi = si[0];
-    __syncthreads();
-}
-
-// Semiglobal end / start search: first max of the last row (index -1 = rborder),
-// then of the last column (index -1 = cborder) only if strictly greater.
-// out = {value, row, col} of the cell (row h-1 / column w-1 for the row / column).
-__global__ __launch_bounds__(1024) void aff_edge_scan_kernel(const int2* __restrict__ row, int w,
-                                                             const int32_t* __restrict__ col, int h, int nge,
-                                                             int rborder, int cborder, int32_t* out) {
-    __shared__ int sv[1024], si[1024];
-    int rv, ri, cv, ci;
-    first_max(true, row, nullptr, w, h - 1, nge, rborder, rv, ri, sv, si);
-    first_max(false, nullptr, col, h, 0, nge, cborder, cv, ci, sv, si);
-    if (threadIdx.x == 0) {
-        if (cv > rv) {
-            out[0] = cv;
-            out[1] = ci;
-            out[2] = w - 1;
-        } else {
-            out[0] = rv;
-            out[1] = h - 1;
-            out[2] = ri;
-        }
-    }
-}
-
-// Hirschberg join of one part per workgroup: rows i = -1 .. len-1 ascending, H
-// join before E join, strict > (first maximum):
-//     HL(i) + HR(len-i-2),   EL(i) + ER(len-i-2) - go
+// Hirschberg join of one part per workgroup, the first maximum (strict >) in the
+// candidate order
+//     BEFORE (free end: best end cell of the left half, pbest[2p]),
+//     AFTER (free start: best start cell of the right half, pbest[2p+1]),
+//     rows i = -1 .. len-1: HL(i) + HR(len-i-2), then EL(i) + ER(len-i-2) - go
 // (L = forward left half's last column, R = reversed right half's; index -1 =
-// the half's top border, a horizontal gap).  Writes the split row and its
-// crossing state (0 = H, 1 = E) at the part's split index.
+// the half's top border: a gap when anchored, no gap when free).  Writes the split
+// row and its type (T_*) at the part's split index; an empty part passes its type
+// on.  score: the value of part 0 (level 1: the optimal score).
 __global__ __launch_bounds__(256) void aff_hb_join_kernel(const PartInfo* __restrict__ parts, int half,
                                                           const int32_t* __restrict__ LH, const int32_t* __restrict__ LE,
                                                           const int32_t* __restrict__ RH,
-                                                          const int32_t* __restrict__ RE, int go, int ge,
-                                                          int32_t* splits, int32_t* types) {
+                                                          const int32_t* __restrict__ RE,
+                                                          const int32_t* __restrict__ pbest, int go, int ge,
+                                                          int32_t* splits, int32_t* types, int32_t* score) {
     __shared__ int sv[256], sk[256];
     const PartInfo pi = parts[blockIdx.x];
     const int off = pi.off, len = pi.len;
-    const int bL = (pi.smode == BM_EFREE ? 0 : go) + half * ge;
-    const int bR = go + pi.rhw * ge;
-    int best = -2147483647, key = 0x7fffffff;   // key = 2 (i + 1) + type: the candidate order
+    if (pi.flags & 4) {
+        if (threadIdx.x == 0) {
+            splits[pi.split_index + 1] = off;
+            types[pi.split_index + 1] = pi.empty_type;
+        }
+        return;
+    }
+    const bool sfree = pi.flags & 1, efree = pi.flags & 2;
+    const int bLH = aff_top_h(pi.smode, half - 1, go, ge), bLE = sfree ? kAffNeg : bLH;
+    const int bRH = aff_top_h(pi.emode, pi.rhw - 1, go, ge), bRE = efree ? kAffNeg : bRH;
+    int best = -2147483647, key = 0x7fffffff;   // key: 0 BEFORE, 1 AFTER, 2 + 2 (i + 1) + type
+    if (threadIdx.x == 0) {
+        if (efree && pbest[2 * blockIdx.x] > best) {
+            best = pbest[2 * blockIdx.x];
+            key = 0;
+        }
+        if (sfree && pbest[2 * blockIdx.x + 1] > best) {
+            best = pbest[2 * blockIdx.x + 1];
+            key = 1;
+        }
+    }
     for (int i = (int)threadIdx.x - 1; i < len; i += blockDim.x) {
         const int k = len - i - 2;
-        const int hl = i < 0 ? bL : LH[off + i], el = i < 0 ? bL : LE[off + i];
-        const int hr = k < 0 ? bR : RH[off + k], er = k < 0 ? bR : RE[off + k];
+        const int hl = i < 0 ? bLH : LH[off + i], el = i < 0 ? bLE : LE[off + i];
+        const int hr = k < 0 ? bRH : RH[off + k], er = k < 0 ? bRE : RE[off + k];
         const int vh = hl + hr, ve = el + er - go;
         if (vh > best) {
             best = vh;
-            key = 2 * (i + 1);
+            key = 2 + 2 * (i + 1);
         }
         if (ve > best) {
             best = ve;
-            key = 2 * (i + 1) + 1;
+            key = 3 + 2 * (i + 1);
         }
     }
     sv[threadIdx.x] = best;
@@ -2004,17 +1976,33 @@ __global__ __launch_bounds__(256) void aff_hb_join_kernel(const PartInfo* __rest
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        const int idx = sk[0] / 2 - 1;
-        splits[pi.split_index + 1] = off + idx + 1;
-        types[pi.split_index + 1] = sk[0] & 1;
+        const int kk = sk[0];
+        int type, spl;
+        if (kk == 0) {
+            type = T_BEFORE;
+            spl = off + len;
+        } else if (kk == 1) {
+            type = T_AFTER;
+            spl = off;
+        } else {
+            type = (kk & 1) ? T_E : T_H;
+            spl = off + (kk - 2) / 2;   // off + idx + 1
+        }
+        splits[pi.split_index + 1] = spl;
+        types[pi.split_index + 1] = type;
+        if (score && blockIdx.x == 0) *score = sv[0];
     }
 }
 
 // Final level: Gotoh with predecessor bytes for one 128-column block per wave,
 // the geometry of pred_kernel (lane l owns columns 2l, 2l+1, anti-diagonal
 // sweep, byte pred[base + (i+j)*128 + j]).  Byte: bits 0-1 H source (0 diag,
-// 1 E, 2 F), bit 2 E extends, bit 3 F extends.
-__global__ __launch_bounds__(64) void aff_pred_kernel(const BlockInfo* __restrict__ blocks, int nblocks,
+// 1 E, 2 F, 3 clamped), bit 2 E extends, bit 3 F extends.  Borders by the start
+// mode (the local clamp for BM_FREE_LOCAL).  A free end (e_end 2) also finds the
+// exit cell: local, the first maximum of all cells in row-major order;
+// semiglobal, the first maximum of the last row, then of the last column (when
+// the block holds it) if strictly greater -> blocks[b].xi / xj.
+__global__ __launch_bounds__(64) void aff_pred_kernel(BlockInfo* __restrict__ blocks, int nblocks,
                                                       const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
                                                       uint8_t* __restrict__ pred, int match, int mismatch, int go,
                                                       int ge) {
@@ -2024,10 +2012,16 @@ __global__ __launch_bounds__(64) void aff_pred_kernel(const BlockInfo* __restric
     if (bi.h <= 0) return;
     const int lane = threadIdx.x;
     const int NEG = kAffNeg;
-    const int C = bi.smode == BM_NORMAL ? 0 : NEG;
-    const int T0 = bi.smode == BM_EFREE ? 0 : go;
-    auto top = [&](int j) { return j < 0 ? C : T0 + (j + 1) * ge; };
-    auto left = [&](int i) { return i < 0 ? C : (bi.smode == BM_NORMAL ? go + (i + 1) * ge : NEG); };
+    const int bm = bi.smode;
+    const bool clamp = bm == BM_FREE_LOCAL;
+    const int C = (bm == BM_EFREE || bm == BM_EPAID) ? NEG : 0;
+    auto top = [&](int j) { return j < 0 ? C : aff_top_h(bm, j, go, ge); };
+    auto left = [&](int i) {
+        if (i < 0) return C;
+        if (bm == BM_NORMAL) return go + (i + 1) * ge;
+        return (bm == BM_FREE_LOCAL || bm == BM_FREE_SEMI_OPEN) ? 0 : NEG;
+    };
+    const bool xfree = bi.e_end == 2, xlocal = bi.flags & 1, xlastcol = bi.flags & 2;
     const int jA = 2 * lane, jB = 2 * lane + 1;
     const int sA = jA < bi.w ? (int)S[bi.oj + jA] : 0x100;
     const int sB = jB < bi.w ? (int)S[bi.oj + jB] : 0x100;
@@ -2035,6 +2029,9 @@ __global__ __launch_bounds__(64) void aff_pred_kernel(const BlockInfo* __restric
     int HB = top(jB), FB = NEG, EB = NEG;
     int HAo = top(jA);                       // A one step earlier: B's diagonal
     int dA = left(-1);                       // A's diagonal (lane 0: the left border)
+    // exit candidates: per column the first row reaching its best (local), the last
+    // row's value (semiglobal), the last column's first maximum (semiglobal)
+    int xvA = -2147483647, xrA = 0, xvB = -2147483647, xrB = 0, cv = -2147483647, cr = 0;
     uint16_t* out16 = reinterpret_cast<uint16_t*>(pred + bi.pred_base);
     const int nsteps = bi.h + 127;
     for (int d = 0; d < nsteps; ++d) {
@@ -2061,6 +2058,7 @@ __global__ __launch_bounds__(64) void aff_pred_kernel(const BlockInfo* __restric
         int hB = HAo + (qB == sB ? match : mismatch);
         if (eB > hB) { hB = eB; pB = (pB & ~3) | 1; }
         if (fB > hB) { hB = fB; pB = (pB & ~3) | 2; }
+        if (clamp && 0 > hB) { hB = 0; pB |= 3; }
         // A
         int pA = 0;
         int eA;
@@ -2076,51 +2074,105 @@ __global__ __launch_bounds__(64) void aff_pred_kernel(const BlockInfo* __restric
         int hA = dA + (qA == sA ? match : mismatch);
         if (eA > hA) { hA = eA; pA = (pA & ~3) | 1; }
         if (fA > hA) { hA = fA; pA = (pA & ~3) | 2; }
+        if (clamp && 0 > hA) { hA = 0; pA |= 3; }
         dA = lH;   // next step's diagonal of A: lane l-1's B at row iA
         if (actB) {
             HB = hB;
             FB = fB;
             EB = eB;
+            if (xfree) {
+                if (xlocal) {
+                    if (hB > xvB) { xvB = hB; xrB = iB; }
+                } else {
+                    if (iB == bi.h - 1) xvB = hB;
+                    if (xlastcol && jB == bi.w - 1 && hB > cv) { cv = hB; cr = iB; }
+                }
+            }
         }
         HAo = HA;
         if (actA) {
             HA = hA;
             FA = fA;
             EA = eA;
+            if (xfree) {
+                if (xlocal) {
+                    if (hA > xvA) { xvA = hA; xrA = iA; }
+                } else {
+                    if (iA == bi.h - 1) xvA = hA;
+                    if (xlastcol && jA == bi.w - 1 && hA > cv) { cv = hA; cr = iA; }
+                }
+            }
         }
         const uint16_t pk = (uint16_t)((actA ? pA : 0) | ((actB ? pB : 0) << 8));
         out16[(size_t)d * 64 + lane] = pk;
     }
+    if (xfree) {
+        // best (value, row, column) of the lane: A before B (same row: smaller column)
+        int v = xvA, r = xlocal ? xrA : bi.h - 1, c = jA;
+        if (xvB > v || (xvB == v && xlocal && xrB < r)) {
+            v = xvB;
+            r = xlocal ? xrB : bi.h - 1;
+            c = jB;
+        }
+        if (jA >= bi.w) v = -2147483647;
+        // first maximum over lanes: larger value, then smaller row, then smaller column
+        for (int o = 32; o >= 1; o >>= 1) {
+            const int v2 = __shfl_xor(v, o), r2 = __shfl_xor(r, o), c2 = __shfl_xor(c, o);
+            if (v2 > v || (v2 == v && (r2 < r || (r2 == r && c2 < c)))) {
+                v = v2;
+                r = r2;
+                c = c2;
+            }
+        }
+        if (!xlocal && xlastcol) {   // the last column's first maximum, if strictly greater
+            const int owner = (bi.w - 1) >> 1;
+            const int cv0 = __shfl(cv, owner), cr0 = __shfl(cr, owner);
+            if (cv0 > v) {
+                v = cv0;
+                r = cr0;
+                c = bi.w - 1;
+            }
+        }
+        if (lane == 0) {
+            blocks[b].xi = r;
+            blocks[b].xj = c;
+        }
+    }
 }
 
-// One thread per block: walk from the block's end (state H, or E after an E
-// crossing) to its start; borders are gap runs; sparse i+j+1 output.
+// One thread per block: walk from the block's end (bottom-right in state H or E,
+// or the free exit cell) back to its start (anchored: the corner through the
+// border's gap runs; free: a clamped cell or the border); sparse i+j+1 output.
 __global__ void aff_walk_kernel(const BlockInfo* __restrict__ blocks, int nblocks, const uint8_t* __restrict__ Q,
                                 const uint8_t* __restrict__ S, const uint8_t* __restrict__ pred, uint8_t* alq,
                                 uint8_t* als) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nblocks) return;
     const BlockInfo bi = blocks[b];
+    if (bi.e_end == 2 && bi.h <= 0) return;   // the path ended at the block's corner
+    const bool free_start = bi.smode >= BM_FREE_LOCAL;
     const int64_t base = (int64_t)bi.oi + bi.oj;
-    int i = bi.h - 1, j = bi.w - 1;
-    int st = bi.e_end ? 1 : 0;
+    int i = bi.e_end == 2 ? bi.xi : bi.h - 1, j = bi.e_end == 2 ? bi.xj : bi.w - 1;
+    int st = bi.e_end == 1 ? 1 : 0;
     while (i >= 0 || j >= 0) {
         const int64_t pos = base + i + j + 1;
-        if (i < 0) {
-            alq[pos] = '_';
-            als[pos] = S[bi.oj + j];
-            --j;
-            continue;
-        }
-        if (j < 0) {
-            alq[pos] = Q[bi.oi + i];
-            als[pos] = '_';
-            --i;
+        if (i < 0 || j < 0) {
+            if (free_start) break;   // the path starts on the border
+            if (i < 0) {
+                alq[pos] = '_';
+                als[pos] = S[bi.oj + j];
+                --j;
+            } else {
+                alq[pos] = Q[bi.oi + i];
+                als[pos] = '_';
+                --i;
+            }
             continue;
         }
         const int pb = pred[bi.pred_base + (int64_t)(i + j) * 128 + j];
         if (st == 0) {
             const int hs = pb & 3;
+            if (hs == 3) break;   // clamped: the path starts after this cell
             if (hs == 0) {
                 alq[pos] = Q[bi.oi + i];
                 als[pos] = S[bi.oj + j];
@@ -2190,20 +2242,8 @@ static hipError_t launch_fill_c(int R, int NW, const DPProblem* probs, const Gro
 template <int NW>
 static hipError_t launch_fill_aff_n(const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
                                     uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
-    const dim3 blk(64 * (NW + 1));
-    switch (fp.kind) {
-        case KIND_GLOBAL:
-            hipLaunchKernelGGL((fill_affine_kernel<KIND_GLOBAL, NW>), dim3(grid), blk, 0, st, probs, groups, ngroups,
-                               dq, err, fp);
-            break;
-        case KIND_SEMIGLOBAL:
-            hipLaunchKernelGGL((fill_affine_kernel<KIND_SEMIGLOBAL, NW>), dim3(grid), blk, 0, st, probs, groups,
-                               ngroups, dq, err, fp);
-            break;
-        default:
-            hipLaunchKernelGGL((fill_affine_kernel<KIND_LOCAL, NW>), dim3(grid), blk, 0, st, probs, groups, ngroups,
-                               dq, err, fp);
-    }
+    hipLaunchKernelGGL((fill_affine_kernel<NW>), dim3(grid), dim3(64 * (NW + 1)), 0, st, probs, groups, ngroups, dq,
+                       err, fp);
     return hipGetLastError();
 }
 #endif  // ANYSEQ_MICRO
@@ -2263,32 +2303,20 @@ hipError_t anyseq_launch_shard_combine(int kind, const int32_t* rowT, int h1, co
     return hipGetLastError();
 }
 
-hipError_t anyseq_launch_aff_rowbest(const void* rowbest, int h, int32_t* out, hipStream_t st) {
-    hipLaunchKernelGGL(anyseq::aff_rowbest_kernel, dim3(1), dim3(1024), 0, st, (const int2*)rowbest, h, out);
-    return hipGetLastError();
-}
-
-hipError_t anyseq_launch_aff_edge_scan(const void* row, int w, const int32_t* col, int h, int nge, int rborder,
-                                       int cborder, int32_t* out, hipStream_t st) {
-    hipLaunchKernelGGL(anyseq::aff_edge_scan_kernel, dim3(1), dim3(1024), 0, st, (const int2*)row, w, col, h, nge,
-                       rborder, cborder, out);
-    return hipGetLastError();
-}
-
 hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, const int32_t* LH, const int32_t* LE,
-                                     const int32_t* RH, const int32_t* RE, int go, int ge, int32_t* splits,
-                                     int32_t* types, hipStream_t st) {
+                                     const int32_t* RH, const int32_t* RE, const int32_t* pbest, int go, int ge,
+                                     int32_t* splits, int32_t* types, int32_t* score, hipStream_t st) {
     if (nparts > 0)
         hipLaunchKernelGGL(anyseq::aff_hb_join_kernel, dim3(nparts), dim3(256), 0, st,
-                           (const anyseq::PartInfo*)parts, half, LH, LE, RH, RE, go, ge, splits, types);
+                           (const anyseq::PartInfo*)parts, half, LH, LE, RH, RE, pbest, go, ge, splits, types, score);
     return hipGetLastError();
 }
 
-hipError_t anyseq_launch_aff_pred(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
+hipError_t anyseq_launch_aff_pred(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
                                   int match, int mismatch, int go, int ge, hipStream_t st) {
     if (nblocks > 0)
-        hipLaunchKernelGGL(anyseq::aff_pred_kernel, dim3(nblocks), dim3(64), 0, st,
-                           (const anyseq::BlockInfo*)blocks, nblocks, Q, S, pred, match, mismatch, go, ge);
+        hipLaunchKernelGGL(anyseq::aff_pred_kernel, dim3(nblocks), dim3(64), 0, st, (anyseq::BlockInfo*)blocks,
+                           nblocks, Q, S, pred, match, mismatch, go, ge);
     return hipGetLastError();
 }
 

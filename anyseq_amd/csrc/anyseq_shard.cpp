@@ -236,6 +236,7 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     P.q_step = 1;
     P.s_step = 1;
     P.w = w;
+    if (aff) set_aff_kind(P, kind);
     P.h = h1;
     P.out_row = rowT;
     P.out_col = colT;

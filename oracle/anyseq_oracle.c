@@ -729,53 +729,73 @@ int64_t oracle_affine_score(int kind, const char* qc, int n, const char* sc_, in
 
 /* ===================================================================== */
 /* Build-defined affine CONSTRUCT (linear space).  No reference semantics */
-/* (see above); this is the semantics of the HIP path, restated:         */
-/*  1. the aligned rectangle [is,ie] x [js,je]:                          */
-/*     global: the whole matrix;                                         */
-/*     local: end = oracle_affine_score's position (max H, then smallest */
-/*       i, then smallest j); start = argmax of the GLOBAL DP of the     */
-/*       reversed prefixes q[0..ie], s[0..je] (same tie rule, reversed   */
-/*       coordinates); best <= 0 -> empty alignment;                     */
-/*     semiglobal: end = oracle_affine_score's position (j or i = -1 ->  */
-/*       empty); start = best cell of that reversed GLOBAL DP's last row */
-/*       (b = -1 .. je, first max) then last column (a = -1 .. ie, only  */
-/*       if strictly greater);                                           */
-/*  2. a GLOBAL affine alignment of the rectangle by the column-split    */
-/*     Hirschberg of the linear construct (same levels, parts, splits),  */
-/*     where a split also records its crossing state: H (any) or E (a    */
-/*     horizontal gap crossing the column boundary, opened once).  A     */
-/*     sub-problem starting after an E crossing forbids a non-gap start  */
-/*     and pays no open for its first gap (BM_EFREE); one ending before  */
-/*     it must end in a horizontal gap (its reversed half: BM_EPAID).    */
-/*     Join of part rows i = -1 .. len-1, ascending, strict >, H before  */
-/*     E: HL(i) + HR(len-i-2), EL(i) + ER(len-i-2) - go;                  */
-/*  3. final 128-column blocks: full Gotoh with predecessors (H: diag >  */
-/*     E > F; E/F: open unless extending is strictly better), walked     */
-/*     from the block's end in state H (or E after an E crossing);       */
-/*     output in the sparse i+j+1 layout of traceback.impala:47-80.      */
+/* (see above); this is the semantics of the HIP path, restated.          */
+/*                                                                       */
+/* One column-split Hirschberg over the WHOLE matrix (the level / part /  */
+/* split structure of the linear construct, align.impala:237-311), where  */
+/* the alignment's ends may be free.  Every split boundary b (between     */
+/* 128-column blocks b and b+1; -1 = left edge, nb-1 = right edge) holds  */
+/* a row spl[b] and a type:                                              */
+/*   H      the path crosses b; rows < spl[b] lie left of it;             */
+/*   E      same, inside a horizontal gap (opened once, left of b);       */
+/*   BEFORE the path ends left of b;  AFTER the path starts right of b.   */
+/* Top level: global H .. H (spl -1 .. nb-1 = 0 .. n); local / semiglobal */
+/* AFTER .. BEFORE.  A part [sb, eb] is empty if T[sb] = BEFORE or        */
+/* T[eb] = AFTER; its start is anchored (H: scheme corner, E: continuing  */
+/* gap) or FREE (T[sb] = AFTER), its end anchored (H, or E: ends in a     */
+/* gap) or FREE (T[eb] = BEFORE).  FREE means local: zero borders + the   */
+/* clamp H >= 0, any cell may end; semiglobal: zero top border (and left  */
+/* border at the matrix's left edge), ends on the last row / column.     */
+/* Per part: left half forward, right half reversed (free end -> free     */
+/* reversed start), then the first maximum (strict >) of                 */
+/*   BEFORE (free end):   best end cell in the left half,                 */
+/*   AFTER  (free start): best start cell in the right half,              */
+/*   rows i = -1 .. len-1: HL(i) + HR(len-i-2), then EL(i) + ER(..) - go. */
+/* Final blocks: Gotoh predecessors (H: diag > E > F, local clamp only if */
+/* 0 > H; E/F open unless extending is strictly better), walked from the  */
+/* block's end (anchored: bottom-right in H or E; free: local first max   */
+/* of all cells in row-major order, semiglobal first max of the last row, */
+/* then of the last column if strictly greater) back to its start         */
+/* (anchored: the corner; free: a clamped cell or the border).  Output in */
+/* the sparse i+j+1 layout of traceback.impala:47-80.  Optimal score <= 0 */
+/* (local / semiglobal): the empty alignment.                            */
 /* ===================================================================== */
-enum { BM_NORMAL = 0, BM_EFREE = 1, BM_EPAID = 2 };
+enum { BM_NORMAL = 0, BM_EFREE = 1, BM_EPAID = 2, BM_FREE_LOCAL = 3, BM_FREE_SEMI = 4, BM_FREE_SEMI_OPEN = 5 };
+enum { T_H = 0, T_E = 1, T_BEFORE = 2, T_AFTER = 3 };
 #define ANEG AFF_NEG_INF
 
 typedef struct { const uint8_t* b; Index off; int step; } Acc;
 static inline uint8_t acc_at(Acc a, Index i) { return a.b[a.off + (Index)a.step * i]; }
 typedef struct { int match, mismatch, go, ge; } AffSc;
 
-/* Global affine DP of q x s (h x w) under border mode bm.  Optional outputs:
- * last column H/E (h each), last row H (w), argmax over all cells (row-major
- * first max: smallest row, then smallest column). */
-static void aff_global_fill(Acc q, Index h, Acc s, Index w, const AffSc* sc, int bm,
-                            Score* colH, Score* colE, Score* lastrow,
-                            Score* best, Index* bi, Index* bj) {
+/* Border values (H space) of a sub-problem by border mode: corner, top row (c >= 0),
+ * left column (r >= 0).  FREE_SEMI: the left border is open only at the matrix edge. */
+static inline Score bm_corner(int bm) { return (bm == BM_EFREE || bm == BM_EPAID) ? ANEG : 0; }
+static inline Score bm_top(int bm, const AffSc* sc, Index c) {
+    if (bm == BM_NORMAL || bm == BM_EPAID) return sc->go + (c + 1) * sc->ge;
+    if (bm == BM_EFREE) return (c + 1) * sc->ge;
+    return 0;
+}
+static inline Score bm_left(int bm, const AffSc* sc, Index r) {
+    if (bm == BM_NORMAL) return sc->go + (r + 1) * sc->ge;
+    if (bm == BM_FREE_LOCAL || bm == BM_FREE_SEMI_OPEN) return 0;
+    return ANEG;
+}
+
+/* Affine DP of q x s (h x w) under border mode bm (local clamp for FREE_LOCAL).
+ * Optional outputs: last column H / E, the maximum over all cells, the maximum
+ * over the last row. */
+static void aff_fill(Acc q, Index h, Acc s, Index w, const AffSc* sc, int bm, Score* colH, Score* colE,
+                     Score* best_all, Score* best_last) {
     Score* H = (Score*)malloc(sizeof(Score) * (size_t)(w + 1));
     Score* F = (Score*)malloc(sizeof(Score) * (size_t)(w + 1));
-    const Score tbase = bm == BM_EFREE ? 0 : sc->go;
-    H[0] = bm == BM_NORMAL ? 0 : ANEG;
-    for (Index c = 0; c < w; ++c) { H[c + 1] = tbase + (c + 1) * sc->ge; F[c + 1] = ANEG; }
-    Score mx = SCORE_MIN_VALUE; Index mi = -1, mj = -1;
+    const int clamp = bm == BM_FREE_LOCAL;
+    H[0] = bm_corner(bm);
+    for (Index c = 0; c < w; ++c) { H[c + 1] = bm_top(bm, sc, c); F[c + 1] = ANEG; }
+    Score ba = ANEG, bl = ANEG;
     for (Index r = 0; r < h; ++r) {
         Score diag = H[0];
-        Score left = bm == BM_NORMAL ? sc->go + (r + 1) * sc->ge : ANEG;
+        Score left = bm_left(bm, sc, r);
         H[0] = left;
         Score E = ANEG;
         const uint8_t qs = acc_at(q, r);
@@ -789,35 +809,57 @@ static void aff_global_fill(Acc q, Index h, Acc s, Index w, const AffSc* sc, int
             Score hv = diag + (qs == acc_at(s, c) ? sc->match : sc->mismatch);
             if (E > hv) hv = E;
             if (f > hv) hv = f;
+            if (clamp && 0 > hv) hv = 0;
             diag = up;
             H[c + 1] = hv;
             left = hv;
-            if (hv > mx) { mx = hv; mi = r; mj = c; }
+            if (hv > ba) ba = hv;
+            if (r == h - 1 && hv > bl) bl = hv;
         }
         if (colH) colH[r] = H[w];
         if (colE) colE[r] = w > 0 ? E : ANEG;
     }
-    if (lastrow) for (Index c = 0; c < w; ++c) lastrow[c] = H[c + 1];
-    if (best) { *best = mx; *bi = mi; *bj = mj; }
+    if (best_all) *best_all = ba;
+    if (best_last) *best_last = bl;
     free(H); free(F);
 }
 
 typedef struct { Score* v; Index n; } IVec;   /* logical index -1 at v[0] */
 #define IV(x, i) ((x).v[(i) + 1])
 
-/* Final 128-column block: Gotoh with predecessor bytes, walk, sparse output. */
-enum { AP_DIAG = 0, AP_E = 1, AP_F = 2 };
+/* Final 128-column block: Gotoh with predecessor bytes (bits 0-1: H source 0 diag,
+ * 1 E, 2 F, 3 clamped; bit 2 E extends, bit 3 F extends), walk, sparse output.
+ * bm: start border mode; e_end: 0 end in H, 1 end in E (both at the bottom-right
+ * corner), 2 free end; semi_lastcol: free semiglobal end, the block holds the
+ * matrix's last column. */
+enum { AP_DIAG = 0, AP_E = 1, AP_F = 2, AP_NONE = 3 };
+/* rows / columns the last construct emitted (tests check them against the kind's rules) */
+static int32_t g_last_rect[4] = {0, -1, 0, -1};   /* is, ie, js, je */
+static inline void emit_q(Index i) {
+    if (g_last_rect[1] < g_last_rect[0]) { g_last_rect[0] = g_last_rect[1] = i; return; }
+    if (i < g_last_rect[0]) g_last_rect[0] = i;
+    if (i > g_last_rect[1]) g_last_rect[1] = i;
+}
+static inline void emit_s(Index j) {
+    if (g_last_rect[3] < g_last_rect[2]) { g_last_rect[2] = g_last_rect[3] = j; return; }
+    if (j < g_last_rect[2]) g_last_rect[2] = j;
+    if (j > g_last_rect[3]) g_last_rect[3] = j;
+}
 static void aff_block_walk(const uint8_t* Q, const uint8_t* S, Index oi, Index h, Index oj, Index w,
-                           const AffSc* sc, int smode, int e_end, char* alq, char* als) {
-    uint8_t* P = (uint8_t*)calloc((size_t)(h > 0 ? h : 1) * (size_t)w, 1);
+                           const AffSc* sc, int bm, int e_end, int kind, int semi_lastcol, char* alq, char* als) {
+    if (e_end == 2 && h <= 0) return;   /* free end, no rows: the path ended at the block's corner */
+    uint8_t* P = (uint8_t*)calloc((size_t)(h > 0 ? h : 1) * (size_t)(w > 0 ? w : 1), 1);
     Score* H = (Score*)malloc(sizeof(Score) * (size_t)(w + 1));
     Score* F = (Score*)malloc(sizeof(Score) * (size_t)(w + 1));
-    const Score tbase = smode == BM_EFREE ? 0 : sc->go;
-    H[0] = smode == BM_NORMAL ? 0 : ANEG;
-    for (Index c = 0; c < w; ++c) { H[c + 1] = tbase + (c + 1) * sc->ge; F[c + 1] = ANEG; }
+    const int clamp = bm == BM_FREE_LOCAL;
+    const int free_start = bm >= BM_FREE_LOCAL;
+    H[0] = bm_corner(bm);
+    for (Index c = 0; c < w; ++c) { H[c + 1] = bm_top(bm, sc, c); F[c + 1] = ANEG; }
+    Score xb = ANEG; Index xi = h - 1, xj = w - 1;   /* free end: the exit cell */
+    Score cb = ANEG; Index ci = -1;                  /* semiglobal: first max of the last column */
     for (Index r = 0; r < h; ++r) {
         Score diag = H[0];
-        Score left = smode == BM_NORMAL ? sc->go + (r + 1) * sc->ge : ANEG;
+        Score left = bm_left(bm, sc, r);
         H[0] = left;
         Score E = ANEG;
         for (Index c = 0; c < w; ++c) {
@@ -833,33 +875,48 @@ static void aff_block_walk(const uint8_t* Q, const uint8_t* S, Index oi, Index h
             int hs = AP_DIAG;
             if (E > hv) { hv = E; hs = AP_E; }
             if (f > hv) { hv = f; hs = AP_F; }
+            if (clamp && 0 > hv) { hv = 0; hs = AP_NONE; }
             pb |= (uint8_t)hs;
             P[(size_t)r * w + c] = pb;
             diag = up;
             H[c + 1] = hv;
             left = hv;
+            if (e_end == 2) {
+                if (kind == SCHEME_LOCAL) {
+                    if (hv > xb) { xb = hv; xi = r; xj = c; }
+                } else {
+                    if (r == h - 1 && hv > xb) { xb = hv; xi = r; xj = c; }
+                    if (semi_lastcol && c == w - 1 && hv > cb) { cb = hv; ci = r; }
+                }
+            }
         }
     }
+    if (e_end == 2 && kind != SCHEME_LOCAL && semi_lastcol && cb > xb) { xb = cb; xi = ci; xj = w - 1; }
     /* walk: state 0 = H, 1 = E, 2 = F */
-    Index i = h - 1, j = w - 1;
-    int st = e_end ? 1 : 0;
+    Index i = xi, j = xj;
+    int st = e_end == 1 ? 1 : 0;
     const Index base = oi + oj;
     while (i >= 0 || j >= 0) {
-        if (i < 0) { alq[base + i + j + 1] = '_'; als[base + i + j + 1] = (char)S[oj + j]; --j; continue; }
-        if (j < 0) { alq[base + i + j + 1] = (char)Q[oi + i]; als[base + i + j + 1] = '_'; --i; continue; }
+        if (i < 0 || j < 0) {
+            if (free_start) break;   /* the path starts on the border */
+            if (i < 0) { alq[base + i + j + 1] = '_'; als[base + i + j + 1] = (char)S[oj + j]; emit_s(oj + j); --j; continue; }
+            alq[base + i + j + 1] = (char)Q[oi + i]; als[base + i + j + 1] = '_'; emit_q(oi + i); --i; continue;
+        }
         const uint8_t pb = P[(size_t)i * w + j];
         if (st == 0) {
             const int hs = pb & 3;
+            if (hs == AP_NONE) break;   /* local: the path starts after this cell */
             if (hs == AP_DIAG) {
                 alq[base + i + j + 1] = (char)Q[oi + i]; als[base + i + j + 1] = (char)S[oj + j];
+                emit_q(oi + i); emit_s(oj + j);
                 --i; --j;
             } else st = hs == AP_E ? 1 : 2;
         } else if (st == 1) {
-            alq[base + i + j + 1] = '_'; als[base + i + j + 1] = (char)S[oj + j];
+            alq[base + i + j + 1] = '_'; als[base + i + j + 1] = (char)S[oj + j]; emit_s(oj + j);
             st = (pb & 4) ? 1 : 0;
             --j;
         } else {
-            alq[base + i + j + 1] = (char)Q[oi + i]; als[base + i + j + 1] = '_';
+            alq[base + i + j + 1] = (char)Q[oi + i]; als[base + i + j + 1] = '_'; emit_q(oi + i);
             st = (pb & 8) ? 2 : 0;
             --i;
         }
@@ -867,22 +924,24 @@ static void aff_block_walk(const uint8_t* Q, const uint8_t* S, Index oi, Index h
     free(P); free(H); free(F);
 }
 
-/* Global affine Hirschberg of the rectangle q x s (n x m); output at
- * alq/als + i + j + 1 (callers pass the rectangle's offset). */
-static void aff_construct_rect(const uint8_t* Q, Index n, const uint8_t* S, Index m, const AffSc* sc,
-                               char* alq, char* als) {
-    if (m <= 0) {   /* all query rows against gaps, down the left border: position i + (-1) + 1 */
-        for (Index i = 0; i < n; ++i) { alq[i] = (char)Q[i]; als[i] = '_'; }
-        return;
-    }
+/* Border mode of a FREE end for the kind: local clamps everywhere; semiglobal opens
+ * the side border only at the matrix edge. */
+static inline int free_bm(int kind, int at_edge) {
+    return kind == SCHEME_LOCAL ? BM_FREE_LOCAL : (at_edge ? BM_FREE_SEMI_OPEN : BM_FREE_SEMI);
+}
+
+
+static void aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8_t* S, Index m, const AffSc* sc,
+                             char* alq, char* als) {
     const Index nb = round_up_div(m, MIN_PART_WIDTH_HB);
     IVec spl, typ;
     spl.n = nb; typ.n = nb;
     spl.v = (Score*)malloc(sizeof(Score) * (size_t)(nb + 1));
-    typ.v = (Score*)calloc((size_t)(nb + 1), sizeof(Score));
-    for (Index i = -1; i < nb; ++i) IV(spl, i) = SPLIT_UNSET;
+    typ.v = (Score*)malloc(sizeof(Score) * (size_t)(nb + 1));
+    for (Index i = -1; i < nb; ++i) { IV(spl, i) = SPLIT_UNSET; IV(typ, i) = T_H; }
     IV(spl, -1) = 0;
     IV(spl, nb - 1) = n;
+    if (kind != SCHEME_GLOBAL) { IV(typ, -1) = T_AFTER; IV(typ, nb - 1) = T_BEFORE; }
     Index pw = next_pow_2(m);
     Index bpp = pw / MIN_PART_WIDTH_HB;
     Score *LH = (Score*)malloc(sizeof(Score) * (size_t)(n + 1)), *LE = (Score*)malloc(sizeof(Score) * (size_t)(n + 1));
@@ -891,93 +950,79 @@ static void aff_construct_rect(const uint8_t* Q, Index n, const uint8_t* S, Inde
         const Index half = pw / 2;
         const Index parts = (m + half - 1) / pw;
         for (Index p = 0; p < parts; ++p) {
-            const Index sb = p * bpp - 1, eb = imin((p + 1) * bpp - 1, nb - 1);
-            const Index off = IV(spl, sb), len = IV(spl, eb) - off;
+            const Index sb = p * bpp - 1, eb = imin((p + 1) * bpp - 1, nb - 1), mid = p * bpp + bpp / 2 - 1;
+            const int ts = IV(typ, sb), te = IV(typ, eb);
+            if (ts == T_BEFORE || te == T_AFTER) {   /* empty part: so are both halves */
+                IV(typ, mid) = ts == T_BEFORE ? T_BEFORE : T_AFTER;
+                IV(spl, mid) = IV(spl, sb);
+                continue;
+            }
             if (IV(spl, sb) == SPLIT_UNSET || IV(spl, eb) == SPLIT_UNSET) { g_error = 1; continue; }
-            const int smode = IV(typ, sb) ? BM_EFREE : BM_NORMAL;
-            const int rmode = IV(typ, eb) ? BM_EPAID : BM_NORMAL;
+            const Index off = IV(spl, sb), len = IV(spl, eb) - off;
             const Index hoj_l = p * pw, hoj_r = p * pw + half;
             const Index hw = imin(half, m - hoj_r);
+            const int lbm = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, hoj_l == 0);
+            const int rbm = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : free_bm(kind, hoj_r + hw == m);
+            const int sfree = ts == T_AFTER, efree = te == T_BEFORE;
+            Score bestL = ANEG, bestR = ANEG;
             if (len > 0) {
+                Score ba, bl;
                 Acc qa = {Q, off, 1}, sa = {S, hoj_l, 1};
-                aff_global_fill(qa, len, sa, half, sc, smode, LH + off, LE + off, NULL, NULL, NULL, NULL);
+                aff_fill(qa, len, sa, half, sc, lbm, LH + off, LE + off, &ba, &bl);
+                if (efree) bestL = kind == SCHEME_LOCAL ? ba : bl;
                 Acc qr = {Q, off + len - 1, -1}, sr = {S, hoj_r + hw - 1, -1};
-                aff_global_fill(qr, len, sr, hw, sc, rmode, RH + off, RE + off, NULL, NULL, NULL, NULL);
+                aff_fill(qr, len, sr, hw, sc, rbm, RH + off, RE + off, &ba, &bl);
+                if (sfree) bestR = kind == SCHEME_LOCAL ? ba : bl;
             }
-            const Score bL = (smode == BM_EFREE ? 0 : sc->go) + half * sc->ge;
-            const Score bR = sc->go + hw * sc->ge;
-            Score best = SCORE_MIN_VALUE; Index idx = -1; int type = 0;
+            /* index -1: the halves' top borders at the midline (a FREE top border is no gap) */
+            const Score bLH = bm_top(lbm, sc, half - 1), bLE = sfree ? ANEG : bLH;
+            const Score bRH = bm_top(rbm, sc, hw - 1), bRE = efree ? ANEG : bRH;
+            Score best = SCORE_MIN_VALUE; Index idx = -1; int type = T_H;
+            if (efree && bestL > best) { best = bestL; type = T_BEFORE; }
+            if (sfree && bestR > best) { best = bestR; type = T_AFTER; }
             for (Index i = -1; i < len; ++i) {
                 const Index k = len - i - 2;
-                const Score hl = i < 0 ? bL : LH[off + i], el = i < 0 ? bL : LE[off + i];
-                const Score hr = k < 0 ? bR : RH[off + k], er = k < 0 ? bR : RE[off + k];
+                const Score hl = i < 0 ? bLH : LH[off + i], el = i < 0 ? bLE : LE[off + i];
+                const Score hr = k < 0 ? bRH : RH[off + k], er = k < 0 ? bRE : RE[off + k];
                 Score v = hl + hr;
-                if (v > best) { best = v; idx = i; type = 0; }
+                if (v > best) { best = v; idx = i; type = T_H; }
                 v = el + er - sc->go;
-                if (v > best) { best = v; idx = i; type = 1; }
+                if (v > best) { best = v; idx = i; type = T_E; }
             }
-            const Index si = p * bpp + bpp / 2 - 1;
-            IV(spl, si) = off + idx + 1;
-            IV(typ, si) = type;
+            IV(typ, mid) = type;
+            IV(spl, mid) = type == T_BEFORE ? off + len : type == T_AFTER ? off : off + idx + 1;
         }
         pw /= 2;
         bpp /= 2;
     }
     for (Index b = 0; b < nb; ++b) {
+        const int ts = IV(typ, b - 1), te = IV(typ, b);
+        if (ts == T_BEFORE || te == T_AFTER) continue;
         const Index oi = IV(spl, b - 1), h = IV(spl, b) - oi;
         const Index oj = b * MIN_PART_WIDTH_HB, w = imin(MIN_PART_WIDTH_HB, m - oj);
         if (IV(spl, b - 1) == SPLIT_UNSET || IV(spl, b) == SPLIT_UNSET) { g_error = 1; continue; }
-        aff_block_walk(Q, S, oi, h, oj, w, sc, IV(typ, b - 1) ? BM_EFREE : BM_NORMAL, IV(typ, b) != 0, alq, als);
+        const int bm = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, oj == 0);
+        const int e_end = te == T_H ? 0 : te == T_E ? 1 : 2;
+        aff_block_walk(Q, S, oi, h, oj, w, sc, bm, e_end, kind, oj + w == m, alq, als);
     }
     free(spl.v); free(typ.v); free(LH); free(LE); free(RH); free(RE);
 }
 
-/* The aligned rectangle of step 1; returns 0 for an empty alignment. */
-int oracle_affine_rect(int kind, const char* qc, int n, const char* sc_, int m, int match, int mismatch, int go,
-                       int ge, int32_t* rect, int64_t* score) {
-    const uint8_t* q = (const uint8_t*)qc; const uint8_t* s = (const uint8_t*)sc_;
-    AffSc sc = {match, mismatch, go, ge};
-    int32_t bi = -1, bj = -1;
-    const int64_t res = oracle_affine_score(kind, qc, n, sc_, m, match, mismatch, go, ge, &bi, &bj);
-    *score = res;
-    if (kind == SCHEME_GLOBAL) { rect[0] = 0; rect[1] = n - 1; rect[2] = 0; rect[3] = m - 1; return n > 0 || m > 0; }
-    if (n <= 0 || m <= 0) return 0;
-    if (kind == SCHEME_LOCAL && res <= 0) return 0;
-    if (bi < 0 || bj < 0) return 0;
-    const Index ie = bi, je = bj;
-    Acc qr = {q, ie, -1}, sr = {s, je, -1};
-    if (kind == SCHEME_LOCAL) {
-        Score best; Index a, b;
-        aff_global_fill(qr, ie + 1, sr, je + 1, &sc, BM_NORMAL, NULL, NULL, NULL, &best, &a, &b);
-        rect[0] = ie - a; rect[1] = ie; rect[2] = je - b; rect[3] = je;
-        return 1;
-    }
-    /* semiglobal: reversed GLOBAL DP, best of its last row (b = -1..je) then last column */
-    Score* colH = (Score*)malloc(sizeof(Score) * (size_t)(ie + 1));
-    Score* row = (Score*)malloc(sizeof(Score) * (size_t)(je + 1));
-    aff_global_fill(qr, ie + 1, sr, je + 1, &sc, BM_NORMAL, colH, NULL, row, NULL, NULL, NULL);
-    Score best = go + (ie + 1) * ge;   /* b = -1: the reversed left border at row ie */
-    Index sa = ie, sb = -1;
-    for (Index b = 0; b <= je; ++b) if (row[b] > best) { best = row[b]; sa = ie; sb = b; }
-    {
-        const Score top = go + (je + 1) * ge;   /* a = -1: the reversed top border at column je */
-        if (top > best) { best = top; sa = -1; sb = je; }
-    }
-    for (Index a = 0; a <= ie; ++a) if (colH[a] > best) { best = colH[a]; sa = a; sb = je; }
-    free(colH); free(row);
-    rect[0] = ie - sa; rect[1] = ie; rect[2] = je - sb; rect[3] = je;
-    return 1;
-}
+/* Rectangle [is, ie] x [js, je] of the last oracle_affine_construct (ie < is: empty). */
+void oracle_affine_last_rect(int32_t* rect) { memcpy(rect, g_last_rect, sizeof g_last_rect); }
 
 int64_t oracle_affine_construct(int kind, const char* qc, int n, const char* sc_, int m, int match, int mismatch,
                                 int go, int ge, char* alq, char* als) {
     for (Index i = 0; i < n + m; ++i) { alq[i] = ' '; als[i] = ' '; }
-    int32_t r[4];
-    int64_t score = 0;
-    if (!oracle_affine_rect(kind, qc, n, sc_, m, match, mismatch, go, ge, r, &score)) return score;
+    g_last_rect[0] = 0; g_last_rect[1] = -1; g_last_rect[2] = 0; g_last_rect[3] = -1;
+    const int64_t score = oracle_affine_score(kind, qc, n, sc_, m, match, mismatch, go, ge, NULL, NULL);
+    if (n + m == 0) return score;
+    if (kind != SCHEME_GLOBAL && (score <= 0 || n == 0 || m == 0)) return score;   /* the empty alignment */
     AffSc sc = {match, mismatch, go, ge};
-    const Index off = r[0] + r[2];
-    aff_construct_rect((const uint8_t*)qc + r[0], r[1] - r[0] + 1, (const uint8_t*)sc_ + r[2], r[3] - r[2] + 1, &sc,
-                       alq + off, als + off);
+    if (m == 0) {   /* global: all query rows against gaps, down the left border: position i + (-1) + 1 */
+        for (Index i = 0; i < n; ++i) { alq[i] = qc[i]; als[i] = '_'; emit_q(i); }
+    } else {
+        aff_construct_hb(kind, (const uint8_t*)qc, n, (const uint8_t*)sc_, m, &sc, alq, als);
+    }
     return score;
 }

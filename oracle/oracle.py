@@ -51,9 +51,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_construct_fulltb.restype = c_i64
         L.oracle_construct_fulltb.argtypes = [c_p, c_int, c_p, c_int, c_int, c_int, c_int,
                                               ctypes.c_void_p, ctypes.c_void_p]
-        L.oracle_affine_rect.restype = c_int
-        L.oracle_affine_rect.argtypes = [c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_int, c_int,
-                                         i32p, ctypes.POINTER(c_i64)]
+        L.oracle_affine_last_rect.argtypes = [i32p]
         _lib = L
     return _lib
 
@@ -129,15 +127,12 @@ def affine_construct(kind, q, s, match=2, mismatch=-1, gap_open=-2, gap_extend=-
     return r, aq.raw[: n + m], as_.raw[: n + m]
 
 
-def affine_rect(kind, q, s, match=2, mismatch=-1, gap_open=-2, gap_extend=-1):
-    """(nonempty, (is, ie, js, je), score): the rectangle an affine construct aligns."""
-    k = KINDS[kind] if isinstance(kind, str) else kind
-    q, s = _b(q), _b(s)
+def affine_last_rect():
+    """(is, ie, js, je): the query rows / subject columns the last affine_construct
+    emitted (ie < is or je < js: none)."""
     rect = (ctypes.c_int32 * 4)()
-    sc = ctypes.c_int64(0)
-    ok = lib().oracle_affine_rect(k, q, len(q), s, len(s), match, mismatch, gap_open, gap_extend, rect,
-                                  ctypes.byref(sc))
-    return bool(ok), tuple(rect), sc.value
+    lib().oracle_affine_last_rect(rect)
+    return tuple(rect)
 
 
 # --------------------------------------------------------------------------

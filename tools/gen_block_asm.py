@@ -302,10 +302,11 @@ def gen_loop_aff(kind, border, pub):
         X  v_max_i32         e, e, hg               E_G = max(E_G, G_left + go)
         E  v_add_u32         A, dg, W
         M  v_max3_i32        OG, A, e, TF           cell
-       (L  v_max_i32         OG, Z, OG              clamp: H >= 0 <=> G >= Z_t (wave-uniform))
+       (L  v_max_i32         OG, Z, OG              clamp: H >= 0 <=> G >= Z_t (wave-uniform);
+                                                    Z far below Z_t when the problem does not clamp)
         H  v_add_u32         hg, go, OG             G + go (next E, this F-down)
         Fm v_max_i32         OF, TF, hg             F-down
-       (L  every 2nd step: best = max3(best, OG - Z, OG' - Z'))
+       (L  every 2nd step: best = max3(best, OG - Zb, OG' - Zb'), Zb = Z_t)
         S  two wave_shl:1 shift-register steps (publishing roles)."""
     L = kind == "L"
     trailing = pub != "lds"
@@ -389,12 +390,15 @@ def gen_loop_aff(kind, border, pub):
             e(f"v_add_u32_e32 %[hg], %[go], {OG(u)}")
             e(f"v_max_i32_e32 {OF(u)}, {tf}, %[hg]")
             if L:
+                # best in H space: OG - Zb (Zb = the true (r+c+2)(-ge); z is the clamp
+                # bound, Zb or far below it when the problem does not clamp)
                 if u % 2 == 0:
-                    e(f"v_subrev_u32_e32 v{AH}, %[z], {OG(u)}")
+                    e(f"v_subrev_u32_e32 v{AH}, %[zb], {OG(u)}")
                 else:
-                    e(f"v_subrev_u32_e32 v{AVT2}, %[z], {OG(u)}")
+                    e(f"v_subrev_u32_e32 v{AVT2}, %[zb], {OG(u)}")
                     e(f"v_max3_i32 %[best], %[best], v{AH}, v{AVT2}")
                 e("s_add_u32 %[z], %[z], %[nge]")
+                e("s_add_u32 %[zb], %[zb], %[nge]")
             if u >= 2 and pub != "none":
                 e(f"v_mov_b32_dpp {OG(u - 1)}, {OG(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_mov_b32_dpp {OF(u - 1)}, {OF(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
