@@ -1,0 +1,42 @@
+"""GPU path against the full-size affine construct fixtures (tests/golden/make_golden_affine.py):
+configs[2] (local affine score + traceback of main.cpp's `-r 65536 65536` pair) and the
+configs[3] workload on a 262,144-bp prefix of the synthetic genome pair (semiglobal).
+Bit-exact: score, SHA-256 of both sparse i+j+1 strings, and the dense CIGAR."""
+import hashlib
+import json
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def check(anyseq, g, q, s):
+    assert (len(q), len(s), sha(q), sha(s)) == (g["lq"], g["ls"], g["sha_q"], g["sha_s"]), "inputs differ"
+    sc = g["scoring"]
+    v, aq, as_ = anyseq.construct(g["kind"], q, s, match=sc["match"], mismatch=sc["mismatch"],
+                                  gap_open=sc["gap_open"], gap_extend=sc["gap_extend"])
+    assert v == g["score"]
+    assert anyseq.cigar(aq, as_) == g["cigar"]
+    assert (sha(aq), sha(as_)) == (g["sha_alq"], g["sha_als"])
+
+
+def test_config2_local_affine_65536(anyseq):
+    g = json.load(open(os.path.join(GOLD, "config2_65536.json")))
+    q, s = anyseq.main_random_pair(65536, 65536)
+    check(anyseq, g, q, s)
+
+
+def test_config3_semiglobal_affine_prefix(anyseq):
+    path = os.path.join(GOLD, "config3_prefix.json")
+    if not os.path.exists(path):
+        pytest.skip("config3_prefix.json not generated")
+    from anyseq_amd import genome
+    g = json.load(open(path))
+    q, s = genome.synthetic_related_pair(4_641_652, 0.9)
+    check(anyseq, g, q[:g["lq"]], s[:g["ls"]])
