@@ -46,6 +46,7 @@ hipError_t anyseq_launch_fulltb(const uint8_t* Q, int n, const uint8_t* S, int m
 hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, const int32_t* LH, const int32_t* LE,
                                      const int32_t* RH, const int32_t* RE, const int32_t* pbest, int go, int ge,
                                      int32_t* splits, int32_t* types, int32_t* score, hipStream_t st);
+hipError_t anyseq_launch_aff_row_to_col(const void* jobs, int njobs, int maxn, int nge, hipStream_t st);
 hipError_t anyseq_launch_aff_pred(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
                                   int match, int mismatch, int go, int ge, hipStream_t st);
 hipError_t anyseq_launch_aff_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
@@ -645,6 +646,50 @@ int free_bm(int kind, bool at_edge) {
     return kind == KIND_LOCAL ? BM_FREE_LOCAL : (at_edge ? BM_FREE_SEMI_OPEN : BM_FREE_SEMI);
 }
 
+// The same borders with query and subject swapped (a transposed half).
+int transposed_bm(int bm) {
+    return bm == BM_EFREE ? BM_FFREE : bm == BM_EPAID ? BM_FPAID : bm == BM_FREE_SEMI ? BM_FREE_SEMI_T : bm;
+}
+
+struct RowToColJob {   // anyseq_kernels.hip RowToCol
+    const void* row;
+    int32_t* H;
+    int32_t* E;
+    int32_t n, hlast;
+};
+
+// One Hirschberg half: rows qoff + qstep*r (r < h) of the query against columns
+// soff + sstep*c (c < w) of the subject, border mode bm, kind bits amode; its last
+// column goes to H / E (h each).  A half taller than wide runs TRANSPOSED (subject
+// bytes as rows): its band chain then follows the shorter side (h/64 bands of lag
+// + w steps becomes w/64 + h), and its bottom row (G, F-down) is the last column
+// (H, E-right) -- the join decisions are unchanged (aff_row_to_col_kernel).  The
+// values are those of the untransposed DP, so parity is unaffected.
+void add_half(std::vector<DPProblem>& probs, std::vector<RowToColJob>& jobs, int32_t*& rowpool, const uint8_t* dq,
+              int qoff, int qstep, int h, const uint8_t* ds, int soff, int sstep, int w, int bm, int amode,
+              int32_t* best, int32_t* H, int32_t* E) {
+    if (g_tuning.afft && h > w) {
+        DPProblem P = aff_problem(ds, soff, sstep, w, dq, qoff, qstep, h);
+        P.bmode = transposed_bm(bm);
+        // the original's last row is the transposed problem's last column
+        P.amode = (amode & AM_CLAMP) | ((amode & AM_BEST_LASTCOL) == AM_BEST_LAST ? AM_BEST_LASTCOL
+                                                                                   : (amode & AM_BEST_LASTCOL));
+        P.best = best;
+        P.out_row = rowpool;
+        rowpool += (size_t)((h + 63) & ~63) * 2;
+        probs.push_back(P);
+        jobs.push_back(RowToColJob{P.out_row, H, E, h, w - 1});
+        return;
+    }
+    DPProblem P = aff_problem(dq, qoff, qstep, h, ds, soff, sstep, w);
+    P.bmode = bm;
+    P.amode = amode;
+    P.best = best;
+    P.out_col = H;
+    P.out_col_e = E;
+    probs.push_back(P);
+}
+
 // Hirschberg levels + final blocks into d_alq / d_als (n+m bytes, already blank).
 // Returns the level-1 join value (the optimal score) or INT64_MIN if m <= 128
 // (no level).  kind != global with a level-1 value <= 0 stops there (empty
@@ -685,6 +730,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         std::vector<DPProblem> probs;
         std::vector<PartInfo>& pinfo = E.host_parts;
         pinfo.assign((size_t)parts, PartInfo{});
+        std::vector<RowToColJob> jobs;
+        // transposed halves' bottom rows: sum of part heights <= n (parts' rows are disjoint)
+        int32_t* rowpool = (int32_t*)E.outrow.get((size_t)2 * ((size_t)n + 64 * (size_t)parts) * 2 * 4);
         for (int p = 0; p < parts; ++p) {
             const int sb = p * sp.bpp - 1, eb = std::min((p + 1) * sp.bpp - 1, sp.nb - 1);
             PartInfo& pi = pinfo[p];
@@ -709,22 +757,23 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             pi.flags = (sfree ? 1 : 0) | (efree ? 2 : 0);
             if (len <= 0) continue;
             const int best_bits = local ? AM_BEST_ALL : AM_BEST_LAST;
-            DPProblem P = aff_problem(dq, off, 1, len, ds, hoj_l, 1, half);
-            P.bmode = pi.smode;
-            P.amode = (pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0);
-            P.best = efree ? pbest + 2 * p : nullptr;
-            P.out_col = LH + off;
-            P.out_col_e = LE + off;
-            probs.push_back(P);
-            P = aff_problem(dq, off + len - 1, -1, len, ds, hoj_r + hw - 1, -1, hw);
-            P.bmode = pi.emode;
-            P.amode = (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0);
-            P.best = sfree ? pbest + 2 * p + 1 : nullptr;
-            P.out_col = RH + off;
-            P.out_col_e = RE + off;
-            probs.push_back(P);
+            add_half(probs, jobs, rowpool, dq, off, 1, len, ds, hoj_l, 1, half, pi.smode,
+                     (pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0),
+                     efree ? pbest + 2 * p : nullptr, LH + off, LE + off);
+            add_half(probs, jobs, rowpool, dq, off + len - 1, -1, len, ds, hoj_r + hw - 1, -1, hw, pi.emode,
+                     (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0),
+                     sfree ? pbest + 2 * p + 1 : nullptr, RH + off, RE + off);
         }
         if (!probs.empty()) run_fill(E, probs, fp, st);
+        if (!jobs.empty()) {
+            int maxn = 0;
+            for (const auto& J : jobs) maxn = std::max(maxn, J.n);
+            E.host_jobs.resize(jobs.size() * sizeof(RowToColJob));
+            memcpy(E.host_jobs.data(), jobs.data(), E.host_jobs.size());
+            void* d_jobs = E.jobs.get(E.host_jobs.size());
+            HIPCHECK(hipMemcpyAsync(d_jobs, E.host_jobs.data(), E.host_jobs.size(), hipMemcpyHostToDevice, st));
+            HIPCHECK(anyseq_launch_aff_row_to_col(d_jobs, (int)jobs.size(), maxn, -sc.gap_extend, st));
+        }
         PartInfo* d_parts = (PartInfo*)E.parts.get(pinfo.size() * sizeof(PartInfo));
         HIPCHECK(hipMemcpyAsync(d_parts, pinfo.data(), pinfo.size() * sizeof(PartInfo), hipMemcpyHostToDevice, st));
         HIPCHECK(anyseq_launch_aff_hb_join(d_parts, parts, half, LH, LE, RH, RE, pbest, sc.gap_open, sc.gap_extend,
@@ -1057,6 +1106,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_grid") g_tuning.grida = value;
     else if (n == "affine_asm") g_tuning.affasm = value;
     else if (n == "ring_slots") g_tuning.ring_slots = value;
+    else if (n == "affine_transpose") g_tuning.afft = value;
     else return -1;
     return 0;
 }

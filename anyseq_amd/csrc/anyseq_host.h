@@ -54,6 +54,7 @@ struct Tuning {
     int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
     int affasm = 1;  // affine fill: asm steady state (0 = C++ blocks only, diagnostics)
     int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
+    int afft = 1;        // affine construct: run Hirschberg halves taller than wide transposed
 };
 extern Tuning g_tuning;
 
@@ -90,6 +91,8 @@ struct Engine {
     std::vector<int32_t> host_i32;
     std::vector<BlockInfo> host_blocks;
     std::vector<PartInfo> host_parts;
+    std::vector<uint8_t> host_jobs;
+    DevBuf jobs;
     explicit Engine(int dev);
 };
 

@@ -30,7 +30,7 @@ struct DPProblem {
     int32_t wpad;          // row-buffer pitch (multiple of 64, >= w)
     int32_t nslots;        // hand-off rows in the ring: group k writes slot k % nslots
     int32_t* out_col;      // optional: H[r][w-1] for r in [0,h)
-    int32_t* out_row;      // optional: raw (kernel value space) bottom row, >= wpad ints
+    int32_t* out_row;      // optional: raw (kernel value space) bottom row, >= wpad ints (affine: G, F-down)
     int32_t* rowbuf;       // nslots * wpad ints: ring of group -> group hand-off rows
     uint32_t* flags;       // ngroups entries, chunk progress of each group's last band
     int32_t* best;         // optional (local): atomicMax of every cell
@@ -70,9 +70,15 @@ struct DPProblem {
 //              and left -inf, top row with the open);
 //   FREE_LOCAL local: every border 0 (with the clamp, amode bit 0);
 //   FREE_SEMI  semiglobal inside the matrix: top 0, left -inf;
-//   FREE_SEMI_OPEN semiglobal at the matrix's left edge: top and left 0.
-enum : int32_t { BM_NORMAL = 0, BM_EFREE = 1, BM_EPAID = 2, BM_FREE_LOCAL = 3, BM_FREE_SEMI = 4, BM_FREE_SEMI_OPEN = 5 };
-enum : int32_t { AM_CLAMP = 1, AM_BEST_ALL = 2, AM_BEST_LAST = 4 };
+//   FREE_SEMI_OPEN semiglobal at the matrix's left edge: top and left 0;
+//   FFREE, FPAID, FREE_SEMI_T: EFREE, EPAID, FREE_SEMI of a TRANSPOSED problem
+//              (query and subject swapped: the top and left borders trade places).
+enum : int32_t {
+    BM_NORMAL = 0, BM_EFREE = 1, BM_EPAID = 2, BM_FREE_LOCAL = 3, BM_FREE_SEMI = 4, BM_FREE_SEMI_OPEN = 5,
+    BM_FFREE = 6, BM_FPAID = 7, BM_FREE_SEMI_T = 8
+};
+// amode: clamp; best of every cell / of the last row / of the last column
+enum : int32_t { AM_CLAMP = 1, AM_BEST_ALL = 2, AM_BEST_LAST = 4, AM_BEST_LASTCOL = 6 };
 // Split boundary types of the affine construct (oracle T_*).
 enum : int32_t { T_H = 0, T_E = 1, T_BEFORE = 2, T_AFTER = 3 };
 

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "anyseq_internal.h"
 
 namespace anyseq {
@@ -1036,12 +1038,12 @@ struct AffBorder {
     int cg, tg, lg;
     bool tfree, lfree;
     __device__ AffBorder(int bm, int go) {
-        const bool neg_corner = bm == BM_EFREE || bm == BM_EPAID;
-        cg = neg_corner ? kAffNeg : 0;
-        tfree = bm >= BM_FREE_LOCAL;
-        tg = bm == BM_EFREE ? 0 : go;
-        lfree = bm == BM_FREE_LOCAL || bm == BM_FREE_SEMI_OPEN;
-        lg = bm == BM_NORMAL ? go : kAffNeg;
+        // the transposed modes (FFREE, FPAID, FREE_SEMI_T) swap the top and left borders
+        cg = (bm == BM_EFREE || bm == BM_EPAID || bm == BM_FFREE || bm == BM_FPAID) ? kAffNeg : 0;
+        tfree = bm == BM_FREE_LOCAL || bm == BM_FREE_SEMI || bm == BM_FREE_SEMI_OPEN;
+        lfree = bm == BM_FREE_LOCAL || bm == BM_FREE_SEMI_T || bm == BM_FREE_SEMI_OPEN;
+        tg = bm == BM_EFREE ? 0 : (bm == BM_NORMAL || bm == BM_EPAID) ? go : kAffNeg;
+        lg = bm == BM_FFREE ? 0 : (bm == BM_NORMAL || bm == BM_FPAID) ? go : kAffNeg;
     }
     __device__ int top(int c, int nge) const { return c < 0 ? cg : (tfree ? (c + 1) * nge : tg); }
     __device__ int left(int r, int nge) const { return r < 0 ? cg : (lfree ? (r + 1) * nge : lg); }
@@ -1080,13 +1082,12 @@ struct AffIO {
 // t0 - 1, rv[u] = top row at column t0 + u, zc / zb = clamp bound / true Z_t of the
 // first step (zc is far below zb when the problem does not clamp).
 // MASK: some lanes are outside [0, w).  PARTIAL: rows >= h pass the row above
-// through.  FINOUT: the problem's last row publishes F[h-1][c] (not F-down), as
-// the two-front combine needs.  og/of: this lane's (G, F-out) after each step
-// (lane 63's are the band's bottom row).
-template <bool MASK, bool PARTIAL, bool FINOUT, bool VIRT>
+// through (so lane 63 publishes the last row's G and F-down).  og/of: this lane's
+// (G, F-down) after each step (lane 63's are the band's bottom row).
+template <bool MASK, bool PARTIAL, bool VIRT>
 __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&rv)[32], const uint32_t (&sw)[8], int q,
-                                          bool dead, bool lastrow, int zc, int zb, int& g, int& e, int& hg, int& fdn,
-                                          int& dg, int& best, int (&og)[32], int (&of)[32], const AffK k) {
+                                          bool dead, int zc, int zb, int& g, int& e, int& hg, int& fdn, int& dg,
+                                          int& best, int (&og)[32], int (&of)[32], const AffK k) {
 #pragma unroll
     for (int u = 0; u < 32; ++u) {
         const int2 top = u == 0 ? tf : rv[u - 1];
@@ -1103,7 +1104,6 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
             v = upg;
             fn = fin;
         }
-        if (FINOUT && lastrow) fn = fin;
         // VIRT: columns < 0 are virtual and computed like real ones
         const bool act = MASK ? (VIRT ? (c0 + u < w) : ((unsigned)(c0 + u) < (unsigned)w)) : true;
         // branch-free masking: inactive lanes keep their state
@@ -1174,7 +1174,7 @@ __device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint3
 }
 #undef AFF_ASM
 
-template <bool PARTIAL, bool FINOUT>
+template <bool PARTIAL>
 __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k) {
     constexpr int CH = 32;
     constexpr int IRM = kSlots * CH - 1;
@@ -1194,7 +1194,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     // so column -1 computes G = F = go, the left border, and E at column 0 = 2 go, as
     // the oracle's.  The prologue then runs in the asm loop.  Other borders keep the
     // masked C++ prologue.
-    constexpr bool VIRT_OK = !PARTIAL && !FINOUT;
+    constexpr bool VIRT_OK = !PARTIAL;
     // (not with a best-cell output: the virtual border column would count as a cell)
     const bool virt = VIRT_OK && bm == BM_NORMAL && !shard_left && !(amode & (AM_BEST_ALL | AM_BEST_LAST));
     const int rb = band * 64;
@@ -1332,16 +1332,16 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         const bool full = (virt || t0 >= 64) && b < fe;
         if (full) {
             if (virt)
-                aff_block<false, PARTIAL, FINOUT, true>(c0, w, tf, rv, sw, q, dead, lastrow, zc, zb, g, e, hg, fdn,
+                aff_block<false, PARTIAL, true>(c0, w, tf, rv, sw, q, dead, zc, zb, g, e, hg, fdn,
                                                         dg, best, og, of, k);
             else
-                aff_block<false, PARTIAL, FINOUT, false>(c0, w, tf, rv, sw, q, dead, lastrow, zc, zb, g, e, hg, fdn,
+                aff_block<false, PARTIAL, false>(c0, w, tf, rv, sw, q, dead, zc, zb, g, e, hg, fdn,
                                                          dg, best, og, of, k);
         } else if (virt) {
-            aff_block<true, PARTIAL, FINOUT, true>(c0, w, tf, rv, sw, q, dead, lastrow, zc, zb, g, e, hg, fdn, dg,
+            aff_block<true, PARTIAL, true>(c0, w, tf, rv, sw, q, dead, zc, zb, g, e, hg, fdn, dg,
                                                    best, og, of, k);
         } else {   // masked prologue / epilogue (also a shard's received border column)
-            aff_block<true, PARTIAL, FINOUT, false>(c0, w, tf, rv, sw, q, dead, lastrow, zc, zb, g, e, hg, fdn, dg,
+            aff_block<true, PARTIAL, false>(c0, w, tf, rv, sw, q, dead, zc, zb, g, e, hg, fdn, dg,
                                                     best, og, of, k);
         }
         tf = rv[CH - 1];
@@ -1379,12 +1379,14 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     if (!dead) {
         if (P.out_col) gmem(P.out_col)[row] = aff_to_h(g, row, w - 1, nge);
         if (P.out_col_e) gmem(P.out_col_e)[row] = aff_to_h(e, row, w - 1, nge);
-        // shard: F of the last row at the last column (the combine pairs it across shards)
+        // shard: F-down of the last row at the last column (the combine pairs it across shards)
         if (lastrow && P.out_f_last) *gmem(P.out_f_last) = aff_to_h(fdn, row, w - 1, nge);
     }
     if (P.progress && !publish_progress(P, band, lane, err)) return;
     if (bestmode && P.best) {
-        // the lane's best covers its row; last-row mode keeps the problem's last row only
+        // the lane's best covers its row; last-row mode keeps the problem's last row only,
+        // last-column mode the lane's cell in the last column
+        if (bestmode == 3) best = aff_to_h(g, row, w - 1, nge);
         if (dead || (bestmode == 2 && !lastrow)) best = kAffNeg;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
@@ -1451,15 +1453,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                 io.next_prod = band < last ? &sh.prod[wave + 1] : nullptr;
                 io.next_cons = band < last ? &sh.cons[wave + 1] : nullptr;
                 io.gout = band < last ? nullptr : g_out;
-                const bool partial = (band + 1) * 64 > P.h;
-                const bool finout = band == P.nbands - 1 && P.out_row != nullptr;
-                if (partial) {
-                    if (finout) run_band_aff<true, true>(P, band, lane, io, err, k);
-                    else run_band_aff<true, false>(P, band, lane, io, err, k);
-                } else {
-                    if (finout) run_band_aff<false, true>(P, band, lane, io, err, k);
-                    else run_band_aff<false, false>(P, band, lane, io, err, k);
-                }
+                if ((band + 1) * 64 > P.h) run_band_aff<true>(P, band, lane, io, err, k);
+                else run_band_aff<false>(P, band, lane, io, err, k);
             }
         }
         __syncthreads();
@@ -1471,7 +1466,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
 // column and 0.  Two fronts (top rows [0,h1) forward, bottom rows [h1,n) reversed):
 // for every split column j in [-1, m-1], with jb = m-2-j,
 //     max(Ht[j] + Hb[jb], Ft[j] + Fb[jb] - go)
-// (F = vertical-gap state of the last row; a vertical gap across the split is
+// (F = the last row's F-down, max(F, H + go): the maximum is that of the exact F
+// join, whose extra terms never exceed Ht + Hb; a vertical gap across the split is
 // opened once), plus the semiglobal end columns / the local best cells.
 __global__ void aff_reduce_kernel(int kind, int two, const int2* __restrict__ rowF, int h1,
                                   const int2* __restrict__ rowB, int h2, int m, int go, int ge,
@@ -1994,6 +1990,28 @@ __global__ __launch_bounds__(256) void aff_hb_join_kernel(const PartInfo* __rest
     }
 }
 
+// Transposed Hirschberg halves: the bottom row (G, F-down) of
+// the transposed problem is the original's last column (H, E-right) -> H space.
+// E-right = max(E, H + go) instead of E changes no join decision: an E candidate
+// that only its H + go term lifts never exceeds the H candidate of its row, which
+// is tried first.
+struct RowToCol {
+    const int2* row;
+    int32_t* H;
+    int32_t* E;
+    int32_t n;      // columns of the transposed problem (rows of the original)
+    int32_t hlast;  // last row of the transposed problem
+};
+__global__ void aff_row_to_col_kernel(const RowToCol* __restrict__ jobs, int nge) {
+    const RowToCol J = jobs[blockIdx.y];
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < J.n; c += blockDim.x * gridDim.x) {
+        const int2 v = J.row[c];
+        const int z = (J.hlast + c + 2) * nge;
+        J.H[c] = v.x - z;
+        J.E[c] = v.y - z;
+    }
+}
+
 // Final level: Gotoh with predecessor bytes for one 128-column block per wave,
 // the geometry of pred_kernel (lane l owns columns 2l, 2l+1, anti-diagonal
 // sweep, byte pred[base + (i+j)*128 + j]).  Byte: bits 0-1 H source (0 diag,
@@ -2309,6 +2327,13 @@ hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, co
     if (nparts > 0)
         hipLaunchKernelGGL(anyseq::aff_hb_join_kernel, dim3(nparts), dim3(256), 0, st,
                            (const anyseq::PartInfo*)parts, half, LH, LE, RH, RE, pbest, go, ge, splits, types, score);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_aff_row_to_col(const void* jobs, int njobs, int maxn, int nge, hipStream_t st) {
+    if (njobs > 0)
+        hipLaunchKernelGGL(anyseq::aff_row_to_col_kernel, dim3(std::max(1, std::min(64, (maxn + 255) / 256)), njobs),
+                           dim3(256), 0, st, (const anyseq::RowToCol*)jobs, nge);
     return hipGetLastError();
 }
 

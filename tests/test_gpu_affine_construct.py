@@ -66,3 +66,21 @@ def test_affine_construct_multi_group(anyseq, oracle, kind):
     same(anyseq, oracle, kind, base, bytes(mut[100:2900]), (2, -1, -3, -1))
     same(anyseq, oracle, kind, rnd(rng, 2500), rnd(rng, 2100), (2, -1, -2, -1))
     same(anyseq, oracle, kind, rnd(rng, 60) + base[300:2000] + rnd(rng, 90), base, (1, -3, -5, -2))
+
+
+@pytest.mark.parametrize("transpose", [0, 1])
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_construct_transposed_halves(anyseq, oracle, kind, transpose):
+    """Hirschberg halves run transposed when taller than wide (affine_transpose 1, the
+    default) or as they are (0): the same strings either way.  Shapes: tall, wide,
+    square, and local alignments in a corner (free ends through several levels)."""
+    rng = random.Random(55 + transpose)
+    anyseq.set_option("affine_transpose", transpose)
+    try:
+        core = rnd(rng, 700)
+        cases = [(rnd(rng, 3000), rnd(rng, 400)), (rnd(rng, 300), rnd(rng, 2600)), (rnd(rng, 1500), rnd(rng, 1500)),
+                 (rnd(rng, 2000) + core, core + rnd(rng, 300)), (core[:500] + rnd(rng, 1800), rnd(rng, 900) + core)]
+        for i, (q, s) in enumerate(cases):
+            same(anyseq, oracle, kind, q, s, SCHEMES[i % len(SCHEMES)])
+    finally:
+        anyseq.set_option("affine_transpose", 1)
