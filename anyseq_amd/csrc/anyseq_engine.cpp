@@ -306,7 +306,8 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.gap_extend = sc.gap_extend;
     fp.affine = sc.gap_open != 0;
     fp.dbg = nullptr;
-    fp.pad = (g_tuning.affasm & 1) ? (g_tuning.affasm & 2) : (1 | (g_tuning.affasm & 2));  // affine_asm bit0: asm steady state, bit1: scalar row stores (diagnostics)
+    // affine_asm bit 0: asm steady state, bit 1: scalar row stores, bit 2: asm prologue (diagnostics)
+    fp.pad = ((g_tuning.affasm & 1) ? 0 : 1) | (g_tuning.affasm & 2) | ((g_tuning.affasm & 4) ? 0 : 4);
     return fp;
 }
 

@@ -1028,7 +1028,7 @@ struct AffK {
     int wm, wx;   // diagonal weight sub - 2 ge
     int go;       // gap open (<= 0): added to a cell to open a gap (G space)
     int nge;      // -ge > 0
-    int flags;    // bit 0: no asm steady state (diagnostics)
+    int flags;    // bit 0: no asm steady state, bit 2: no asm prologue (diagnostics)
 };
 
 // Borders of a problem in G space (H border values by border mode, see
@@ -1172,6 +1172,40 @@ __device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint3
     tf = make_int2(tfg, tff);
     return st;
 }
+
+// Blocks 0 and 1 of a band without virtual lanes (tools/gen_block_asm.py,
+// gen_prologue_aff): the steady-state steps under a growing exec mask.
+template <bool L, bool BORDER, bool TRAIL>
+__device__ __forceinline__ uint32_t aff_prologue_asm(uint32_t& sp, uint32_t& sf, uint32_t& sc,
+                                                     const AffLoopArgs& la, int q, int& g, int& fdn, int& dg,
+                                                     int2& tf, int& e, int& hg, int& best, uint32_t& z, uint32_t& zb,
+                                                     const AffK& k) {
+    uint32_t st, x0, x1, x2, x3, x4, b = 0, be = 2;
+    const uint64_t hm = 0xffffffff00000000ull;
+#define RFL(x) __builtin_amdgcn_readfirstlane(x)
+    sp = RFL(sp);
+    sf = RFL(sf);
+    sc = RFL(sc);
+    z = RFL(z);
+    zb = RFL(zb);
+    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), nge = RFL(k.nge);
+    const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
+#undef RFL
+    int tfg = tf.x, tff = tf.y;
+    if constexpr (L) {
+        if constexpr (BORDER && TRAIL) AFF_ASM(ANYSEQ_AFFP_L_B1_T1);
+        if constexpr (BORDER && !TRAIL) AFF_ASM(ANYSEQ_AFFP_L_B1_T0);
+        if constexpr (!BORDER && TRAIL) AFF_ASM(ANYSEQ_AFFP_L_B0_T1);
+        if constexpr (!BORDER && !TRAIL) AFF_ASM(ANYSEQ_AFFP_L_B0_T0);
+    } else {
+        if constexpr (BORDER && TRAIL) AFF_ASM(ANYSEQ_AFFP_G_B1_T1);
+        if constexpr (BORDER && !TRAIL) AFF_ASM(ANYSEQ_AFFP_G_B1_T0);
+        if constexpr (!BORDER && TRAIL) AFF_ASM(ANYSEQ_AFFP_G_B0_T1);
+        if constexpr (!BORDER && !TRAIL) AFF_ASM(ANYSEQ_AFFP_G_B0_T0);
+    }
+    tf = make_int2(tfg, tff);
+    return st;
+}
 #undef AFF_ASM
 
 template <bool PARTIAL>
@@ -1256,6 +1290,37 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
         if constexpr (VIRT_OK) {
+            if (b == 0 && !virt && !shard_left && fe >= 2 && !(k.flags & 5)) {
+                // blocks 0, 1 in asm under a growing exec mask (no virtual lanes)
+                uint32_t zb = (uint32_t)((rb + 1) * nge);
+                uint32_t z = zb + (uint32_t)zoff;
+                const int role = (io.in_border ? 2 : 0) + (io.trailing ? 1 : 0);
+                uint32_t st = 0;
+#define AP_CALL(LV, BD, TR) \
+    st = aff_prologue_asm<LV, BD, TR>(seen_prod, seen_sfill, seen_cons, la, q, g, fdn, dg, tf, e, hg, best, z, zb, k)
+                if (amode) {
+                    switch (role) {
+                        case 0: AP_CALL(true, false, false); break;
+                        case 1: AP_CALL(true, false, true); break;
+                        case 2: AP_CALL(true, true, false); break;
+                        default: AP_CALL(true, true, true); break;
+                    }
+                } else {
+                    switch (role) {
+                        case 0: AP_CALL(false, false, false); break;
+                        case 1: AP_CALL(false, false, true); break;
+                        case 2: AP_CALL(false, true, false); break;
+                        default: AP_CALL(false, true, true); break;
+                    }
+                }
+#undef AP_CALL
+                if (st) {
+                    atomicOr(err, ERR_SPIN_TIMEOUT);
+                    return;
+                }
+                b = 1;   // ++b of the for: the steady state from block 2
+                continue;
+            }
             if ((virt || t0 >= 64) && b < fe && !(k.flags & 1)) {
                 uint32_t bb = (uint32_t)b;
                 uint32_t zb = (uint32_t)((rb + t0 + 1) * nge);

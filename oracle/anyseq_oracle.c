@@ -931,8 +931,23 @@ static inline int free_bm(int kind, int at_edge) {
 }
 
 
-static void aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8_t* S, Index m, const AffSc* sc,
-                             char* alq, char* als) {
+/* One half fill of a Hirschberg level (the tasks of a level are independent and
+ * run on g_threads threads, as the HIP path runs them in one launch). */
+typedef struct {
+    Acc q, s; Index h, w; int bm; Score *colH, *colE; Score best_all, best_last;
+} HalfTask;
+typedef struct { HalfTask* t; const AffSc* sc; } HalfCtx;
+static void half_body(void* p, Index i) {
+    HalfCtx* c = (HalfCtx*)p;
+    HalfTask* t = &c->t[i];
+    aff_fill(t->q, t->h, t->s, t->w, c->sc, t->bm, t->colH, t->colE, &t->best_all, &t->best_last);
+}
+
+/* Returns the level-1 join value (the optimal score; semiglobal: with the empty
+ * alignment's 0) or INT64_MIN when m <= 128 (no level); writes the alignment
+ * unless a local / semiglobal level-1 value is <= 0 (the empty alignment). */
+static int64_t aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8_t* S, Index m, const AffSc* sc,
+                                char* alq, char* als) {
     const Index nb = round_up_div(m, MIN_PART_WIDTH_HB);
     IVec spl, typ;
     spl.n = nb; typ.n = nb;
@@ -946,10 +961,36 @@ static void aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8_t*
     Index bpp = pw / MIN_PART_WIDTH_HB;
     Score *LH = (Score*)malloc(sizeof(Score) * (size_t)(n + 1)), *LE = (Score*)malloc(sizeof(Score) * (size_t)(n + 1));
     Score *RH = (Score*)malloc(sizeof(Score) * (size_t)(n + 1)), *RE = (Score*)malloc(sizeof(Score) * (size_t)(n + 1));
+    HalfTask* tasks = (HalfTask*)malloc(sizeof(HalfTask) * (size_t)(2 * nb + 2));
+    Index* tpart = (Index*)malloc(sizeof(Index) * (size_t)(nb + 1));   /* part -> its first task, -1: none */
+    int64_t score = INT64_MIN;
+    int level1 = 1;
     while (pw > MIN_PART_WIDTH_HB) {
         const Index half = pw / 2;
         const Index parts = (m + half - 1) / pw;
-        for (Index p = 0; p < parts; ++p) {
+        Index nt = 0;
+        for (Index p = 0; p < parts; ++p) {   /* this level's half fills */
+            const Index sb = p * bpp - 1, eb = imin((p + 1) * bpp - 1, nb - 1);
+            const int ts = IV(typ, sb), te = IV(typ, eb);
+            tpart[p] = -1;
+            if (ts == T_BEFORE || te == T_AFTER) continue;
+            if (IV(spl, sb) == SPLIT_UNSET || IV(spl, eb) == SPLIT_UNSET) { g_error = 1; continue; }
+            const Index off = IV(spl, sb), len = IV(spl, eb) - off;
+            if (len <= 0) continue;
+            const Index hoj_l = p * pw, hoj_r = p * pw + half, hw = imin(half, m - hoj_r);
+            tpart[p] = nt;
+            HalfTask* L = &tasks[nt++];
+            L->q = (Acc){Q, off, 1}; L->s = (Acc){S, hoj_l, 1}; L->h = len; L->w = half;
+            L->bm = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, hoj_l == 0);
+            L->colH = LH + off; L->colE = LE + off;
+            HalfTask* R = &tasks[nt++];
+            R->q = (Acc){Q, off + len - 1, -1}; R->s = (Acc){S, hoj_r + hw - 1, -1}; R->h = len; R->w = hw;
+            R->bm = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : free_bm(kind, hoj_r + hw == m);
+            R->colH = RH + off; R->colE = RE + off;
+        }
+        HalfCtx hc = {tasks, sc};
+        parallel_for(0, nt, half_body, &hc);
+        for (Index p = 0; p < parts; ++p) {   /* joins */
             const Index sb = p * bpp - 1, eb = imin((p + 1) * bpp - 1, nb - 1), mid = p * bpp + bpp / 2 - 1;
             const int ts = IV(typ, sb), te = IV(typ, eb);
             if (ts == T_BEFORE || te == T_AFTER) {   /* empty part: so are both halves */
@@ -965,14 +1006,11 @@ static void aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8_t*
             const int rbm = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : free_bm(kind, hoj_r + hw == m);
             const int sfree = ts == T_AFTER, efree = te == T_BEFORE;
             Score bestL = ANEG, bestR = ANEG;
-            if (len > 0) {
-                Score ba, bl;
-                Acc qa = {Q, off, 1}, sa = {S, hoj_l, 1};
-                aff_fill(qa, len, sa, half, sc, lbm, LH + off, LE + off, &ba, &bl);
-                if (efree) bestL = kind == SCHEME_LOCAL ? ba : bl;
-                Acc qr = {Q, off + len - 1, -1}, sr = {S, hoj_r + hw - 1, -1};
-                aff_fill(qr, len, sr, hw, sc, rbm, RH + off, RE + off, &ba, &bl);
-                if (sfree) bestR = kind == SCHEME_LOCAL ? ba : bl;
+            if (tpart[p] >= 0) {
+                const HalfTask* L = &tasks[tpart[p]];
+                const HalfTask* R = L + 1;
+                if (efree) bestL = kind == SCHEME_LOCAL ? L->best_all : L->best_last;
+                if (sfree) bestR = kind == SCHEME_LOCAL ? R->best_all : R->best_last;
             }
             /* index -1: the halves' top borders at the midline (a FREE top border is no gap) */
             const Score bLH = bm_top(lbm, sc, half - 1), bLE = sfree ? ANEG : bLH;
@@ -991,7 +1029,10 @@ static void aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8_t*
             }
             IV(typ, mid) = type;
             IV(spl, mid) = type == T_BEFORE ? off + len : type == T_AFTER ? off : off + idx + 1;
+            if (level1 && p == 0) score = kind == SCHEME_SEMIGLOBAL && best < 0 ? 0 : best;
         }
+        if (level1 && kind != SCHEME_GLOBAL && score <= 0) goto done;   /* the empty alignment */
+        level1 = 0;
         pw /= 2;
         bpp /= 2;
     }
@@ -1005,7 +1046,9 @@ static void aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8_t*
         const int e_end = te == T_H ? 0 : te == T_E ? 1 : 2;
         aff_block_walk(Q, S, oi, h, oj, w, sc, bm, e_end, kind, oj + w == m, alq, als);
     }
-    free(spl.v); free(typ.v); free(LH); free(LE); free(RH); free(RE);
+done:
+    free(spl.v); free(typ.v); free(LH); free(LE); free(RH); free(RE); free(tasks); free(tpart);
+    return score;
 }
 
 /* Rectangle [is, ie] x [js, je] of the last oracle_affine_construct (ie < is: empty). */
@@ -1015,10 +1058,13 @@ int64_t oracle_affine_construct(int kind, const char* qc, int n, const char* sc_
                                 int go, int ge, char* alq, char* als) {
     for (Index i = 0; i < n + m; ++i) { alq[i] = ' '; als[i] = ' '; }
     g_last_rect[0] = 0; g_last_rect[1] = -1; g_last_rect[2] = 0; g_last_rect[3] = -1;
+    AffSc sc = {match, mismatch, go, ge};
+    /* the score: the level-1 join of the Hirschberg (m > 128), else one score fill */
+    if (n > 0 && m > MIN_PART_WIDTH_HB)
+        return aff_construct_hb(kind, (const uint8_t*)qc, n, (const uint8_t*)sc_, m, &sc, alq, als);
     const int64_t score = oracle_affine_score(kind, qc, n, sc_, m, match, mismatch, go, ge, NULL, NULL);
     if (n + m == 0) return score;
     if (kind != SCHEME_GLOBAL && (score <= 0 || n == 0 || m == 0)) return score;   /* the empty alignment */
-    AffSc sc = {match, mismatch, go, ge};
     if (m == 0) {   /* global: all query rows against gaps, down the left border: position i + (-1) + 1 */
         for (Index i = 0; i < n; ++i) { alq[i] = qc[i]; als[i] = '_'; emit_q(i); }
     } else {

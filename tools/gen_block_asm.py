@@ -464,6 +464,114 @@ def gen_loop_aff(kind, border, pub):
     return out
 
 
+def gen_prologue_aff(kind, border, trailing):
+    """Affine prologue: blocks 0 and 1 of a band whose lanes left of column 0 are
+    NOT virtual (any border mode but the scheme's own): the steps of gen_loop_aff
+    under an exec mask that grows by one lane per step (lane l first runs at step
+    l + 1, column 0), so lanes keep their initial border state until they start.
+    The DPPs run on the full exec (5 wait states after the exec write: the step's
+    two leading VALU + s_nop 2) so that a lane's first diagonal is its upper
+    neighbour's initial state; s_bfm_b64 then masks the cell update.  No publishing (the first chunk leaves in
+    block 2); the consumed / tail counters are written with the full exec."""
+    L = kind == "L"
+    out = []
+    e = out.append
+
+    def TG(u):
+        return v(AT0 + 2 * u)
+
+    def TF(u):
+        return v(AT0 + 2 * u + 1)
+
+    def OG(u):
+        return v(AO0 + 2 * u)
+
+    def OF(u):
+        return v(AO0 + 2 * u + 1)
+
+    for k in (0, 1):
+        e(f"s_mov_b32 %[b], {k}")
+        e("s_mov_b32 %[x1], " + str(k + 1))
+        wait(e, f"psf{k}", "%[sf]", "%[x1]", "%[asf]", tmp=AVT2)
+        # this block's subject words (set 0)
+        e(f"s_mov_b32 %[x2], {k << 11}")
+        e(f"v_add_u32_e32 v{AVA}, %[x2], %[skb]")
+        for i in range(4):
+            e(f"ds_read2st64_b32 v[{ASK0 + 2 * i}:{ASK0 + 2 * i + 1}], v{AVA} offset0:{2 * i} offset1:{2 * i + 1}")
+        if border:
+            e(f"s_mov_b32 %[x0], {32 * k}")
+            e("s_mul_i32 %[x2], %[x0], %[bvs]")
+            e(f"v_add_u32_e32 v{AVT}, %[x2], %[bvb]")
+            e(f"v_add_u32_e32 v{AVT + 1}, %[go], v{AVT}")
+            e(f"s_mov_b32 %[x2], {(32 * k) << 3}")
+            e(f"v_add_u32_e32 v{AVA}, %[x2], %[lid8]")
+            e(f"v_and_b32_e32 v{AVA}, 0xfff, v{AVA}")
+            e(f"v_add_u32_e32 v{AVA}, %[rb], v{AVA}")
+            e(f"ds_write_b64 v{AVA}, v[{AVT}:{AVT + 1}]")
+        else:
+            wait(e, f"ppr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=AVT2)
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"s_mov_b32 %[x2], {(k << 8) & 4095}")
+        e("s_add_u32 %[x2], %[x2], %[rb]")
+        e(f"v_mov_b32_e32 v{AVB}, %[x2]")
+        for i in range(16):
+            e(f"ds_read_b128 v[{AT0 + 4 * i}:{AT0 + 4 * i + 3}], v{AVB} offset:{16 * i}")
+        e("s_waitcnt lgkmcnt(0)")
+        # lanes that have not started hold their state in every step register, so
+        # the full-exec DPPs below hand them (and their lower neighbours) the
+        # values of the C++ masked path
+        for u in range(32):
+            e(f"v_mov_b32_e32 {OG(u)}, %[cur]")
+            e(f"v_mov_b32_e32 {OF(u)}, %[fd]")
+        g, f, dg = "%[cur]", "%[fd]", "%[dg]"
+        for u in range(32):
+            t = 32 * k + u
+            sw = v(ASK0 + u // 4)
+            tg = "%[tfg]" if u == 0 else TG(u - 1)
+            tf = "%[tff]" if u == 0 else TF(u - 1)
+            e("s_mov_b64 exec, -1")
+            e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+            e(f"v_cndmask_b32_e32 v{AW}, %[wx], %[wm], vcc")
+            e("s_nop 2")
+            e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
+            # the cell's own update only on the lanes at column >= 0 (lane l from step l + 1)
+            e(f"s_bfm_b64 exec, {t}, 0")
+            e("v_max_i32_e32 %[e], %[e], %[hg]")
+            e(f"v_add_u32_e32 v{AA}, {dg}, v{AW}")
+            e(f"v_max3_i32 {OG(u)}, v{AA}, %[e], {tf}")
+            if L:
+                e(f"v_max_i32_e32 {OG(u)}, %[z], {OG(u)}")
+            e(f"v_add_u32_e32 %[hg], %[go], {OG(u)}")
+            e(f"v_max_i32_e32 {OF(u)}, {tf}, %[hg]")
+            if L:
+                e(f"v_subrev_u32_e32 v{AH}, %[zb], {OG(u)}")
+                e(f"v_max_i32_e32 %[best], %[best], v{AH}")
+                e("s_add_u32 %[z], %[z], %[nge]")
+                e("s_add_u32 %[zb], %[zb], %[nge]")
+            g, f, dg = OG(u), OF(u), tg
+        # state moves under the last step's mask: lanes that have not started keep theirs
+        e(f"v_mov_b32_e32 %[cur], {OG(31)}")
+        e(f"v_mov_b32_e32 %[fd], {OF(31)}")
+        e(f"v_mov_b32_e32 %[dg], {TG(30)}")
+        e(f"v_mov_b32_e32 %[tfg], {TG(31)}")
+        e(f"v_mov_b32_e32 %[tff], {TF(31)}")
+        e("s_mov_b64 exec, -1")
+        e(f"v_mov_b32_e32 v{AVT2}, %[x1]")
+        if not border:
+            e(f"ds_write_b32 %[acn], v{AVT2}")
+        if trailing:
+            e(f"ds_write_b32 %[atl], v{AVT2}")
+    e("s_mov_b32 %[b], 2")
+    e("s_mov_b32 %[st], 0")
+    e("s_branch L_end_%=")
+    e("L_timeout_%=:")
+    e("s_mov_b64 exec, -1")
+    e("s_mov_b32 %[st], 1")
+    e("L_end_%=:")
+    return out
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
     dst = os.path.join(here, "..", "anyseq_amd", "csrc", "anyseq_block_asm.inc")
@@ -496,6 +604,14 @@ def main():
                 name = f"ANYSEQ_AFF_{kind}_B{border}_{pub.upper()}"
                 lines.append(f"#define {name} \\")
                 for ln in gen_loop_aff(kind, border, pub):
+                    lines.append(f'    "{ln}\\n" \\')
+                lines.append("")
+    for kind in ("G", "L"):
+        for border in (0, 1):
+            for trailing in (0, 1):
+                name = f"ANYSEQ_AFFP_{kind}_B{border}_T{trailing}"
+                lines.append(f"#define {name} \\")
+                for ln in gen_prologue_aff(kind, border, trailing):
                     lines.append(f'    "{ln}\\n" \\')
                 lines.append("")
     clob = ", ".join(f'"v{n}"' for n in range(AT0, AVB + 1))
