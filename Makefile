@@ -24,7 +24,7 @@ $(SRC)/anyseq_io.o: $(SRC)/anyseq_io.cpp include/anyseq.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(SRC)/anyseq_kernels.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -Wl,-z,defs -o $@ $^ -L/opt/rocm/lib -lrccl
+	$(HIPCC) --offload-arch=$(ARCH) -shared -Wl,-z,defs -o $@ $^ -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
 oracle:
 	$(MAKE) -s -C oracle

@@ -3,8 +3,10 @@
 // (the reference's column-split Hirschberg, align.impala:237-311,
 // traceback_lintime.impala:1-148) over the HIP kernels of anyseq_kernels.hip.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -79,7 +81,8 @@ void set_last_error(const std::string& m) { g_last_error = m; }
 void* DevBuf::get(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes > cap) {
-        if (p) HIPCHECK(hipFree(p));
+        static const int no_free = env_int("ANYSEQ_NO_FREE", 0);
+        if (p && !no_free) HIPCHECK(hipFree(p));
         p = nullptr;
         size_t c = std::max(bytes, cap * 3 / 2);
         c = (c + 255) & ~size_t(255);
@@ -100,7 +103,51 @@ void FillCtx::init() {
     if (!ev1) HIPCHECK(hipEventCreate(&ev1));
 }
 
+// Diagnostics (ANYSEQ_FAULT_INFO=1): report the address of a GPU memory fault and the
+// engine buffer it falls in or next to (the HIP runtime itself prints no address).
+namespace {
+struct NamedBuf {
+    const char* name;
+    const DevBuf* buf;
+};
+std::vector<NamedBuf> g_named;
+
+hsa_status_t fault_handler(const hsa_amd_event_t* ev, void*) {
+    if (ev->event_type != HSA_AMD_GPU_MEMORY_FAULT_EVENT) return HSA_STATUS_SUCCESS;
+    const uint64_t a = ev->memory_fault.virtual_address;
+    fprintf(stderr, "anyseq: GPU memory fault at 0x%llx, reason mask 0x%x\n", (unsigned long long)a,
+            ev->memory_fault.fault_reason_mask);
+    for (const NamedBuf& nb : g_named) {
+        const uint64_t p = (uint64_t)(size_t)nb.buf->p;
+        if (!p) continue;
+        const long long d = (long long)(a - p);
+        if (d >= -(1ll << 16) && d < (long long)nb.buf->cap + (1ll << 16))
+            fprintf(stderr, "anyseq:   %-8s %p + %zu: fault at offset %lld\n", nb.name, nb.buf->p, nb.buf->cap, d);
+    }
+    return HSA_STATUS_SUCCESS;
+}
+std::mutex g_named_mu;
+}  // namespace
+
+void register_fault_buf(const char* name, const DevBuf* b) {
+    if (!env_int("ANYSEQ_FAULT_INFO", 0)) return;
+    std::lock_guard<std::mutex> lk(g_named_mu);
+    g_named.push_back(NamedBuf{name, b});
+}
+
 Engine::Engine(int dev) : device(dev) {
+    if (env_int("ANYSEQ_FAULT_INFO", 0)) {
+        const NamedBuf nb[] = {{"q", &q},       {"s", &s},         {"outcol", &outcol}, {"outrow", &outrow},
+                               {"L", &L},       {"R", &R},         {"LE", &LE},         {"RE", &RE},
+                               {"spl", &spl},   {"typ", &typ},     {"parts", &parts},   {"bmax", &bmax},
+                               {"bind", &bind}, {"blocks", &blocks}, {"pred", &pred},   {"alq", &alq},
+                               {"als", &als},   {"pos", &pos},     {"jobs", &jobs},     {"fc.probs", &fc.probs},
+                               {"fc.groups", &fc.groups}, {"fc.rowbuf", &fc.rowbuf}, {"fc.flags", &fc.flags},
+                               {"fc.ctr", &fc.ctr}};
+        std::lock_guard<std::mutex> lk(g_named_mu);
+        g_named.insert(g_named.end(), std::begin(nb), std::end(nb));
+        hsa_amd_register_system_event_handler(fault_handler, nullptr);
+    }
     HIPCHECK(hipSetDevice(dev));
     hipDeviceProp_t prop;
     HIPCHECK(hipGetDeviceProperties(&prop, dev));
@@ -115,15 +162,22 @@ int g_device = -1;
 Tuning g_tuning;
 bool g_tuning_init = false;
 
+// Tuning knobs from the environment, once, before the first use or change.
+void init_tuning_locked() {
+    if (g_tuning_init) return;
+    g_tuning.R = env_int("ANYSEQ_R", g_tuning.R);
+    g_tuning.NW = env_int("ANYSEQ_NW", g_tuning.NW);
+    g_tuning.CH = env_int("ANYSEQ_CH", g_tuning.CH);
+    g_tuning.grid = env_int("ANYSEQ_GRID", g_tuning.grid);
+    g_tuning.fronts = env_int("ANYSEQ_FRONTS", g_tuning.fronts);
+    g_tuning.affasm = env_int("ANYSEQ_AFFINE_ASM", g_tuning.affasm);
+    g_tuning.afft = env_int("ANYSEQ_AFFINE_TRANSPOSE", g_tuning.afft);
+    g_tuning_init = true;
+}
+
 Engine& engine() {
     std::lock_guard<std::mutex> lk(g_engines_mu);
-    if (!g_tuning_init) {
-        g_tuning.R = env_int("ANYSEQ_R", g_tuning.R);
-        g_tuning.NW = env_int("ANYSEQ_NW", g_tuning.NW);
-        g_tuning.CH = env_int("ANYSEQ_CH", g_tuning.CH);
-        g_tuning.grid = env_int("ANYSEQ_GRID", g_tuning.grid);
-        g_tuning_init = true;
-    }
+    init_tuning_locked();
     if (g_device < 0) g_device = env_int("ANYSEQ_DEVICE", 0);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) fail("no HIP device available (hipGetDeviceCount)");
@@ -182,6 +236,9 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     int32_t* rowbuf = (int32_t*)C.rowbuf.get(rowbuf_ints * 4);
     uint32_t* flags = (uint32_t*)C.flags.get((flag_words + 4) * 4);
     size_t ro = 0, fo = 0;
+    static std::atomic<int32_t> g_epoch{0};
+    const int32_t epoch = (g_epoch.fetch_add(1) + 1) & 0x7ffff;
+    for (size_t i = 0; i < probs.size(); ++i) probs[i].magic = kProbMagic ^ (int32_t)i ^ (epoch << 12);
     for (auto& P : probs) {
         P.rowbuf = rowbuf + ro;
         P.flags = flags + fo;
@@ -193,7 +250,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     groups.clear();
     for (int k = 0; k < max_groups; ++k)
         for (size_t p = 0; p < probs.size(); ++p)
-            if (k < probs[p].ngroups) groups.push_back(GroupRef{(int32_t)p, k});
+            if (k < probs[p].ngroups) groups.push_back(GroupRef{(int32_t)p, k, epoch, 0});
     C.R = R;
     C.NW = NW;
     if (groups.empty()) {
@@ -213,6 +270,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     uint32_t* ctr = (uint32_t*)C.ctr.get(128);
     HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));  // ctr[0] = dequeue counter, ctr[1] = error word
     FillParams fpl = fp;
+    fpl.epoch = epoch;
     unsigned long long* dbg = nullptr;
     static DevBuf stamp_buf;
     if (getenv("ANYSEQ_STAMPS")) {
@@ -250,10 +308,56 @@ void fill_async(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fill
     fill_launch(C);
 }
 
+// Launch context for error messages: the stage label and the shapes of the launch's
+// first problems, so a device fault names what was running.
+thread_local const char* g_stage = "fill";
+thread_local int g_stage_level = -1;
+
+std::string fill_summary(const FillCtx& C) {
+    char buf[160];
+    snprintf(buf, sizeof buf, "%s level %d, %s fill of %zu problem(s), grid %d:", g_stage, g_stage_level,
+             C.aff ? "affine" : "linear", C.h_probs.size(), C.grid);
+    std::string s = buf;
+    snprintf(buf, sizeof buf, " buffers: probs %p groups %p rowbuf %p+%zu flags %p ctr %p;", C.probs.p, C.groups.p,
+             C.rowbuf.p, C.rowbuf.cap, C.flags.p, C.ctr.p);
+    s += buf;
+    for (size_t i = 0; i < C.h_probs.size() && i < 6; ++i) {
+        const DPProblem& P = C.h_probs[i];
+        snprintf(buf, sizeof buf, " [%dx%d q%+d@%d s%+d@%d bm%d am%d]", P.h, P.w, P.q_step, P.q_off, P.s_step,
+                 P.s_off, P.bmode, P.amode);
+        s += buf;
+    }
+    return s;
+}
+
+void stage_check(hipStream_t st, const char* what) {
+    static const int on = env_int("ANYSEQ_DEBUG_SYNC", 0);
+    if (!on) return;
+    const hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) fail("%s (%s level %d) failed: %s", what, g_stage, g_stage_level, hipGetErrorString(e));
+}
+
 void fill_finish(FillCtx& C) {
     const int R = C.R, NW = C.NW;
     unsigned long long* dbg = C.stamps;
-    HIPCHECK(hipEventSynchronize(C.ev1));
+    {
+        const hipError_t e = hipEventSynchronize(C.ev1);
+        if (e != hipSuccess) {
+            if (const char* path = getenv("ANYSEQ_FAIL_DUMP")) {   // every problem of the failed launch
+                if (FILE* f = fopen(path, "w")) {
+                    fprintf(f, "# %s\n", fill_summary(C).c_str());
+                    for (const DPProblem& P : C.h_probs)
+                        fprintf(f, "%d %d q=%p %d %d s=%p %d %d bm=%d am=%d out_row=%p out_col=%p out_col_e=%p best=%p "
+                                   "rowbuf=%p nslots=%d wpad=%d nbands=%d ngroups=%d\n",
+                                P.h, P.w, (const void*)P.q, P.q_off, P.q_step, (const void*)P.s, P.s_off, P.s_step,
+                                P.bmode, P.amode, (void*)P.out_row, (void*)P.out_col, (void*)P.out_col_e,
+                                (void*)P.best, (void*)P.rowbuf, P.nslots, P.wpad, P.nbands, P.ngroups);
+                    fclose(f);
+                }
+            }
+            fail("fill failed: %s (%s)", hipGetErrorString(e), fill_summary(C).c_str());
+        }
+    }
     float ms = 0.f;
     HIPCHECK(hipEventElapsedTime(&ms, C.ev0, C.ev1));
     g_fill_ms += ms;
@@ -287,6 +391,7 @@ void fill_finish(FillCtx& C) {
             }
         }
     }
+    if (err & ERR_BAD_DESC) fail("fill kernel read a corrupt problem descriptor (error %u; %s)", err, fill_summary(C).c_str());
     if (err) fail("fill kernel reported error %u (spin timeout)", err);
 }
 
@@ -723,9 +828,14 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     auto tp = [&](int idx) { return typ[idx + 1]; };
     int64_t score = INT64_MIN;
     bool level1 = true;
+    struct StageScope {
+        StageScope() { g_stage = "affine construct", g_stage_level = 0; }
+        ~StageScope() { g_stage = "fill", g_stage_level = -1; }
+    } stage_scope;
     while (pw > MIN_PART_WIDTH_HB) {
         const int half = pw / 2;
         const int parts = (m + half - 1) / pw;
+        ++g_stage_level;
         int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * parts * 4);
         HIPCHECK(hipMemsetD32Async(pbest, kAffNegH, (size_t)2 * parts, st));
         std::vector<DPProblem> probs;
@@ -766,6 +876,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                      sfree ? pbest + 2 * p + 1 : nullptr, RH + off, RE + off);
         }
         if (!probs.empty()) run_fill(E, probs, fp, st);
+        stage_check(st, "affine fill");
         if (!jobs.empty()) {
             int maxn = 0;
             for (const auto& J : jobs) maxn = std::max(maxn, J.n);
@@ -774,16 +885,27 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             void* d_jobs = E.jobs.get(E.host_jobs.size());
             HIPCHECK(hipMemcpyAsync(d_jobs, E.host_jobs.data(), E.host_jobs.size(), hipMemcpyHostToDevice, st));
             HIPCHECK(anyseq_launch_aff_row_to_col(d_jobs, (int)jobs.size(), maxn, -sc.gap_extend, st));
+            stage_check(st, "aff_row_to_col");
         }
         PartInfo* d_parts = (PartInfo*)E.parts.get(pinfo.size() * sizeof(PartInfo));
         HIPCHECK(hipMemcpyAsync(d_parts, pinfo.data(), pinfo.size() * sizeof(PartInfo), hipMemcpyHostToDevice, st));
         HIPCHECK(anyseq_launch_aff_hb_join(d_parts, parts, half, LH, LE, RH, RE, pbest, sc.gap_open, sc.gap_extend,
                                            d_spl, d_typ, level1 ? d_score : nullptr, st));
+        stage_check(st, "aff_hb_join");
         HIPCHECK(hipMemcpyAsync(sp.v.data(), d_spl, sp.v.size() * 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipMemcpyAsync(typ.data(), d_typ, typ.size() * 4, hipMemcpyDeviceToHost, st));
         int32_t s32 = 0;
         if (level1) HIPCHECK(hipMemcpyAsync(&s32, d_score, 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipStreamSynchronize(st));
+        // every split this level set lies inside its part and has a known type (the
+        // next level's sub-problems are built from them)
+        for (int p = 0; p < parts; ++p) {
+            const int si = pinfo[p].split_index + 1;
+            const int lo = pinfo[p].off, hi = (pinfo[p].flags & 4) ? lo : lo + std::max(pinfo[p].len, 0);
+            if (sp.v[si] < lo || sp.v[si] > hi || typ[si] < T_H || typ[si] > T_AFTER)
+                fail("internal: level %d part %d split %d (type %d) outside rows [%d, %d]", g_stage_level, p,
+                     sp.v[si], typ[si], lo, hi);
+        }
         if (level1) {
             // semiglobal: the empty alignment (a border cell, 0) is a candidate too
             score = kind == KIND_SEMIGLOBAL ? std::max(s32, 0) : s32;
@@ -817,7 +939,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
     HIPCHECK(anyseq_launch_aff_pred(d_blocks, (int)blocks.size(), dq, ds, d_pred, sc.match, sc.mismatch,
                                     sc.gap_open, sc.gap_extend, st));
+    stage_check(st, "aff_pred");
     HIPCHECK(anyseq_launch_aff_walk(d_blocks, (int)blocks.size(), dq, ds, d_pred, d_alq, d_als, st));
+    stage_check(st, "aff_walk");
     return score;
 }
 
@@ -1077,11 +1201,7 @@ const char* anyseq_last_error(void) { return g_last_error.c_str(); }
 
 void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid) {
     std::lock_guard<std::mutex> lk(g_engines_mu);
-    if (!g_tuning_init) {
-        g_tuning.CH = env_int("ANYSEQ_CH", g_tuning.CH);
-        g_tuning.fronts = env_int("ANYSEQ_FRONTS", g_tuning.fronts);
-    }
-    g_tuning_init = true;
+    init_tuning_locked();
     if (rows_per_lane > 0) g_tuning.R = rows_per_lane;
     if (waves_per_group > 0) g_tuning.NW = waves_per_group;
     if (grid >= 0) g_tuning.grid = grid;
@@ -1089,14 +1209,7 @@ void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid) {
 
 int anyseq_set_option(const char* name, int value) {
     std::lock_guard<std::mutex> lk(g_engines_mu);
-    if (!g_tuning_init) {
-        g_tuning.R = env_int("ANYSEQ_R", g_tuning.R);
-        g_tuning.NW = env_int("ANYSEQ_NW", g_tuning.NW);
-        g_tuning.grid = env_int("ANYSEQ_GRID", g_tuning.grid);
-        g_tuning.CH = env_int("ANYSEQ_CH", g_tuning.CH);
-        g_tuning.fronts = env_int("ANYSEQ_FRONTS", g_tuning.fronts);
-        g_tuning_init = true;
-    }
+    init_tuning_locked();
     const std::string n = name ? name : "";
     if (n == "rows_per_lane") g_tuning.R = value;
     else if (n == "chunk") g_tuning.CH = value == 16 ? 16 : 32;

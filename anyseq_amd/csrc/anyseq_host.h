@@ -43,6 +43,8 @@ struct DevBuf {
 };
 
 int env_int(const char* name, int dflt);
+// Diagnostics (ANYSEQ_FAULT_INFO): name a buffer for the GPU memory-fault report.
+void register_fault_buf(const char* name, const DevBuf* b);
 
 struct Tuning {
     int R = 1;

@@ -60,7 +60,12 @@ struct DPProblem {
     int32_t amode;
     uint32_t* progress;
     uint32_t* stage;       // diagnostics (ANYSEQ_SHARD_DEBUG): per-band stage reached
+    // kProbMagic ^ (index in the launch's problem table) ^ (epoch << 12), set by
+    // fill_prepare: a fill group checks it before it uses any pointer of the descriptor
+    int32_t magic;
+    int32_t pad_;
 };
+constexpr int32_t kProbMagic = 0x5eb1a700;
 
 // Affine border modes (H space; oracle bm_corner / bm_top / bm_left):
 //   NORMAL     the scheme's global borders (corner 0, gaps paid from it);
@@ -89,6 +94,8 @@ constexpr int32_t kShardSentinel = (int32_t)0x80808080;
 struct GroupRef {
     int32_t prob;
     int32_t group;
+    int32_t epoch;   // FillParams::epoch of the launch that uploaded it
+    int32_t pad_;
 };
 
 struct FillParams {
@@ -98,6 +105,8 @@ struct FillParams {
     int32_t affine;
     int32_t pad;                      // affine: bit 0 = C++ steady state only (diagnostics)
     unsigned long long* dbg;          // diagnostic build only (ANYSEQ_STAMPS): per-launch stamp sums
+    int32_t epoch;                    // launch counter: descriptors carry it (stale uploads are detected)
+    int32_t pad2_;
 };
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).
@@ -124,6 +133,6 @@ struct BlockInfo {
 };
 
 // Device-side error codes written to the error word.
-enum : uint32_t { ERR_NONE = 0, ERR_SPIN_TIMEOUT = 1 };
+enum : uint32_t { ERR_NONE = 0, ERR_SPIN_TIMEOUT = 1, ERR_BAD_DESC = 0x100 };
 
 }  // namespace anyseq

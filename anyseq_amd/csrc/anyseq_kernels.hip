@@ -942,6 +942,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
         if (gi >= ngroups_total || err_set(err)) break;
         const GroupRef g = groups[gi];
         const DPProblem P = probs[g.prob];
+        if (g.epoch != fp.epoch || P.magic != (kProbMagic ^ g.prob ^ (fp.epoch << 12)) ||
+            g.group >= P.ngroups) {
+            if (threadIdx.x == 0) atomicOr(err, ERR_BAD_DESC);
+            break;
+        }
         const int first = g.group * NW;
         const int last = min(P.nbands, first + NW) - 1;   // last band of this group
         // where the group's bottom row goes: the next group's input row (rowbuf, pre-filled
@@ -1487,6 +1492,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
         if (gi >= ngroups_total || err_set(err)) break;
         const GroupRef gr = groups[gi];
         const DPProblem P = probs[gr.prob];
+        if (gr.epoch != fp.epoch || P.magic != (kProbMagic ^ gr.prob ^ (fp.epoch << 12)) ||
+            gr.group >= P.ngroups) {
+            if (threadIdx.x == 0) atomicOr(err, ERR_BAD_DESC);
+            break;
+        }
         const int first = gr.group * NW;
         const int last = min(P.nbands, first + NW) - 1;
         int2* rows = reinterpret_cast<int2*>(P.rowbuf);

@@ -94,6 +94,10 @@ struct Shard {
     const int32_t* lBe = nullptr;
     void init() {
         if (st) return;
+        for (Front* f : {&top, &bot})
+            for (DevBuf* b : {&f->out_col, &f->left_in, &f->out_row, &f->out_col_e, &f->left_in_e, &f->left_flag})
+                register_fault_buf(f == &top ? "shard.top" : "shard.bot", b);
+        for (DevBuf* b : {&fc.probs, &fc.groups, &fc.rowbuf, &fc.flags, &fc.ctr, &res}) register_fault_buf("shard.fc", b);
         // polled across kernels / XCDs: never L2-cached (see DevBuf::uncached)
         for (Front* f : {&top, &bot})
             f->out_col.uncached = f->left_in.uncached = f->out_col_e.uncached = f->left_in_e.uncached =
@@ -496,6 +500,8 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
     Engine& E = engine();
     std::lock_guard<std::mutex> lk(E.mu);
     static std::vector<Shard> shards;   // kept: streams, counters, buffers are reused
+    if (N > 64) fail("sharded fill: at most 64 local shards");
+    if (shards.capacity() < 64) shards.reserve(64);   // shards never move (buffers are registered by address)
     if ((int)shards.size() < N) shards.resize(N);
     uint8_t* dq = (uint8_t*)E.q.get((size_t)n);
     uint8_t* ds = (uint8_t*)E.s.get((size_t)m);

@@ -1,26 +1,33 @@
 #!/usr/bin/env python3
 """bench.py — GCUPS of the AnySeq hot path on MI355X (driver contract).
 
-Workload at N=1 (BASELINE.json configs[1]): global (NW) alignment score, linear
-gap (+2/-1/-1, the reference ABI's scheme), 65536 x 65536, on the exact inputs
-the reference driver generates for ``align -r 65536 65536`` (main.cpp:200-210,
-reproduced by anyseq_main_random_pair; fingerprints in SURVEY.md App. B).
-One step = one global_alignment_score-equivalent fill of the whole matrix with
-both sequences already resident in HBM (anyseq_score_device), score copied back.
+Default workload at N=1: BASELINE.json configs[2], the north-star target —
+local (Smith-Waterman) alignment with affine gaps (+2/-1, open -2, extend -1) of
+the 65536 x 65536 pair that the reference driver generates for
+``align -r 65536 65536`` (main.cpp:200-210, reproduced by anyseq_main_random_pair),
+score + linear-space (Hirschberg) traceback.  One step = one
+anyseq_construct_device call: sequences resident in HBM, the optimal score and the
+two aligned strings (sparse i+j+1 layout, export.impala:131-147) written to HBM.
+``value`` = n*m / step time (end-to-end GCUPS: every fill, join, predecessor and
+walk kernel of the construct inside the timed region).
 
-N>1 (one process per GPU, torch.distributed.run): weak scaling over ONE
-column-blocked matrix of 65536 rows x 65536*N columns; rank g owns columns
-[65536 g, 65536 (g+1)); the two fronts' boundary columns travel between
-neighbouring ranks in 1024-row chunks with RCCL send/recv over xGMI while the
-fills run (libanyseq.so, anyseq_shard.cpp).  torch.distributed
-(gloo) is the control plane only: barrier, max-over-ranks time, RCCL ids.
+Default at N>1 (one process per GPU, torch.distributed.run): configs[4], strong
+scaling — ONE semi-global affine score of the 4.64 Mbp genome pair, column-blocked
+over the ranks, boundary columns over RCCL send/recv (anyseq_shard.cpp).
 
---config 2 (BASELINE.json configs[2], the north-star target): local (SW) affine
-alignment (+2/-1, open -2, extend -1) of the same 65536^2 pair, score + Hirschberg
-traceback: one step = anyseq_construct_device into device strings.
---config 3 (configs[3]): semi-global affine linear-memory traceback of a 4.64 Mbp
-synthetic related-genome pair (the E. coli / S. boydii FASTAs are absent from the
-reference snapshot; anyseq_amd/genome.py), or of --fasta Q S (first records).
+Other workloads: --config 1 (configs[1]: NW linear score, 65536^2), --config 3
+(configs[3]: semi-global affine linear-memory traceback of the genome pair),
+--config 4 at N=1.
+
+Every line carries:
+  * roofline  — the dominant kernel (the DP fill) against the §8(d) model of 4 B
+    per cell (peak 8 TB/s), plus the VALU-issue ceiling of the same kernel
+    (``roofline.valu``) and the PMC-measured HBM bytes when a profile of this
+    build exists under profiles/ (``traffic``);
+  * cpu_baseline — the oracle restatement of the same workload (a bounded
+    prefix sample), at T = 4 (the reference's get_thread_count(),
+    backend_cpu.impala:13) and at T = the host cores available, median and min
+    of >= 5 runs, CPU model stated.
 
 Prints ONE JSON line on rank 0.
 """
@@ -30,6 +37,7 @@ import argparse
 import glob
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -38,34 +46,68 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES_PER_CELL = 4           # one int32 H store per cell
+# VALU issue ceiling of the fill design: one compute wave per SIMD issues at most one
+# wave64 VALU instruction per 4 cycles (MI355X_MICROARCH.md, "vector-instruction ISSUE
+# cost", one wave alone): 256 CUs x 4 SIMDs x 2.4 GHz / 4.
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
+# VALU instructions per wave step (64 cells) of the steady-state asm loops
+# (tools/gen_block_asm.py): linear 5 (+1 publishing shift), affine 9
+# (+2 publishing shifts) plain, +2.5 with the local clamp and best tracking.
+VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.0, "affine_local": 13.5}
+
+AFFINE = dict(match=2, mismatch=-1, gap_open=-2, gap_extend=-1)
+METRIC = "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; % of HBM roofline"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--m", type=int, default=65536)
-    ap.add_argument("--kind", default="global", choices=["global", "semiglobal", "local"])
+    ap.add_argument("--kind", default=None, choices=["global", "semiglobal", "local"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
-                    help="run the RCCL column-block path even at N=1 (plumbing check; the N=1 line is single GPU)")
-    ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
-                    help="BASELINE.json configs index: 1 NW linear score, 2 SW affine score+traceback, "
-                         "3 genome semi-global affine traceback, 4 genome semi-global affine score "
-                         "column-blocked over the ranks (strong scaling)")
+                    help="config 1: run the RCCL column-block path even at N=1 (plumbing check)")
+    ap.add_argument("--config", type=int, default=None, choices=[1, 2, 3, 4],
+                    help="BASELINE.json configs index (default: 2 at N=1, 4 at N>1): 1 NW linear score, "
+                         "2 SW affine score+traceback, 3 genome semi-global affine traceback, 4 genome "
+                         "semi-global affine score column-blocked over the ranks (strong scaling)")
     ap.add_argument("--gap-open", type=int, default=0,
                     help="config 1 only: affine gap open (extend -1); 0 = the reference's linear scheme")
-    ap.add_argument("--fasta", nargs=2, metavar=("QUERY", "SUBJECT"), help="config 3: real genome files")
-    ap.add_argument("--cpu-threads", type=int, default=4,
-                    help="oracle threads (reference get_thread_count() = 4, backend_cpu.impala:13)")
+    ap.add_argument("--fasta", nargs=2, metavar=("QUERY", "SUBJECT"), help="configs 3/4: real genome files")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="CPU baseline repetitions per thread count")
     return ap.parse_args()
 
 
+# ----------------------------------------------------------------- helpers --
+def host_cores() -> int:
+    """Cores this process may use (the GPU box's share, not the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def load_traffic(kernel_tag: str):
-    """HBM bytes per launch from the newest committed PMC summary (profiles/*pmc*.json)."""
+    """HBM bytes per launch from the newest committed PMC summary (profiles/*pmc*.json)
+    whose build matches this one (same libanyseq.so digest), else the newest one."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    lib_digest = _lib_digest()
+    best = None
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -73,45 +115,82 @@ def load_traffic(kernel_tag: str):
             continue
         ent = d.get("kernels", {}).get(kernel_tag)
         if ent and ent.get("hbm_bytes_per_launch"):
-            return ent["hbm_bytes_per_launch"], os.path.basename(f)
-    return None, None
+            same = lib_digest and d.get("lib_sha16") == lib_digest
+            cand = (ent["hbm_bytes_per_launch"], os.path.basename(f) + ("" if same else " (other build)"))
+            if same:
+                return cand
+            best = best or cand
+    return best if best else (None, None)
 
 
-def cpu_baseline(q: bytes, s: bytes, kind: str, threads: int, expect: int, gap_open: int = 0):
-    from oracle import oracle as O   # bench.py's cpu_baseline leg is allowed to use the oracle
+def _lib_digest():
+    import hashlib
+    p = os.path.join(ROOT, "anyseq_amd", "libanyseq.so")
+    try:
+        return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def timed_runs(fn, runs: int):
+    ts = []
+    for _ in range(runs):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    return ts
+
+
+def cpu_baseline(what: str, work, cells: int, sample: str, runs: int):
+    """The oracle (test infrastructure; bench.py's cpu_baseline leg may use it) timed at
+    T = 4 and T = host cores, median and min of `runs`."""
+    from oracle import oracle as O
     O.build()
-    O.set_threads(threads)
-    t = time.perf_counter()
-    if gap_open:
-        v = O.affine_score(kind, q, s, 2, -1, gap_open, -1)   # single-threaded restatement
-        threads = 1
-    else:
-        v = O.score(kind, q, s)
-    dt = time.perf_counter() - t
-    if v != expect:
-        raise SystemExit(f"cpu baseline disagrees with GPU: {v} != {expect}")
-    what = (f"affine (open {gap_open}) score (oracle_affine_score, 1 thread)" if gap_open else
-            f"linear score (oracle restatement of iteration_cpu/scoring_cpu, 1024^2 tiles, {threads} threads)")
-    return {"value": round(len(q) * len(s) / dt / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
-            "sample": f"full {len(q)}x{len(s)} {kind} {what}, {dt:.2f} s"}
+    out = {"unit": "GCUPS", "kind": "port", "cpu_model": cpu_model(), "sample": sample, "what": what,
+           "runs": runs, "threads": {}}
+    tmax = host_cores()
+    for T in sorted({4, tmax}):
+        O.set_threads(T)
+        work()   # warm (page-in, thread start)
+        ts = timed_runs(work, runs)
+        out["threads"][str(T)] = {"median_s": round(statistics.median(ts), 4), "min_s": round(min(ts), 4),
+                                  "gcups_median": round(cells / statistics.median(ts) / 1e9, 4),
+                                  "gcups_best": round(cells / min(ts) / 1e9, 4)}
+    top = out["threads"][str(tmax)]
+    out["value"] = top["gcups_median"]
+    out["cores"] = tmax
+    return out
 
 
-AFFINE = dict(match=2, mismatch=-1, gap_open=-2, gap_extend=-1)
+def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: str, traffic_tag: str):
+    achieved = cells_per_launch * BYTES_PER_CELL / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
+    traffic, traffic_src = load_traffic(traffic_tag)
+    gcups = cells_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
+    v = VALU_PER_STEP[valu_key]
+    valu_peak_gcups = VALU_PEAK_WAVE_INSTR * 64 / v / 1e9
+    return {
+        "bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
+        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+        "traffic": traffic, "traffic_source": traffic_src,
+        "kernel": kernel, "kernel_ms": round(kernel_ms, 4), "cells_per_launch": int(cells_per_launch),
+        "bytes_model": f"{BYTES_PER_CELL} B/cell x DP cells per launch (SURVEY.md 8(d)); the kernel keeps cells "
+                       "in VGPRs and stores only hand-off rows, so the measured traffic is far below the model "
+                       "and the binding limits are VALU issue and the band chain (DESIGN.md §3.5)",
+        "valu": {"instr_per_wave_step": v, "peak_gcups": round(valu_peak_gcups, 1),
+                 "achieved_gcups": round(gcups, 2) if gcups else None,
+                 "frac": round(gcups / valu_peak_gcups, 4) if gcups else None,
+                 "model": "one compute wave per SIMD, one wave64 VALU per 4 cycles at 2.4 GHz, 64 cells "
+                          "per wave step"},
+    }
 
 
-def cpu_baseline_construct(q: bytes, s: bytes, kind: str, side: int):
-    """Oracle affine construct (single-threaded restatement) on a side x side prefix sample."""
-    from oracle import oracle as O   # bench.py's cpu_baseline leg is allowed to use the oracle
-    O.build()
-    qs, ss = q[:side], s[:side]
-    t = time.perf_counter()
-    O.affine_construct(kind, qs, ss, **AFFINE)
-    dt = time.perf_counter() - t
-    return {"value": round(len(qs) * len(ss) / dt / 1e9, 4), "unit": "GCUPS", "cores": 1, "kind": "port",
-            "sample": f"{len(qs)}x{len(ss)} prefix of the same pair, {kind} affine score + linear-memory "
-                      f"traceback (oracle_affine_construct, 1 thread), {dt:.2f} s"}
+def step_stats(ts):
+    ms = [t * 1e3 for t in ts]
+    return {"ms_per_step": round(sum(ms) / len(ms), 4), "ms_per_step_median": round(statistics.median(ms), 4),
+            "ms_per_step_min": round(min(ms), 4)}
 
 
+# -------------------------------------------------------- configs[2] / [3] --
 def construct_bench(args):
     """configs[2] / configs[3]: affine construct (score + Hirschberg traceback) on one GPU."""
     import torch
@@ -121,12 +200,12 @@ def construct_bench(args):
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     if args.config == 2:
-        kind = "local"
+        kind = args.kind or "local"
         q, s = A.main_random_pair(args.n, args.m)
         data = "synthetic: main.cpp `-r 65536 65536` generator (mt19937_64 default seed, uniform ACGT)"
-        workload = f"local (SW) affine alignment, score + Hirschberg traceback, {len(q)}x{len(s)}"
+        workload = f"{kind} affine alignment, score + Hirschberg traceback, {len(q)}x{len(s)}"
     else:
-        kind = "semiglobal"
+        kind = args.kind or "semiglobal"
         if args.fasta:
             (_, q), (_, s) = genome.first_record(args.fasta[0]), genome.first_record(args.fasta[1])
             data = f"FASTA first records: {os.path.basename(args.fasta[0])}, {os.path.basename(args.fasta[1])}"
@@ -134,16 +213,16 @@ def construct_bench(args):
             q, s = genome.synthetic_related_pair(4_641_652, 0.9)
             data = ("synthetic related-genome pair (E. coli K-12 length, 90% identity; the reference's "
                     "ecoli/sboydii FASTAs are absent)")
-        workload = f"semi-global affine alignment, linear-memory traceback, {len(q)}x{len(s)}"
+        workload = f"{kind} affine alignment, linear-memory traceback, {len(q)}x{len(s)}"
     n, m = len(q), len(s)
-    stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
+    sh = torch.cuda.current_stream().cuda_stream
     dq = torch.frombuffer(bytearray(q), dtype=torch.uint8).to(dev)
     ds = torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev)
     alq = torch.empty(n + m, dtype=torch.uint8, device=dev)
     als = torch.empty(n + m, dtype=torch.uint8, device=dev)
 
     def step():
+        # anyseq_construct_device synchronises the stream before it returns
         return A.construct_device(kind, dq.data_ptr(), n, ds.data_ptr(), m, alq.data_ptr(), als.data_ptr(),
                                   stream=sh, **AFFINE)
 
@@ -151,58 +230,57 @@ def construct_bench(args):
         step()
     torch.cuda.synchronize()
     A.last_fill_stats()
-    t0 = time.perf_counter()
+    ts = []
+    score = None
     for _ in range(args.steps):
+        t = time.perf_counter()
         score = step()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t)
+    elapsed = sum(ts)
     fill_ms, launches, fill_cells = A.last_fill_stats()
-    # the alignment re-scored on the host equals the fill's optimum (size-independent check)
+    # size-independent check: the alignment re-scored on the host equals the optimum
     rs = genome.affine_rescore(alq.cpu().numpy().tobytes(), als.cpu().numpy().tobytes(), **AFFINE)
     if rs != score:
         raise SystemExit(f"construct strings score {rs} != optimum {score}")
-    cells = n * m
-    gcups = cells * args.steps / elapsed / 1e9
-    achieved = fill_cells * BYTES_PER_CELL / (fill_ms * 1e-3) / 1e9 if fill_ms > 0 else None
-    traffic, traffic_src = load_traffic(f"fill_affine_kernel<{kind}> construct {n}x{m}")
+    gcups = n * m * args.steps / elapsed / 1e9
+    kernel_ms = fill_ms / max(launches, 1)
     out = {
-        "metric": "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; % of HBM roofline",
-        "value": round(gcups, 2), "unit": "GCUPS", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed * 1e3 / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "metric": METRIC, "value": round(gcups, 2), "unit": "GCUPS", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, **step_stats(ts), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int32", "data": data,
         "config": {"workload": workload, "baseline_config": args.config, "query_len": n, "subject_len": m,
                    "scoring": "match +2, mismatch -1, gap open -2, extend -1", "parallelism": "single GPU",
                    "score": int(score), "fill_cells_per_step": fill_cells // max(args.steps, 1),
-                   "fill_launches_per_step": launches // max(args.steps, 1)},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic, "kernel_ms": round(fill_ms / max(launches, 1), 4),
-                     "bytes_model": f"{BYTES_PER_CELL} B/cell x cells computed by the fill launches "
-                                    "(Hirschberg halves included) / their summed duration (SURVEY.md 8(d))",
-                     "traffic_source": traffic_src},
+                   "fill_launches_per_step": launches // max(args.steps, 1),
+                   "fill_ms_per_step": round(fill_ms / max(args.steps, 1), 4),
+                   "fill_gcups": round(fill_cells / (fill_ms * 1e-3) / 1e9, 2) if fill_ms > 0 else None},
+        "roofline": roofline("fill_affine_kernel", fill_cells / max(launches, 1), kernel_ms,
+                             "affine_local" if kind == "local" else "affine",
+                             f"fill_affine_kernel<{kind}> construct {n}x{m}"),
     }
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_construct(q, s, kind, 16384)
+        from oracle import oracle as O
+        side = 16384 if args.config == 2 else 8192
+        qs, ss = q[:side], s[:side]
+        out["cpu_baseline"] = cpu_baseline(
+            f"oracle_affine_construct ({kind} affine score + linear-memory traceback; level half-fills on T "
+            "threads)", lambda: O.affine_construct(kind, qs, ss, **AFFINE), side * side,
+            f"{side}x{side} prefix of the same pair", args.cpu_runs)
     print(json.dumps(out), flush=True)
 
 
-def main():
-    args = parse()
-    if args.config in (2, 3):
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            raise SystemExit("--config 2/3 run on one GPU (the column-block sharded path is config 1 / 4)")
-        return construct_bench(args)
+# -------------------------------------------------------- configs[1] / [4] --
+def score_bench(args, world, rank, local_rank):
     genome = args.config == 4
     if genome:   # configs[4]: semi-global affine, one genome-length matrix split over the ranks
-        args.kind, args.sharded = "semiglobal", True
+        args.kind, args.sharded = args.kind or "semiglobal", True
         args.gap_open = args.gap_open or -2
+    kind = args.kind or "global"
     # the sharded path's fill + transport streams each need a hardware queue of their own
     # (anyseq_shard.cpp check_hw_queues); HIP reads this at its first call
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
         os.environ["GPU_MAX_HW_QUEUES"] = "16"
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import anyseq_amd as A
 
@@ -218,8 +296,8 @@ def main():
     torch.cuda.set_device(local_rank if world > 1 else 0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    kind = args.kind
     parallelism = "single GPU"
+    q = s = None
     if dist and genome:
         from anyseq_amd import sharded, genome as G
         if args.fasta:
@@ -231,12 +309,10 @@ def main():
         from anyseq_amd import sharded
         step, n, m, parallelism = sharded.make_weak_step(dist, rank, world, kind, rows=args.n, cols_per_rank=args.m,
                                                          gap_open=args.gap_open)
-        q = s = None
     else:
         q, s = A.main_random_pair(args.n, args.m)
         n, m = len(q), len(s)
-        stream = torch.cuda.current_stream()
-        sh = stream.cuda_stream
+        sh = torch.cuda.current_stream().cuda_stream
         dq = torch.frombuffer(bytearray(q), dtype=torch.uint8).to(dev)
         ds = torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev)
 
@@ -244,6 +320,7 @@ def main():
             return A.score_device(kind, dq.data_ptr(), n, ds.data_ptr(), m, stream=sh, gap_open=args.gap_open,
                                   gap_extend=-1)
 
+    score = None
     for _ in range(args.warmup):
         score = step()
     torch.cuda.synchronize()
@@ -251,16 +328,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     A.last_fill_timing()
+    ts = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        t = time.perf_counter()
         score = step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    t1 = time.perf_counter()
+    elapsed = time.perf_counter() - t0
     fill_ms, launches = A.last_fill_timing()
-    elapsed = t1 - t0
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -273,60 +352,73 @@ def main():
     else:        # weak scaling: each rank owns n x m cells
         cells_per_step = n * m * world
         cells_per_launch = n * m
-    ms_per_step = elapsed * 1e3 / args.steps
     gcups = cells_per_step * args.steps / elapsed / 1e9
     kernel_ms = fill_ms / max(launches, 1)
-    achieved = cells_per_launch * BYTES_PER_CELL / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
-    tag = f"fill_kernel<{kind}> {n}x{m}" if not args.gap_open else f"fill_affine_kernel<{kind}> {n}x{m}"
-    traffic, traffic_src = load_traffic(tag)
+    aff = bool(args.gap_open)
+    valu_key = ("affine" if aff else "linear") + ("_local" if kind == "local" else "")
+    tag = f"fill_affine_kernel<{kind}> {n}x{m}" if aff else f"fill_kernel<{kind}> {n}x{m}"
 
     if rank == 0:
+        st = step_stats(ts)
+        st["ms_per_step"] = round(elapsed * 1e3 / args.steps, 4)   # includes the closing barrier (max over ranks)
         out = {
-            "metric": "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; % of HBM roofline",
-            "value": round(gcups, 2),
-            "unit": "GCUPS",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "strong" if genome else "weak",
-            "vs_baseline": None,
-            "dtype": "int32",
+            "metric": METRIC, "value": round(gcups, 2), "unit": "GCUPS", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, **st, "higher_is_better": True,
+            "scaling": "strong" if genome else "weak", "vs_baseline": None, "dtype": "int32",
             "data": ("synthetic related-genome pair (E. coli K-12 length, 90% identity; the reference's "
                      "ecoli/sboydii FASTAs are absent)" if genome and not args.fasta else
                      "FASTA first records" if genome else
                      "synthetic: main.cpp `-r 65536 65536` generator (mt19937_64 default seed, uniform ACGT)"),
             "config": {"workload": f"{kind} alignment score, "
-                                   + (f"affine gap (+2/-1, open {args.gap_open}, extend -1)" if args.gap_open
+                                   + (f"affine gap (+2/-1, open {args.gap_open}, extend -1)" if aff
                                       else "linear gap (+2/-1/-1)")
                                    + (f", one {n}x{m} matrix column-blocked over {world} GPU(s)" if genome
                                       else f", {n}x{m} cells per GPU"),
-                       "baseline_config": args.config,
-                       "query_len": n, "subject_len": m,
-                       "parallelism": parallelism,
-                       "score": int(score)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": traffic,
-                         "kernel_ms": round(kernel_ms, 4),
-                         "bytes_model": f"{BYTES_PER_CELL} B/cell x {cells_per_launch} cells per launch "
-                                        "(SURVEY.md 8(d))",
-                         "traffic_source": traffic_src},
+                       "baseline_config": args.config, "query_len": n, "subject_len": m,
+                       "parallelism": parallelism, "score": int(score),
+                       "transport": ("RCCL send/recv, unverified on >1 GPU until a SCALE run exists"
+                                     if world > 1 else None)},
+            "roofline": roofline("fill_affine_kernel" if aff else "fill_kernel", cells_per_launch, kernel_ms,
+                                 valu_key, tag),
         }
-        if world == 1 and not dist and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(q, s, kind, args.cpu_threads, int(score), args.gap_open)
-        elif world == 1 and genome and not args.no_cpu_baseline:
-            qs, ss = q[:16384], s[:16384]
-            v = A.score(kind, qs, ss, gap_open=args.gap_open, gap_extend=-1)
-            out["cpu_baseline"] = cpu_baseline(qs, ss, kind, 1, v, args.gap_open)
-            out["cpu_baseline"]["sample"] = "16384x16384 prefix of the pair: " + out["cpu_baseline"]["sample"]
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import oracle as O
+            if genome or aff:
+                side = 16384
+                qs, ss = (q[:side], s[:side])
+                go = args.gap_open
+                out["cpu_baseline"] = cpu_baseline(
+                    f"oracle_affine_score ({kind}, open {go}; single-threaded restatement)",
+                    lambda: O.affine_score(kind, qs, ss, 2, -1, go, -1), side * side,
+                    f"{side}x{side} prefix of the same pair", args.cpu_runs)
+            else:
+                side = 16384
+                qs, ss = q[:side], s[:side]
+                out["cpu_baseline"] = cpu_baseline(
+                    f"oracle linear {kind} score (restatement of iteration_cpu/scoring_cpu, 1024^2 tiles)",
+                    lambda: O.score(kind, qs, ss), side * side, f"{side}x{side} prefix of the same pair",
+                    args.cpu_runs)
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
-        sharded.finalize()
+        if args.sharded:
+            from anyseq_amd import sharded
+            sharded.finalize()
         dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config is None:
+        args.config = 2 if world == 1 else 4
+    if args.config in (2, 3):
+        if world > 1:
+            raise SystemExit("--config 2/3 run on one GPU (the column-block sharded path is config 1 / 4)")
+        return construct_bench(args)
+    return score_bench(args, world, rank, local_rank)
 
 
 if __name__ == "__main__":
