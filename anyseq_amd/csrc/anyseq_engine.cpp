@@ -172,6 +172,9 @@ void init_tuning_locked() {
     g_tuning.fronts = env_int("ANYSEQ_FRONTS", g_tuning.fronts);
     g_tuning.affasm = env_int("ANYSEQ_AFFINE_ASM", g_tuning.affasm);
     g_tuning.afft = env_int("ANYSEQ_AFFINE_TRANSPOSE", g_tuning.afft);
+    g_tuning.prio = env_int("ANYSEQ_PRIO", g_tuning.prio);
+    g_tuning.NWa = env_int("ANYSEQ_NWA", g_tuning.NWa);
+    g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning_init = true;
 }
 
@@ -271,6 +274,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));  // ctr[0] = dequeue counter, ctr[1] = error word
     FillParams fpl = fp;
     fpl.epoch = epoch;
+    fpl.prio = g_tuning.prio;
     unsigned long long* dbg = nullptr;
     static DevBuf stamp_buf;
     if (getenv("ANYSEQ_STAMPS")) {
@@ -1221,6 +1225,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_asm") g_tuning.affasm = value;
     else if (n == "ring_slots") g_tuning.ring_slots = value;
     else if (n == "affine_transpose") g_tuning.afft = value;
+    else if (n == "priority") g_tuning.prio = value;
     else return -1;
     return 0;
 }

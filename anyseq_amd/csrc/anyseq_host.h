@@ -57,6 +57,7 @@ struct Tuning {
     int affasm = 1;  // affine fill: bit 0 asm steady state, bit 2 asm prologue (experimental, off)
     int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
     int afft = 1;        // affine construct: run Hirschberg halves taller than wide transposed
+    int prio = 0;        // compute waves at s_setprio 3 (the I/O wave stays at 0)
 };
 extern Tuning g_tuning;
 

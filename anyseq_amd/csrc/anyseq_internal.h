@@ -106,7 +106,7 @@ struct FillParams {
     int32_t pad;                      // affine: bit 0 = C++ steady state only (diagnostics)
     unsigned long long* dbg;          // diagnostic build only (ANYSEQ_STAMPS): per-launch stamp sums
     int32_t epoch;                    // launch counter: descriptors carry it (stale uploads are detected)
-    int32_t pad2_;
+    int32_t prio;                     // compute waves raise their issue priority (s_setprio 3) when set
 };
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).

@@ -927,6 +927,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
         ck.wm = fp.match - 2 * fp.gap;
         ck.wx = fp.mismatch - 2 * fp.gap;
     }
+    if (fp.prio && wave < NW) __builtin_amdgcn_s_setprio(3);   // compute waves before the I/O wave
     for (;;) {
         if (threadIdx.x == 0) {
             sh.group = (int32_t)atomicAdd(dq, 1u);
@@ -1477,6 +1478,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
     k.wm = fp.match + 2 * k.nge;
     k.wx = fp.mismatch + 2 * k.nge;
     k.flags = fp.pad;
+    if (fp.prio && wave < NW) __builtin_amdgcn_s_setprio(3);   // compute waves before the I/O wave
     for (;;) {
         if (threadIdx.x == 0) {
             sh.group = (int32_t)atomicAdd(dq, 1u);

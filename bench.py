@@ -184,6 +184,14 @@ def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: s
     }
 
 
+def pair(A, n: int, m: int):
+    """main.cpp's `-r L L` pair (L = max(n, m); exactly the reference inputs at 65536),
+    cut to n x m."""
+    L = max(n, m)
+    q, s = A.main_random_pair(L, L)
+    return q[:n], s[:m]
+
+
 def step_stats(ts):
     ms = [t * 1e3 for t in ts]
     return {"ms_per_step": round(sum(ms) / len(ms), 4), "ms_per_step_median": round(statistics.median(ms), 4),
@@ -201,7 +209,7 @@ def construct_bench(args):
     dev = torch.device("cuda", 0)
     if args.config == 2:
         kind = args.kind or "local"
-        q, s = A.main_random_pair(args.n, args.m)
+        q, s = pair(A, args.n, args.m)
         data = "synthetic: main.cpp `-r 65536 65536` generator (mt19937_64 default seed, uniform ACGT)"
         workload = f"{kind} affine alignment, score + Hirschberg traceback, {len(q)}x{len(s)}"
     else:
@@ -310,7 +318,7 @@ def score_bench(args, world, rank, local_rank):
         step, n, m, parallelism = sharded.make_weak_step(dist, rank, world, kind, rows=args.n, cols_per_rank=args.m,
                                                          gap_open=args.gap_open)
     else:
-        q, s = A.main_random_pair(args.n, args.m)
+        q, s = pair(A, args.n, args.m)
         n, m = len(q), len(s)
         sh = torch.cuda.current_stream().cuda_stream
         dq = torch.frombuffer(bytearray(q), dtype=torch.uint8).to(dev)
