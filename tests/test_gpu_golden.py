@@ -23,6 +23,18 @@ def test_kat(anyseq):
         assert (r, aq.decode(), as_.decode()) == (c["ret"], c["alq"], c["als"]), c["kind"]
 
 
+@pytest.mark.parametrize("case", load("kat.json")["hand_constructs"], ids=lambda c: c["id"])
+def test_hand_kat_constructs(anyseq, case):
+    """HIP path (ABI construct_*) against the round-2 hand-derived known answers."""
+    r, aq, as_ = getattr(anyseq, f"construct_{case['kind']}_alignment")(case["q"], case["s"])
+    assert (r, aq.decode(), as_.decode()) == (case["ret"], case["alq"], case["als"])
+
+
+@pytest.mark.parametrize("case", load("kat.json")["hand_positions"], ids=lambda c: c["id"])
+def test_hand_kat_scores(anyseq, case):
+    assert getattr(anyseq, f"{case['kind']}_alignment_score")(case["q"], case["s"]) == case["score"]
+
+
 def test_oracle_cases(anyseq):
     for c in load("oracle_cases.json")["cases"]:
         for k in KINDS:

@@ -26,6 +26,22 @@ def test_kat_constructs(oracle):
         assert (r, aq.decode(), as_.decode()) == (c["ret"], c["alq"], c["als"]), c["kind"]
 
 
+@pytest.mark.parametrize("case", load("kat.json")["hand_constructs"], ids=lambda c: c["id"])
+def test_hand_kat_constructs(oracle, case):
+    """Round-2 hand-derived known answers (derivations in kat.json): hb_sum candidate order
+    across two Hirschberg levels and across stride classes, compat walks that stop at
+    PRED_NONE (local clamp, semiglobal border)."""
+    r, aq, as_ = oracle.construct(case["kind"], case["q"], case["s"])
+    assert (r, aq.decode(), as_.decode()) == (case["ret"], case["alq"], case["als"])
+
+
+@pytest.mark.parametrize("case", load("kat.json")["hand_positions"], ids=lambda c: c["id"])
+def test_hand_kat_semiglobal_position(oracle, case):
+    """The semiglobal first-maximum position rule (scoring.impala:46-63): last row first,
+    index -1 first, the column only if strictly greater."""
+    assert oracle.score(case["kind"], case["q"], case["s"], with_pos=True) == (case["score"], *case["pos"])
+
+
 def test_textbook_cross_check(oracle):
     rng = random.Random(5)
     for _ in range(150):
