@@ -73,6 +73,12 @@ _lib.anyseq_construct_device.argtypes = [_c_int, ctypes.POINTER(Scoring), _vp, _
 _lib.anyseq_shard_score_local.restype = _c_int
 _lib.anyseq_shard_score_local.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _c_int,
                                           ctypes.POINTER(_c_i64)]
+_lib.anyseq_construct_local_sharded.restype = _c_int
+_lib.anyseq_construct_local_sharded.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _c_int,
+                                                _vp, _vp, ctypes.POINTER(_c_i64)]
+_lib.anyseq_shard_construct.restype = _c_int
+_lib.anyseq_shard_construct.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _vp, _vp,
+                                        ctypes.POINTER(_c_i64)]
 _lib.anyseq_shard_unique_ids.restype = _c_int
 _lib.anyseq_shard_unique_ids.argtypes = [_vp, _c_int]
 _lib.anyseq_shard_init.restype = _c_int
@@ -232,6 +238,22 @@ def shard_score_local(kind, query, subject, nshards: int, match=2, mismatch=-1, 
                                      ctypes.byref(out)) != 0:
         raise AnySeqError(_err())
     return out.value
+
+
+def construct_local_sharded(kind, query, subject, nshards: int, match=2, mismatch=-1, gap_open=-2, gap_extend=-1):
+    """Sharded affine construct with `nshards` virtual ranks in this process on one GPU:
+    the level-by-level round-robin plan of the RCCL path, one fill
+    launch per rank per level.  Returns (optimal_score, alQuery, alSubject)."""
+    q, s = _b(query), _b(subject)
+    L = len(q) + len(s)
+    aq = ctypes.create_string_buffer(max(L, 1))
+    as_ = ctypes.create_string_buffer(max(L, 1))
+    out = _c_i64(0)
+    sc = _scoring(match, mismatch, gap_open, gap_extend)
+    if _lib.anyseq_construct_local_sharded(_kind(kind), ctypes.byref(sc), q, len(q), s, len(s), int(nshards), aq,
+                                           as_, ctypes.byref(out)) != 0:
+        raise AnySeqError(_err())
+    return out.value, aq.raw[:L], as_.raw[:L]
 
 
 def set_device(dev: int) -> None:

@@ -805,8 +805,13 @@ void add_half(std::vector<DPProblem>& probs, std::vector<RowToColJob>& jobs, int
 // (no level).  kind != global with a level-1 value <= 0 stops there (empty
 // alignment).
 int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds,
-                         int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st) {
+                         int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st, const ConstructShards* shards) {
     const FillParams fp = make_params(KIND_GLOBAL, sc);
+    // Sharded construct: half fills and final blocks are dealt round-robin
+    // to the ranks (virtual ranks: one launch each, in turn); every rank joins every part.
+    const int world = shards ? shards->world : 1;
+    const int nlaunch = shards && shards->local ? world : 1;   // launches per level (local mode)
+    auto owner = [&](int idx) { return idx % world; };
     const bool local = kind == KIND_LOCAL;
     HostSplits sp;
     sp.nb = (m + MIN_PART_WIDTH_HB - 1) / MIN_PART_WIDTH_HB;
@@ -842,10 +847,14 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         ++g_stage_level;
         int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * parts * 4);
         HIPCHECK(hipMemsetD32Async(pbest, kAffNegH, (size_t)2 * parts, st));
-        std::vector<DPProblem> probs;
+        std::vector<std::vector<DPProblem>> probs_of((size_t)nlaunch);
         std::vector<PartInfo>& pinfo = E.host_parts;
         pinfo.assign((size_t)parts, PartInfo{});
         std::vector<RowToColJob> jobs;
+        int half_index = 0;   // the level's half fills in part order: left 2k, right 2k+1
+        if (shards && !shards->local) {   // rows this rank does not fill are zero in the SUM reduction
+            for (int32_t* b : {LH, LE, RH, RE}) HIPCHECK(hipMemsetAsync(b, 0, nn, st));
+        }
         // transposed halves' bottom rows: sum of part heights <= n (parts' rows are disjoint)
         int32_t* rowpool = (int32_t*)E.outrow.get((size_t)2 * ((size_t)n + 64 * (size_t)parts) * 2 * 4);
         for (int p = 0; p < parts; ++p) {
@@ -872,14 +881,20 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             pi.flags = (sfree ? 1 : 0) | (efree ? 2 : 0);
             if (len <= 0) continue;
             const int best_bits = local ? AM_BEST_ALL : AM_BEST_LAST;
-            add_half(probs, jobs, rowpool, dq, off, 1, len, ds, hoj_l, 1, half, pi.smode,
-                     (pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0),
-                     efree ? pbest + 2 * p : nullptr, LH + off, LE + off);
-            add_half(probs, jobs, rowpool, dq, off + len - 1, -1, len, ds, hoj_r + hw - 1, -1, hw, pi.emode,
-                     (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0),
-                     sfree ? pbest + 2 * p + 1 : nullptr, RH + off, RE + off);
+            // (half_index advances on every rank, so all ranks agree on the owners)
+            const int ol = owner(half_index++), orr = owner(half_index++);
+            if (!shards || shards->local || ol == shards->rank)
+                add_half(probs_of[shards && shards->local ? ol : 0], jobs, rowpool, dq, off, 1, len, ds, hoj_l, 1,
+                         half, pi.smode, (pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0),
+                         efree ? pbest + 2 * p : nullptr, LH + off, LE + off);
+            if (!shards || shards->local || orr == shards->rank)
+                add_half(probs_of[shards && shards->local ? orr : 0], jobs, rowpool, dq, off + len - 1, -1, len, ds,
+                         hoj_r + hw - 1, -1, hw, pi.emode,
+                         (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0),
+                         sfree ? pbest + 2 * p + 1 : nullptr, RH + off, RE + off);
         }
-        if (!probs.empty()) run_fill(E, probs, fp, st);
+        for (auto& probs : probs_of)
+            if (!probs.empty()) run_fill(E, probs, fp, st);
         stage_check(st, "affine fill");
         if (!jobs.empty()) {
             int maxn = 0;
@@ -890,6 +905,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             HIPCHECK(hipMemcpyAsync(d_jobs, E.host_jobs.data(), E.host_jobs.size(), hipMemcpyHostToDevice, st));
             HIPCHECK(anyseq_launch_aff_row_to_col(d_jobs, (int)jobs.size(), maxn, -sc.gap_extend, st));
             stage_check(st, "aff_row_to_col");
+        }
+        if (shards && !shards->local) {   // every rank gets every part's columns and best cells
+            for (int32_t* b : {LH, LE, RH, RE}) shards->sum_i32(b, (size_t)n, st);
+            shards->max_i32(pbest, (size_t)2 * parts, st);
         }
         PartInfo* d_parts = (PartInfo*)E.parts.get(pinfo.size() * sizeof(PartInfo));
         HIPCHECK(hipMemcpyAsync(d_parts, pinfo.data(), pinfo.size() * sizeof(PartInfo), hipMemcpyHostToDevice, st));
@@ -925,6 +944,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     for (int b = 0; b < sp.nb; ++b) {
         const int ts = tp(b - 1), te = tp(b);
         if (ts == T_BEFORE || te == T_AFTER) continue;   // the path does not touch the block
+        if (shards && !shards->local && owner(b) != shards->rank) continue;   // another rank walks it
         BlockInfo bi{};
         bi.oi = sp.at(b - 1);
         bi.h = sp.at(b) - bi.oi;
@@ -937,7 +957,13 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         if (bi.h > 0) pred_bytes += (int64_t)(bi.h + 127) * 128;
         blocks.push_back(bi);
     }
-    if (blocks.empty()) return score;
+    if (blocks.empty()) {
+        if (shards && !shards->local) {
+            shards->max_u8(d_alq, (size_t)n + m, st);
+            shards->max_u8(d_als, (size_t)n + m, st);
+        }
+        return score;
+    }
     BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
     HIPCHECK(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, st));
     uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
@@ -946,13 +972,22 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     stage_check(st, "aff_pred");
     HIPCHECK(anyseq_launch_aff_walk(d_blocks, (int)blocks.size(), dq, ds, d_pred, d_alq, d_als, st));
     stage_check(st, "aff_walk");
+    if (shards && !shards->local) {
+        // blocks write disjoint positions over a ' ' prefill, and every written byte
+        // ('_' or a symbol) is above ' ': a byte-wise MAX merges the ranks' strings
+        shards->max_u8(d_alq, (size_t)n + m, st);
+        shards->max_u8(d_als, (size_t)n + m, st);
+    }
     return score;
 }
 
 // Affine construct on device-resident sequences into device strings (n+m bytes);
 // returns the optimal score.
+}  // namespace
+
 int64_t construct_affine_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n,
-                             const uint8_t* ds, int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st) {
+                             const uint8_t* ds, int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st,
+                             const ConstructShards* shards) {
     const size_t L = (size_t)n + (size_t)m;
     if (L == 0) return empty_score(kind, n, m, sc);
     HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
@@ -967,11 +1002,13 @@ int64_t construct_affine_dev(Engine& E, int kind, const anyseq_scoring& sc, cons
     if (m <= MIN_PART_WIDTH_HB) {   // no Hirschberg level: the score from a (small) fill
         const int64_t score = score_dev(E, kind, sc, dq, n, ds, m, st);
         if (kind != KIND_GLOBAL && score <= 0) return score;
-        aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st);
+        aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st, shards);
         return score;
     }
-    return aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st);
+    return aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st, shards);
 }
+
+namespace {
 
 int64_t construct_affine_host(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m,
                               char* alq, char* als) {

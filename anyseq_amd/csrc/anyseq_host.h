@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -125,6 +126,22 @@ void fill_finish(FillCtx& C);
 void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st);
 
 void set_last_error(const std::string& m);
+
+// Sharded affine construct: the half fills of every Hirschberg level
+// and the final blocks are dealt round-robin to `world` ranks; after each level's fills
+// the ranks' columns are summed (rows a rank did not fill are zero) and the free-end
+// best cells max-reduced, so every rank joins every part and holds the same splits;
+// the ranks' output strings merge by a byte-wise max.  local: `world` virtual ranks in
+// this process, one fill launch each, sharing the buffers (no reduction needed).
+struct ConstructShards {
+    int rank = 0, world = 1;
+    bool local = false;
+    std::function<void(int32_t*, size_t, hipStream_t)> sum_i32, max_i32;
+    std::function<void(uint8_t*, size_t, hipStream_t)> max_u8;
+};
+int64_t construct_affine_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n,
+                             const uint8_t* ds, int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st,
+                             const ConstructShards* shards = nullptr);
 
 }  // namespace host
 }  // namespace anyseq

@@ -59,12 +59,13 @@ namespace {
 
 constexpr int kComms = 4;   // top even/odd links, bottom even/odd links
 
-// Transport trigger: by default a host thread per direction polls the progress
-// counter in pinned host memory and issues each chunk's transfer; with
-// ANYSEQ_SHARD_WAITVALUE=1 the chunk transfers are enqueued up front behind
-// hipStreamWaitValue32 on signal memory.  ANYSEQ_SHARD_DIRECT=1 (local shards
-// only): the receiver polls the sender's out_col itself, no transfer at all.
-bool use_wait_value() { return env_int("ANYSEQ_SHARD_WAITVALUE", 0) != 0; }
+// Transport trigger: by default every chunk transfer is enqueued up front on the
+// direction's transport stream behind hipStreamWaitValue32 on the sender's progress
+// counter (signal memory): no host thread sits in the data path.  With
+// ANYSEQ_SHARD_WAITVALUE=0 a host thread per direction polls the counter in pinned
+// host memory instead and issues each chunk's transfer.  ANYSEQ_SHARD_DIRECT=1
+// (local shards only): the receiver polls the sender's out_col itself.
+bool use_wait_value() { return env_int("ANYSEQ_SHARD_WAITVALUE", 1) != 0; }
 bool use_direct() { return env_int("ANYSEQ_SHARD_DIRECT", 0) != 0; }
 
 
@@ -772,6 +773,77 @@ int anyseq_shard_finalize(void) {
         g_rccl.reset();
     }
     return 0;
+}
+
+// Sharded affine construct.  Every rank passes the whole pair; the
+// result (score, both strings) is returned on every rank.
+static int64_t sharded_construct(int kind, const anyseq_scoring& s, const char* query, int lenq, const char* subject,
+                                 int lens, char* alq, char* als, const ConstructShards& shards) {
+    check_scoring(kind, s);
+    if (s.gap_open == 0) fail("sharded construct: affine gaps only (gap_open < 0)");
+    if (lenq < 0 || lens < 0) fail("negative sequence length");
+    Engine& E = engine();
+    std::lock_guard<std::mutex> lk(E.mu);
+    hipStream_t st = E.stream;
+    const size_t L = (size_t)lenq + (size_t)lens;
+    uint8_t* dq = (uint8_t*)E.q.get((size_t)std::max(lenq, 1));
+    uint8_t* ds = (uint8_t*)E.s.get((size_t)std::max(lens, 1));
+    if (lenq > 0) HIPCHECK(hipMemcpyAsync(dq, query, (size_t)lenq, hipMemcpyHostToDevice, st));
+    if (lens > 0) HIPCHECK(hipMemcpyAsync(ds, subject, (size_t)lens, hipMemcpyHostToDevice, st));
+    uint8_t* d_alq = (uint8_t*)E.alq.get(std::max<size_t>(L, 1));
+    uint8_t* d_als = (uint8_t*)E.als.get(std::max<size_t>(L, 1));
+    const int64_t v = construct_affine_dev(E, kind, s, dq, lenq, ds, lens, d_alq, d_als, st, &shards);
+    if (L) {
+        HIPCHECK(hipMemcpyAsync(alq, d_alq, L, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(als, d_als, L, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHECK(hipStreamSynchronize(st));
+    return v;
+}
+
+int anyseq_construct_local_sharded(int kind, const anyseq_scoring* sc, const char* query, int lenq,
+                                   const char* subject, int lens, int nshards, char* alQuery, char* alSubject,
+                                   int64_t* score) {
+    try {
+        if (nshards < 1 || nshards > 64) fail("sharded construct: 1..64 local shards");
+        ConstructShards cs;
+        cs.world = nshards;
+        cs.local = true;
+        const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
+                                            lens, alQuery, alSubject, cs);
+        if (score) *score = v;
+        return 0;
+    } catch (const Failure& f) {
+        set_last_error(f.msg);
+        return -1;
+    }
+}
+
+int anyseq_shard_construct(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
+                           int lens, char* alQuery, char* alSubject, int64_t* score) {
+    try {
+        if (!g_rccl || g_rccl->rank < 0) fail("anyseq_shard_init has not been called");
+        ncclComm_t comm = g_rccl->comm[0];
+        ConstructShards cs;
+        cs.rank = g_rccl->rank;
+        cs.world = g_rccl->world;
+        cs.sum_i32 = [comm](int32_t* p, size_t n, hipStream_t st) {
+            NCCLCHECK(ncclAllReduce(p, p, n, ncclInt32, ncclSum, comm, st));
+        };
+        cs.max_i32 = [comm](int32_t* p, size_t n, hipStream_t st) {
+            NCCLCHECK(ncclAllReduce(p, p, n, ncclInt32, ncclMax, comm, st));
+        };
+        cs.max_u8 = [comm](uint8_t* p, size_t n, hipStream_t st) {
+            NCCLCHECK(ncclAllReduce(p, p, n, ncclUint8, ncclMax, comm, st));
+        };
+        const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
+                                            lens, alQuery, alSubject, cs);
+        if (score) *score = v;
+        return 0;
+    } catch (const Failure& f) {
+        set_last_error(f.msg);
+        return -1;
+    }
 }
 
 int anyseq_shard_score_local(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,

@@ -64,3 +64,35 @@ def chunks(h: int, chunk_rows: int = 1024):
         r1 = min(h, r0 + chunk_rows)
         out.append((r0, r1, (r1 + 63) // 64))
     return out
+
+
+# ---------------------------------------------------------------- construct --
+# Sharded affine construct (anyseq_engine.cpp aff_construct_hb with a
+# ConstructShards): the half fills of a Hirschberg level are numbered in part order
+# (part p's left half 2k, right half 2k+1 over the non-empty parts) and dealt
+# round-robin; so are the final 128-column blocks.  A rank fills only its halves'
+# rows of the level's columns (zero elsewhere), a SUM all-reduce assembles them, a
+# MAX all-reduce the free-end best cells, and a byte-wise MAX merges the ranks'
+# output strings (blanks ' ' are below every written byte).
+
+def half_owner(half_index: int, world: int) -> int:
+    return half_index % world
+
+
+def block_owner(block: int, world: int) -> int:
+    return block % world
+
+
+def level_halves(parts):
+    """(half_index, part, side, off, len) of a level's half fills; `parts` lists
+    (off, len) per part, None for an empty part (no fill)."""
+    out = []
+    k = 0
+    for p, pr in enumerate(parts):
+        if pr is None or pr[1] <= 0:
+            continue
+        off, ln = pr
+        out.append((k, p, "left", off, ln))
+        out.append((k + 1, p, "right", off, ln))
+        k += 2
+    return out

@@ -49,6 +49,22 @@ def score(kind, match=2, mismatch=-1, gap_open=0, gap_extend=-1) -> int:
     return out.value
 
 
+def construct(kind, query, subject, match=2, mismatch=-1, gap_open=-2, gap_extend=-1):
+    """Sharded affine construct over the initialised ranks (every rank passes the whole
+    pair and gets the same (score, alQuery, alSubject)): half fills and final blocks dealt
+    round-robin, level columns all-reduced over RCCL."""
+    q, s = _b(query), _b(subject)
+    L = len(q) + len(s)
+    aq = ctypes.create_string_buffer(max(L, 1))
+    as_ = ctypes.create_string_buffer(max(L, 1))
+    out = ctypes.c_int64(0)
+    sc = _scoring(match, mismatch, gap_open, gap_extend)
+    if _lib.anyseq_shard_construct(_kind(kind), ctypes.byref(sc), q, len(q), s, len(s), aq, as_,
+                                   ctypes.byref(out)) != 0:
+        raise AnySeqError(_err())
+    return out.value, aq.raw[:L], as_.raw[:L]
+
+
 def finalize() -> None:
     _lib.anyseq_shard_finalize()
 

@@ -134,6 +134,18 @@ int anyseq_shard_score(int kind, const anyseq_scoring* sc, int64_t* score);
 int anyseq_shard_finalize(void);
 /* The same sharded fill with `nshards` shards inside this process on the current
  * device (device copies instead of RCCL between them). */
+/* Sharded affine construct (align.impala:237-311 distributed by level):
+ * every rank calls it with the whole pair after anyseq_shard_init; the half fills of
+ * each Hirschberg level and the final 128-column blocks are dealt round-robin to the
+ * ranks, the level's boundary columns are all-reduced over RCCL, and every rank returns
+ * the same score and strings (sparse i+j+1 layout, lenq+lens bytes each). */
+int anyseq_shard_construct(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
+                           int lens, char* alQuery, char* alSubject, int64_t* score);
+/* The same plan with `nshards` virtual ranks in this process on one device (one fill
+ * launch per rank per level): the 1-GPU parity check of the sharded construct. */
+int anyseq_construct_local_sharded(int kind, const anyseq_scoring* sc, const char* query, int lenq,
+                                   const char* subject, int lens, int nshards, char* alQuery, char* alSubject,
+                                   int64_t* score);
 int anyseq_shard_score_local(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
                              int lens, int nshards, int64_t* score);
 

@@ -130,3 +130,88 @@ def test_plan_partition_and_chunks():
         assert all(blocks[g][0] + blocks[g][1] == blocks[g + 1][0] for g in range(N - 1))
     ch = SP.chunks(2500, 1024)
     assert ch == [(0, 1024, 16), (1024, 2048, 32), (2048, 2500, 40)]
+
+
+# ----------------------------------------------- sharded construct plan (§6.2) --
+def _construct_worker(rank, world, port, layouts, results):
+    """Each rank fills only the rows of its halves (deterministic stand-in values) and
+    writes only its blocks' string positions; SUM / MAX all-reduces must rebuild the
+    arrays every rank joins on, and the merged strings."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    for n, parts, blocks in layouts:
+        LH = torch.zeros(n, dtype=torch.int64)
+        RH = torch.zeros(n, dtype=torch.int64)
+        owned = []
+        for k, p, side, off, ln in SP.level_halves(parts):
+            if SP.half_owner(k, world) != rank:
+                continue
+            owned.append(k)
+            col = LH if side == "left" else RH
+            for r in range(off, off + ln):
+                col[r] = (r * 7 + 1) if side == "left" else -(r * 3 + 2)
+        dist.all_reduce(LH, op=dist.ReduceOp.SUM)
+        dist.all_reduce(RH, op=dist.ReduceOp.SUM)
+        L = sum(h for _, h in blocks) + 128 * len(blocks)
+        al = torch.full((L,), ord(" "), dtype=torch.uint8)
+        pos = 0
+        for b, (oi, h) in enumerate(blocks):
+            if SP.block_owner(b, world) == rank:
+                for i in range(0, h + 128, 2):   # a diagonal-ish walk: every other position
+                    al[pos + i] = ord("ACGT_"[(b + i) % 5])
+            pos += h + 128
+        t = al.to(torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        owned_t = torch.tensor([len(owned)], dtype=torch.int64)
+        dist.all_reduce(owned_t, op=dist.ReduceOp.SUM)
+        out.append((LH.tolist(), RH.tolist(), bytes(t.to(torch.uint8).tolist()), int(owned_t.item())))
+    if rank == 0:
+        results.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_construct_plan(world):
+    import torch.multiprocessing as mp
+    rng = random.Random(77 + world)
+    layouts = []
+    for _ in range(4):
+        n = rng.randint(5, 300)
+        cuts = sorted(rng.randint(0, n) for _ in range(rng.randint(1, 6)))
+        bounds = [0] + cuts + [n]
+        parts = [None if rng.random() < 0.2 else (a, b - a) for a, b in zip(bounds, bounds[1:])]
+        blocks = [(a, b - a) for a, b in zip(bounds, bounds[1:])]
+        layouts.append((n, parts, blocks))
+    ctx = mp.get_context("spawn")
+    results = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_construct_worker, args=(r, world, port, layouts, results)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = results.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for (n, parts, blocks), (LH, RH, al, nowned) in zip(layouts, got):
+        halves = SP.level_halves(parts)
+        assert nowned == len(halves)   # every half filled by exactly one rank
+        wantL, wantR = [0] * n, [0] * n
+        for _, _, side, off, ln in halves:
+            for r in range(off, off + ln):
+                if side == "left":
+                    wantL[r] = r * 7 + 1
+                else:
+                    wantR[r] = -(r * 3 + 2)
+        assert LH == wantL and RH == wantR
+        want = bytearray(b" " * len(al))
+        pos = 0
+        for b, (oi, h) in enumerate(blocks):
+            for i in range(0, h + 128, 2):
+                want[pos + i] = ord("ACGT_"[(b + i) % 5])
+            pos += h + 128
+        assert al == bytes(want)
