@@ -93,6 +93,19 @@ void* DevBuf::get(size_t bytes) {
     return p;
 }
 
+void* PinBuf::get(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes > cap) {
+        if (p) HIPCHECK(hipHostFree(p));
+        p = nullptr;
+        size_t c = std::max(bytes, cap * 3 / 2);
+        c = (c + 4095) & ~size_t(4095);
+        HIPCHECK(hipHostMalloc(&p, c, hipHostMallocDefault));
+        cap = c;
+    }
+    return p;
+}
+
 int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return (v && *v) ? atoi(v) : dflt;
@@ -101,6 +114,7 @@ int env_int(const char* name, int dflt) {
 void FillCtx::init() {
     if (!ev0) HIPCHECK(hipEventCreate(&ev0));
     if (!ev1) HIPCHECK(hipEventCreate(&ev1));
+    if (!ev2) HIPCHECK(hipEventCreateWithFlags(&ev2, hipEventDisableTiming));
 }
 
 // Diagnostics (ANYSEQ_FAULT_INFO=1): report the address of a GPU memory fault and the
@@ -257,15 +271,24 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     C.R = R;
     C.NW = NW;
     if (groups.empty()) {
+        if (C.err_host) *C.err_host = 0u;   // (no copy targets it: the previous launch has completed)
         HIPCHECK(hipEventRecord(C.ev0, st));
         HIPCHECK(hipEventRecord(C.ev1, st));
+        HIPCHECK(hipEventRecord(C.ev2, st));
         return;
     }
     DPProblem* d_probs = (DPProblem*)C.probs.get(probs.size() * sizeof(DPProblem));
     GroupRef* d_groups = (GroupRef*)C.groups.get(groups.size() * sizeof(GroupRef));
     C.h_probs = probs;
-    HIPCHECK(hipMemcpyAsync(d_probs, C.h_probs.data(), probs.size() * sizeof(DPProblem), hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemcpyAsync(d_groups, groups.data(), groups.size() * sizeof(GroupRef), hipMemcpyHostToDevice, st));
+    // staged in pinned memory (a truly asynchronous copy); the previous launch of this
+    // context has completed (fill_finish / fill_collect), so the staging area is free
+    const size_t pb = probs.size() * sizeof(DPProblem), gb = groups.size() * sizeof(GroupRef);
+    char* pin = (char*)C.pin.get(64 + pb + gb);
+    C.err_host = (uint32_t*)pin;
+    memcpy(pin + 64, C.h_probs.data(), pb);
+    memcpy(pin + 64 + pb, groups.data(), gb);
+    HIPCHECK(hipMemcpyAsync(d_probs, pin + 64, pb, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemcpyAsync(d_groups, pin + 64 + pb, gb, hipMemcpyHostToDevice, st));
     HIPCHECK(hipMemsetAsync(flags, 0, flag_words * 4, st));
     // group -> group hand-off rows start as a sentinel (the consumer polls the data):
     // -1 for linear, 0x80808080 for affine
@@ -304,6 +327,8 @@ void fill_launch(FillCtx& C) {
         HIPCHECK(anyseq_launch_fill(C.R, g_tuning.CH, C.NW, C.d_probs, C.d_groups, C.ngroups, ctr, ctr + 1, &C.fp,
                                     C.grid, C.st));
     HIPCHECK(hipEventRecord(C.ev1, C.st));
+    HIPCHECK(hipMemcpyAsync(C.err_host, ctr + 1, 4, hipMemcpyDeviceToHost, C.st));
+    HIPCHECK(hipEventRecord(C.ev2, C.st));
 }
 
 void fill_async(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
@@ -342,10 +367,18 @@ void stage_check(hipStream_t st, const char* what) {
 }
 
 void fill_finish(FillCtx& C) {
+    {
+        const hipError_t e = hipEventSynchronize(C.ev1);
+        if (e != hipSuccess) fail("fill failed: %s (%s)", hipGetErrorString(e), fill_summary(C).c_str());
+    }
+    fill_collect(C);
+}
+
+void fill_collect(FillCtx& C) {
     const int R = C.R, NW = C.NW;
     unsigned long long* dbg = C.stamps;
     {
-        const hipError_t e = hipEventSynchronize(C.ev1);
+        const hipError_t e = hipEventSynchronize(C.ev2);
         if (e != hipSuccess) {
             if (const char* path = getenv("ANYSEQ_FAIL_DUMP")) {   // every problem of the failed launch
                 if (FILE* f = fopen(path, "w")) {
@@ -367,9 +400,7 @@ void fill_finish(FillCtx& C) {
     g_fill_ms += ms;
     g_fill_launches += 1;
     g_fill_cells += C.cells;
-    uint32_t err = 0;
-    uint32_t* ctr = (uint32_t*)C.ctr.get(128);
-    HIPCHECK(hipMemcpy(&err, ctr + 1, 4, hipMemcpyDeviceToHost));
+    const uint32_t err = C.err_host ? *(volatile uint32_t*)C.err_host : 0u;
     if (dbg) {
         unsigned long long h[16];
         HIPCHECK(hipMemcpy(h, dbg, sizeof h, hipMemcpyDeviceToHost));
@@ -825,15 +856,21 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         typ[0] = T_AFTER;
         typ[sp.nb] = T_BEFORE;
     }
-    int32_t* d_spl = (int32_t*)E.spl.get(sp.v.size() * 4);
-    int32_t* d_typ = (int32_t*)E.typ.get(typ.size() * 4);
-    HIPCHECK(hipMemcpyAsync(d_spl, sp.v.data(), sp.v.size() * 4, hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemcpyAsync(d_typ, typ.data(), typ.size() * 4, hipMemcpyHostToDevice, st));
-    HIPCHECK(hipStreamSynchronize(st));   // the host vectors change below
+    // one device status block per construct: splits | types | level-1 score, downloaded
+    // in one copy per level into pinned memory (the level's only synchronisation)
+    const size_t nsv = sp.v.size();
+    int32_t* d_status = (int32_t*)E.status.get((2 * nsv + 4) * 4);
+    int32_t* d_spl = d_status;
+    int32_t* d_typ = d_status + nsv;
+    int32_t* d_score = d_status + 2 * nsv;
+    int32_t* h_status = (int32_t*)E.pin_down.get((2 * nsv + 4) * 4);
+    memcpy(h_status, sp.v.data(), nsv * 4);
+    memcpy(h_status + nsv, typ.data(), nsv * 4);
+    HIPCHECK(hipMemcpyAsync(d_status, h_status, 2 * nsv * 4, hipMemcpyHostToDevice, st));
     const size_t nn = (size_t)std::max(n, 1) * 4;
     int32_t *LH = (int32_t*)E.L.get(nn), *LE = (int32_t*)E.LE.get(nn);
     int32_t *RH = (int32_t*)E.R.get(nn), *RE = (int32_t*)E.RE.get(nn);
-    int32_t* d_score = (int32_t*)E.pos.get(64);
+    HIPCHECK(hipStreamSynchronize(st));   // h_status is rewritten by the first level's download
     auto tp = [&](int idx) { return typ[idx + 1]; };
     int64_t score = INT64_MIN;
     bool level1 = true;
@@ -893,16 +930,28 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                          (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0),
                          sfree ? pbest + 2 * p + 1 : nullptr, RH + off, RE + off);
         }
-        for (auto& probs : probs_of)
-            if (!probs.empty()) run_fill(E, probs, fp, st);
+        // the level's parts and row-to-column jobs, staged together in pinned memory
+        const size_t jb = jobs.size() * sizeof(RowToColJob), pb = pinfo.size() * sizeof(PartInfo);
+        char* up = (char*)E.pin_up.get(jb + pb + 16);
+        memcpy(up, pinfo.data(), pb);
+        memcpy(up + pb, jobs.data(), jb);
+        // one fill launch per level is left running (collected after the level's single
+        // synchronisation); local virtual ranks share the fill context, so all but the
+        // last of their launches complete in turn
+        bool pending_fill = false;
+        for (size_t li = 0; li < probs_of.size(); ++li) {
+            auto& probs = probs_of[li];
+            if (probs.empty()) continue;
+            if (pending_fill) fill_finish(E.fc);
+            fill_async(E, E.fc, probs, fp, st);
+            pending_fill = true;
+        }
         stage_check(st, "affine fill");
         if (!jobs.empty()) {
             int maxn = 0;
             for (const auto& J : jobs) maxn = std::max(maxn, J.n);
-            E.host_jobs.resize(jobs.size() * sizeof(RowToColJob));
-            memcpy(E.host_jobs.data(), jobs.data(), E.host_jobs.size());
-            void* d_jobs = E.jobs.get(E.host_jobs.size());
-            HIPCHECK(hipMemcpyAsync(d_jobs, E.host_jobs.data(), E.host_jobs.size(), hipMemcpyHostToDevice, st));
+            void* d_jobs = E.jobs.get(jb);
+            HIPCHECK(hipMemcpyAsync(d_jobs, up + pb, jb, hipMemcpyHostToDevice, st));
             HIPCHECK(anyseq_launch_aff_row_to_col(d_jobs, (int)jobs.size(), maxn, -sc.gap_extend, st));
             stage_check(st, "aff_row_to_col");
         }
@@ -910,16 +959,22 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             for (int32_t* b : {LH, LE, RH, RE}) shards->sum_i32(b, (size_t)n, st);
             shards->max_i32(pbest, (size_t)2 * parts, st);
         }
-        PartInfo* d_parts = (PartInfo*)E.parts.get(pinfo.size() * sizeof(PartInfo));
-        HIPCHECK(hipMemcpyAsync(d_parts, pinfo.data(), pinfo.size() * sizeof(PartInfo), hipMemcpyHostToDevice, st));
+        PartInfo* d_parts = (PartInfo*)E.parts.get(pb);
+        HIPCHECK(hipMemcpyAsync(d_parts, up, pb, hipMemcpyHostToDevice, st));
         HIPCHECK(anyseq_launch_aff_hb_join(d_parts, parts, half, LH, LE, RH, RE, pbest, sc.gap_open, sc.gap_extend,
                                            d_spl, d_typ, level1 ? d_score : nullptr, st));
         stage_check(st, "aff_hb_join");
-        HIPCHECK(hipMemcpyAsync(sp.v.data(), d_spl, sp.v.size() * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(typ.data(), d_typ, typ.size() * 4, hipMemcpyDeviceToHost, st));
-        int32_t s32 = 0;
-        if (level1) HIPCHECK(hipMemcpyAsync(&s32, d_score, 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipStreamSynchronize(st));
+        HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + (level1 ? 1 : 0)) * 4, hipMemcpyDeviceToHost, st));
+        {
+            const hipError_t e = hipStreamSynchronize(st);
+            if (e != hipSuccess && pending_fill)
+                fail("fill failed: %s (%s)", hipGetErrorString(e), fill_summary(E.fc).c_str());
+            HIPCHECK(e);
+        }
+        if (pending_fill) fill_collect(E.fc);
+        memcpy(sp.v.data(), h_status, nsv * 4);
+        memcpy(typ.data(), h_status + nsv, nsv * 4);
+        const int32_t s32 = level1 ? h_status[2 * nsv] : 0;
         // every split this level set lies inside its part and has a known type (the
         // next level's sub-problems are built from them)
         for (int p = 0; p < parts; ++p) {

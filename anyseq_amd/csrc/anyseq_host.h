@@ -43,6 +43,15 @@ struct DevBuf {
     void* get(size_t bytes);
 };
 
+// Grow-only pinned host buffer: the source / destination of truly asynchronous copies
+// (a pageable hipMemcpyAsync stages through the runtime and may block).  Callers must
+// not rewrite it before the stream has passed the copy.
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void* get(size_t bytes);
+};
+
 int env_int(const char* name, int dflt);
 // Diagnostics (ANYSEQ_FAULT_INFO): name a buffer for the GPU memory-fault report.
 void register_fault_buf(const char* name, const DevBuf* b);
@@ -81,6 +90,9 @@ struct FillCtx {
     // memory after it returns, so they live as long as the context, not the call
     std::vector<DPProblem> h_probs;
     std::vector<GroupRef> h_groups;
+    PinBuf pin;                  // staged descriptors + group table of the launch, and the error word
+    hipEvent_t ev2 = nullptr;    // after the error word's copy to `pin`
+    uint32_t* err_host = nullptr;
     void init();
 };
 
@@ -92,6 +104,8 @@ struct Engine {
     FillCtx fc;
     DevBuf q, s, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq, als;
     DevBuf LE, RE, typ, pos;   // affine construct
+    DevBuf status;             // affine construct: splits | types | score of a level (one download)
+    PinBuf pin_up, pin_down;   // affine construct: staged uploads / downloads of a level
     std::vector<int32_t> host_i32;
     std::vector<BlockInfo> host_blocks;
     std::vector<PartInfo> host_parts;
@@ -122,6 +136,9 @@ void fill_async(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fill
                 int grid = 0);
 // Waits for the launch of fill_async, accounts its time, checks the error word.
 void fill_finish(FillCtx& C);
+// The same without waiting: for a caller that has already synchronised the stream
+// past the launch (one synchronisation per Hirschberg level).
+void fill_collect(FillCtx& C);
 // fill_async + fill_finish on the engine's context.
 void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st);
 

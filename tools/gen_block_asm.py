@@ -108,6 +108,8 @@ def gen(kind, reads=True, stores=True, store_mode="shift"):
     e(f"v_mov_b32_e32 %[tf], v{T0 + 31}")
     return out
 
+# s_sleep between polls of an LDS counter (0: spin); ANYSEQ_GEN_SLEEP overrides (experiments)
+SLEEP = int(os.environ.get("ANYSEQ_GEN_SLEEP", "1"))
 SK0, VT, VT2, VA, VB = 130, 138, 139, 140, 141   # subject words, temps, LDS addresses
 TA, TB = 96, 98                                   # fixed SGPR pairs for s_memrealtime
 
@@ -129,7 +131,8 @@ def wait(e, name, seen, target, addr, count=None, tmp=None):
     e(f"s_cbranch_scc1 L_{name}_ok_%=")
     if count:
         e(f"s_add_u32 {count}, {count}, 1")
-    e("s_sleep 1")
+    if SLEEP:
+        e(f"s_sleep {SLEEP}")
     e("s_add_u32 %[x3], %[x3], 1")
     e("s_and_b32 %[x2], %[x3], 255")
     e(f"s_cbranch_scc1 L_{name}_loop_%=")
