@@ -49,6 +49,10 @@ hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, co
                                      const int32_t* RH, const int32_t* RE, const int32_t* pbest, int go, int ge,
                                      int32_t* splits, int32_t* types, int32_t* score, hipStream_t st);
 hipError_t anyseq_launch_aff_row_to_col(const void* jobs, int njobs, int maxn, int nge, hipStream_t st);
+hipError_t anyseq_launch_aff_hb_join2(const void* parts, int nparts, int maxlen, int half, const int32_t* LH,
+                                      const int32_t* LE, const int32_t* RH, const int32_t* RE, const int32_t* pbest,
+                                      int go, int ge, void* partial, int32_t* splits, int32_t* types, int32_t* score,
+                                      hipStream_t st);
 hipError_t anyseq_launch_aff_pred(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
                                   int match, int mismatch, int go, int ge, hipStream_t st);
 hipError_t anyseq_launch_aff_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
@@ -454,6 +458,18 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
 void set_aff_kind(DPProblem& P, int kind) {
     P.bmode = kind == KIND_GLOBAL ? BM_NORMAL : kind == KIND_SEMIGLOBAL ? BM_FREE_SEMI_OPEN : BM_FREE_LOCAL;
     P.amode = kind == KIND_LOCAL ? (AM_CLAMP | AM_BEST_ALL) : 0;
+}
+
+// The kernels keep every DP value in int32 with -2^29 as "minus infinity", and the
+// G-space shift (r + c + 2)·|gap| grows with the matrix: reject problems whose values
+// could come near it (a silently wrong score otherwise).
+void check_value_range(const anyseq_scoring& sc, int64_t n, int64_t m) {
+    const int64_t per = std::llabs(sc.match) + std::llabs(sc.mismatch) + std::llabs(sc.gap_open) +
+                        2 * std::llabs(sc.gap_extend);
+    if ((n + m + 2) * per >= (int64_t(1) << 28))
+        fail("%lld x %lld with these scores (sum of |match|, |mismatch|, |gap open|, 2|gap extend| = %lld) can "
+             "exceed the kernels' int32 value range: (n + m + 2) x that sum must stay below 2^28",
+             (long long)n, (long long)m, (long long)per);
 }
 
 void check_scoring(int kind, const anyseq_scoring& sc) {
@@ -961,8 +977,12 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         }
         PartInfo* d_parts = (PartInfo*)E.parts.get(pb);
         HIPCHECK(hipMemcpyAsync(d_parts, up, pb, hipMemcpyHostToDevice, st));
-        HIPCHECK(anyseq_launch_aff_hb_join(d_parts, parts, half, LH, LE, RH, RE, pbest, sc.gap_open, sc.gap_extend,
-                                           d_spl, d_typ, level1 ? d_score : nullptr, st));
+        int maxlen = 0;
+        for (const PartInfo& q : pinfo) maxlen = std::max(maxlen, (q.flags & 4) ? 0 : q.len);
+        const size_t nsl = (size_t)std::max(1, (maxlen + 1 + 4095) / 4096);
+        void* partial = E.joinbuf.get((size_t)parts * nsl * 8);
+        HIPCHECK(anyseq_launch_aff_hb_join2(d_parts, parts, maxlen, half, LH, LE, RH, RE, pbest, sc.gap_open,
+                                            sc.gap_extend, partial, d_spl, d_typ, level1 ? d_score : nullptr, st));
         stage_check(st, "aff_hb_join");
         HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + (level1 ? 1 : 0)) * 4, hipMemcpyDeviceToHost, st));
         {
@@ -1213,6 +1233,7 @@ int anyseq_score(int kind, const anyseq_scoring* sc, const char* query, int lenq
     try {
         const anyseq_scoring s = sc ? *sc : kAbiScoring;
         check_scoring(kind, s);
+        check_value_range(s, lenq, lens);
         const int64_t v = score_host(kind, s, query, lenq, subject, lens);
         if (score) *score = v;
         return 0;
@@ -1227,6 +1248,7 @@ int anyseq_score_device(int kind, const anyseq_scoring* sc, const uint8_t* d_que
     try {
         const anyseq_scoring s = sc ? *sc : kAbiScoring;
         check_scoring(kind, s);
+        check_value_range(s, lenq, lens);
         Engine& E = engine();
         std::lock_guard<std::mutex> lk(E.mu);
         hipStream_t st = stream ? (hipStream_t)stream : E.stream;
@@ -1244,6 +1266,7 @@ int anyseq_construct(int kind, const anyseq_scoring* sc, const char* query, int 
     try {
         const anyseq_scoring s = sc ? *sc : kAbiScoring;
         check_scoring(kind, s);
+        check_value_range(s, lenq, lens);
         if (s.gap_open != 0) {   // build-defined affine construct (true global / semiglobal / local)
             const int64_t v = construct_affine_host(kind, s, query, lenq, subject, lens, alQuery, alSubject);
             if (score) *score = v;
@@ -1264,6 +1287,7 @@ int anyseq_construct_device(int kind, const anyseq_scoring* sc, const uint8_t* d
     try {
         const anyseq_scoring s = sc ? *sc : kAbiScoring;
         check_scoring(kind, s);
+        check_value_range(s, lenq, lens);
         if (lenq < 0 || lens < 0) fail("negative sequence length");
         Engine& E = engine();
         std::lock_guard<std::mutex> lk(E.mu);

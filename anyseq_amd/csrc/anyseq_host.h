@@ -105,6 +105,7 @@ struct Engine {
     DevBuf q, s, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq, als;
     DevBuf LE, RE, typ, pos;   // affine construct
     DevBuf status;             // affine construct: splits | types | score of a level (one download)
+    DevBuf joinbuf;            // affine construct: per-slice partial maxima of the level's joins
     PinBuf pin_up, pin_down;   // affine construct: staged uploads / downloads of a level
     std::vector<int32_t> host_i32;
     std::vector<BlockInfo> host_blocks;
@@ -123,6 +124,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc);
 // border mode and clamp / best bits (DPProblem::bmode / amode).
 void set_aff_kind(DPProblem& P, int kind);
 void check_scoring(int kind, const anyseq_scoring& sc);
+void check_value_range(const anyseq_scoring& sc, int64_t n, int64_t m);
 
 // Enqueues one batched fill over `probs` on `st` (the problems' nbands/ngroups/
 // wpad/rowbuf/flags are filled in here).  grid <= 0: the tuning's grid.

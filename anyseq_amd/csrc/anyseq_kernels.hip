@@ -2067,6 +2067,103 @@ __global__ __launch_bounds__(256) void aff_hb_join_kernel(const PartInfo* __rest
     }
 }
 
+// The same join in two stages for long parts: stage 1 takes the first maximum of one
+// slice of a part's candidates per workgroup (slice 0 also tries BEFORE / AFTER),
+// stage 2 combines a part's slices in order (larger value, then the earlier key).
+constexpr int kJoinSlice = 4096;
+__global__ __launch_bounds__(256) void aff_hb_join_slice_kernel(const PartInfo* __restrict__ parts, int half,
+                                                                const int32_t* __restrict__ LH,
+                                                                const int32_t* __restrict__ LE,
+                                                                const int32_t* __restrict__ RH,
+                                                                const int32_t* __restrict__ RE,
+                                                                const int32_t* __restrict__ pbest, int go, int ge,
+                                                                int nslices, int2* __restrict__ partial) {
+    __shared__ int sv[256], sk[256];
+    const int part = blockIdx.y, slice = blockIdx.x;
+    const PartInfo pi = parts[part];
+    const int off = pi.off, len = pi.len;
+    int best = -2147483647, key = 0x7fffffff;
+    if (!(pi.flags & 4)) {
+        const bool sfree = pi.flags & 1, efree = pi.flags & 2;
+        const int bLH = aff_top_h(pi.smode, half - 1, go, ge), bLE = sfree ? kAffNeg : bLH;
+        const int bRH = aff_top_h(pi.emode, pi.rhw - 1, go, ge), bRE = efree ? kAffNeg : bRH;
+        if (slice == 0 && threadIdx.x == 0) {
+            if (efree && pbest[2 * part] > best) {
+                best = pbest[2 * part];
+                key = 0;
+            }
+            if (sfree && pbest[2 * part + 1] > best) {
+                best = pbest[2 * part + 1];
+                key = 1;
+            }
+        }
+        const int i0 = slice * kJoinSlice - 1, i1 = min(len, i0 + kJoinSlice);
+        for (int i = i0 + (int)threadIdx.x; i < i1; i += blockDim.x) {
+            const int k = len - i - 2;
+            const int hl = i < 0 ? bLH : LH[off + i], el = i < 0 ? bLE : LE[off + i];
+            const int hr = k < 0 ? bRH : RH[off + k], er = k < 0 ? bRE : RE[off + k];
+            const int vh = hl + hr, ve = el + er - go;
+            if (vh > best) {
+                best = vh;
+                key = 2 + 2 * (i + 1);
+            }
+            if (ve > best) {
+                best = ve;
+                key = 3 + 2 * (i + 1);
+            }
+        }
+    }
+    sv[threadIdx.x] = best;
+    sk[threadIdx.x] = key;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            const int v2 = sv[threadIdx.x + o], k2 = sk[threadIdx.x + o];
+            if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && k2 < sk[threadIdx.x])) {
+                sv[threadIdx.x] = v2;
+                sk[threadIdx.x] = k2;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[(size_t)part * nslices + slice] = make_int2(sv[0], sk[0]);
+}
+
+__global__ void aff_hb_join_final_kernel(const PartInfo* __restrict__ parts, int nparts, int nslices,
+                                         const int2* __restrict__ partial, int32_t* splits, int32_t* types,
+                                         int32_t* score) {
+    const int part = blockIdx.x * blockDim.x + threadIdx.x;
+    if (part >= nparts) return;
+    const PartInfo pi = parts[part];
+    if (pi.flags & 4) {
+        splits[pi.split_index + 1] = pi.off;
+        types[pi.split_index + 1] = pi.empty_type;
+        return;
+    }
+    int best = -2147483647, kk = 0x7fffffff;
+    for (int sl = 0; sl < nslices; ++sl) {
+        const int2 v = partial[(size_t)part * nslices + sl];
+        if (v.x > best || (v.x == best && v.y < kk)) {
+            best = v.x;
+            kk = v.y;
+        }
+    }
+    int type, spl;
+    if (kk == 0) {
+        type = T_BEFORE;
+        spl = pi.off + pi.len;
+    } else if (kk == 1) {
+        type = T_AFTER;
+        spl = pi.off;
+    } else {
+        type = (kk & 1) ? T_E : T_H;
+        spl = pi.off + (kk - 2) / 2;
+    }
+    splits[pi.split_index + 1] = spl;
+    types[pi.split_index + 1] = type;
+    if (score && part == 0) *score = best;
+}
+
 // Transposed Hirschberg halves: the bottom row (G, F-down) of
 // the transposed problem is the original's last column (H, E-right) -> H space.
 // E-right = max(E, H + go) instead of E changes no join decision: an E candidate
@@ -2404,6 +2501,21 @@ hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, co
     if (nparts > 0)
         hipLaunchKernelGGL(anyseq::aff_hb_join_kernel, dim3(nparts), dim3(256), 0, st,
                            (const anyseq::PartInfo*)parts, half, LH, LE, RH, RE, pbest, go, ge, splits, types, score);
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_aff_hb_join2(const void* parts, int nparts, int maxlen, int half, const int32_t* LH,
+                                      const int32_t* LE, const int32_t* RH, const int32_t* RE, const int32_t* pbest,
+                                      int go, int ge, void* partial, int32_t* splits, int32_t* types, int32_t* score,
+                                      hipStream_t st) {
+    using namespace anyseq;
+    const int nslices = std::max(1, (maxlen + 1 + kJoinSlice - 1) / kJoinSlice);
+    if (nparts > 0) {
+        hipLaunchKernelGGL(aff_hb_join_slice_kernel, dim3(nslices, nparts), dim3(256), 0, st,
+                           (const PartInfo*)parts, half, LH, LE, RH, RE, pbest, go, ge, nslices, (int2*)partial);
+        hipLaunchKernelGGL(aff_hb_join_final_kernel, dim3((nparts + 63) / 64), dim3(64), 0, st,
+                           (const PartInfo*)parts, nparts, nslices, (const int2*)partial, splits, types, score);
+    }
     return hipGetLastError();
 }
 

@@ -485,6 +485,7 @@ void dump_shards(const char* path, std::vector<Shard>& shards, int N, int kind, 
 
 void check_shard_shape(int kind, const anyseq_scoring& sc, int n, int m, int N) {
     check_scoring(kind, sc);
+    check_value_range(sc, n, m);
     if (N < 1) fail("sharded fill: need at least one shard");
     if (n < 2) fail("sharded fill: need at least 2 query rows (two fronts), got %d", n);
     if (m < N) fail("sharded fill: %d columns cannot be split over %d shards", m, N);
@@ -780,6 +781,7 @@ int anyseq_shard_finalize(void) {
 static int64_t sharded_construct(int kind, const anyseq_scoring& s, const char* query, int lenq, const char* subject,
                                  int lens, char* alq, char* als, const ConstructShards& shards) {
     check_scoring(kind, s);
+    check_value_range(s, lenq, lens);
     if (s.gap_open == 0) fail("sharded construct: affine gaps only (gap_open < 0)");
     if (lenq < 0 || lens < 0) fail("negative sequence length");
     Engine& E = engine();

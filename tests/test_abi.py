@@ -67,3 +67,16 @@ def test_reference_driver_links_unchanged(tmp_path):
                            f"{src}/alignment_io.cpp", "-L", os.path.dirname(LIB), "-lanyseq",
                            f"-Wl,-rpath,{os.path.dirname(LIB)}", "-o", str(exe)])
     assert exe.exists()
+
+
+def test_value_range_guard_without_gpu():
+    """Scores x lengths that could leave the kernels' int32 range are rejected before any
+    GPU call: the error names the limit."""
+    import ctypes
+    import anyseq_amd as A
+    sc = A._scoring(1000, -1000, -1000, -1000)
+    out = ctypes.c_int64(0)
+    q = b"A" * 16
+    rc = A._lib.anyseq_score(0, ctypes.byref(sc), q, 200000, q, 200000, ctypes.byref(out))
+    assert rc == -1
+    assert b"int32 value range" in A._lib.anyseq_last_error()
