@@ -53,10 +53,9 @@ hipError_t anyseq_launch_aff_hb_join2(const void* parts, int nparts, int maxlen,
                                       const int32_t* LE, const int32_t* RH, const int32_t* RE, const int32_t* pbest,
                                       int go, int ge, void* partial, int32_t* splits, int32_t* types, int32_t* score,
                                       hipStream_t st);
-hipError_t anyseq_launch_aff_pred(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
-                                  int match, int mismatch, int go, int ge, hipStream_t st);
-hipError_t anyseq_launch_aff_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
-                                  const uint8_t* pred, uint8_t* alq, uint8_t* als, hipStream_t st);
+hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
+                                      int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als,
+                                      hipStream_t st);
 }
 
 namespace anyseq {
@@ -191,6 +190,7 @@ void init_tuning_locked() {
     g_tuning.affasm = env_int("ANYSEQ_AFFINE_ASM", g_tuning.affasm);
     g_tuning.afft = env_int("ANYSEQ_AFFINE_TRANSPOSE", g_tuning.afft);
     g_tuning.prio = env_int("ANYSEQ_PRIO", g_tuning.prio);
+    g_tuning.thr = env_int("ANYSEQ_THROTTLE", g_tuning.thr);
     g_tuning.NWa = env_int("ANYSEQ_NWA", g_tuning.NWa);
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning_init = true;
@@ -302,6 +302,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     FillParams fpl = fp;
     fpl.epoch = epoch;
     fpl.prio = g_tuning.prio;
+    fpl.throttle = g_tuning.thr;
     unsigned long long* dbg = nullptr;
     static DevBuf stamp_buf;
     if (getenv("ANYSEQ_STAMPS")) {
@@ -1029,7 +1030,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         bi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, bi.oj == 0);
         bi.e_end = te == T_H ? 0 : te == T_E ? 1 : 2;
         bi.flags = (local ? 1 : 0) | (bi.oj + bi.w == m ? 2 : 0);
-        if (bi.h > 0) pred_bytes += (int64_t)(bi.h + 127) * 128;
+        if (bi.h > kPredLdsRows) pred_bytes += (int64_t)(bi.h + 127) * 128;   // (shorter blocks: LDS)
         blocks.push_back(bi);
     }
     if (blocks.empty()) {
@@ -1042,11 +1043,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
     HIPCHECK(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, st));
     uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
-    HIPCHECK(anyseq_launch_aff_pred(d_blocks, (int)blocks.size(), dq, ds, d_pred, sc.match, sc.mismatch,
-                                    sc.gap_open, sc.gap_extend, st));
-    stage_check(st, "aff_pred");
-    HIPCHECK(anyseq_launch_aff_walk(d_blocks, (int)blocks.size(), dq, ds, d_pred, d_alq, d_als, st));
-    stage_check(st, "aff_walk");
+    HIPCHECK(anyseq_launch_aff_predwalk(d_blocks, (int)blocks.size(), dq, ds, d_pred, sc.match, sc.mismatch,
+                                        sc.gap_open, sc.gap_extend, d_alq, d_als, st));
+    stage_check(st, "aff_predwalk");
     if (shards && !shards->local) {
         // blocks write disjoint positions over a ' ' prefill, and every written byte
         // ('_' or a symbol) is above ' ': a byte-wise MAX merges the ranks' strings
@@ -1342,6 +1341,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "ring_slots") g_tuning.ring_slots = value;
     else if (n == "affine_transpose") g_tuning.afft = value;
     else if (n == "priority") g_tuning.prio = value;
+    else if (n == "throttle") g_tuning.thr = value;
     else return -1;
     return 0;
 }

@@ -68,6 +68,7 @@ struct Tuning {
     int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
     int afft = 1;        // affine construct: run Hirschberg halves taller than wide transposed
     int prio = 0;        // compute waves at s_setprio 3 (the I/O wave stays at 0)
+    int thr = 0;         // band 0 of every problem sleeps thr s_sleep-1 units per block (chain pace)
 };
 extern Tuning g_tuning;
 

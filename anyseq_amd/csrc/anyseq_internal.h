@@ -107,6 +107,7 @@ struct FillParams {
     unsigned long long* dbg;          // diagnostic build only (ANYSEQ_STAMPS): per-launch stamp sums
     int32_t epoch;                    // launch counter: descriptors carry it (stale uploads are detected)
     int32_t prio;                     // compute waves raise their issue priority (s_setprio 3) when set
+    int32_t throttle;                 // s_sleep 1 units per block in a problem's band 0 (chain pace)
 };
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).
@@ -131,6 +132,11 @@ struct BlockInfo {
     int32_t flags;        // affine construct: bit 0 local (free end = any cell), bit 1 holds the last column
     int32_t xi, xj;       // affine construct, free end: the exit cell (written by aff_pred_kernel)
 };
+
+// Affine final level (aff_predwalk_kernel): blocks of at most kPredLdsRows rows
+// keep their predecessor bytes and query rows in LDS; taller ones use an HBM slab.
+constexpr int kPredLdsRows = 376;
+constexpr int kPredLdsBytes = (kPredLdsRows + 127) * 128 + kPredLdsRows;   // 64760 <= 64 KiB
 
 // Device-side error codes written to the error word.
 enum : uint32_t { ERR_NONE = 0, ERR_SPIN_TIMEOUT = 1, ERR_BAD_DESC = 0x100 };

@@ -123,6 +123,7 @@ struct FillShared {
 // local wm = match - gap, wx = mismatch - gap, and H = sat(x - ng).
 struct CellK {
     int wm, wx, ng;
+    int thr;   // FillParams::throttle
 };
 
 // LDS progress counters between waves of one workgroup.  The LDS executes one
@@ -317,7 +318,7 @@ struct LoopArgs {
                  : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [rb] "s"(rb), [nb] "s"(nb),       \
                    [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc), [asf] "v"(la.asf), \
                    [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4), [bvb] "v"(la.bvb), \
-                   [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp)                                                  \
+                   [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp), [thr] "s"(thr)                                   \
                  : ANYSEQ_LOOP2_ASM_CLOBBERS, "memory")
 #define AQ_ASM_L(NAME)                                                                                          \
     asm volatile(NAME                                                                                          \
@@ -327,7 +328,7 @@ struct LoopArgs {
                  : [be] "s"(be), [q] "v"(q), [wm] "v"(ck.wm), [wx] "v"(ck.wx), [ng] "v"(ck.ng), [rb] "s"(rb),   \
                    [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp), [anc] "v"(la.anc),     \
                    [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo), [lid4] "v"(la.lid4), \
-                   [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp)                               \
+                   [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp), [thr] "s"(thr)                \
                  : ANYSEQ_LOOP2_ASM_CLOBBERS, "memory")
 template <int KIND, bool BORDER, int PUB>
 __device__ __forceinline__ uint32_t band_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
@@ -342,7 +343,7 @@ __device__ __forceinline__ uint32_t band_loop_asm(uint32_t& b, uint32_t be, uint
     sf = RFL(sf);
     sc = RFL(sc);
     be = RFL(be);
-    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs);
+    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), thr = RFL((uint32_t)ck.thr);
     // (readfirstlane returns int: widen through uint32_t, or bit 31 sign-extends into the high half)
     const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
 #undef RFL
@@ -920,6 +921,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     CellK ck;
     ck.ng = -fp.gap;
+    ck.thr = fp.throttle;
     if (KIND == KIND_LOCAL) {
         ck.wm = fp.match - fp.gap;
         ck.wx = fp.mismatch - fp.gap;
@@ -1035,6 +1037,7 @@ struct AffK {
     int go;       // gap open (<= 0): added to a cell to open a gap (G space)
     int nge;      // -ge > 0
     int flags;    // bit 0: no asm steady state, bit 2: no asm prologue (diagnostics)
+    int thr;      // FillParams::throttle
 };
 
 // Borders of a problem in G space (H border values by border mode, see
@@ -1139,7 +1142,8 @@ struct AffLoopArgs {
                  : [be] "s"(be), [q] "v"(q), [wm] "v"(k.wm), [wx] "v"(k.wx), [go] "v"(k.go), [nge] "s"(nge),     \
                    [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp),          \
                    [anc] "v"(la.anc), [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo),  \
-                   [lid8] "v"(la.lid8), [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp)            \
+                   [lid8] "v"(la.lid8), [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp),           \
+                   [thr] "s"(thr)                                                                              \
                  : ANYSEQ_AFF_ASM_CLOBBERS, "memory")
 // L: the clamp + best loop (any amode != 0), else the plain loop.
 template <bool L, bool BORDER, int PUB>
@@ -1156,7 +1160,7 @@ __device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint3
     be = RFL(be);
     z = RFL(z);
     zb = RFL(zb);
-    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), nge = RFL(k.nge);
+    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), nge = RFL(k.nge), thr = RFL((uint32_t)k.thr);
     const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
 #undef RFL
     int tfg = tf.x, tff = tf.y;
@@ -1194,7 +1198,7 @@ __device__ __forceinline__ uint32_t aff_prologue_asm(uint32_t& sp, uint32_t& sf,
     sc = RFL(sc);
     z = RFL(z);
     zb = RFL(zb);
-    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), nge = RFL(k.nge);
+    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), nge = RFL(k.nge), thr = 0;
     const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
 #undef RFL
     int tfg = tf.x, tff = tf.y;
@@ -1478,6 +1482,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
     k.wm = fp.match + 2 * k.nge;
     k.wx = fp.mismatch + 2 * k.nge;
     k.flags = fp.pad;
+    k.thr = fp.throttle;
     if (fp.prio && wave < NW) __builtin_amdgcn_s_setprio(3);   // compute waves before the I/O wave
     for (;;) {
         if (threadIdx.x == 0) {
@@ -2194,14 +2199,11 @@ __global__ void aff_row_to_col_kernel(const RowToCol* __restrict__ jobs, int nge
 // exit cell: local, the first maximum of all cells in row-major order;
 // semiglobal, the first maximum of the last row, then of the last column (when
 // the block holds it) if strictly greater -> blocks[b].xi / xj.
-__global__ __launch_bounds__(64) void aff_pred_kernel(BlockInfo* __restrict__ blocks, int nblocks,
-                                                      const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
-                                                      uint8_t* __restrict__ pred, int match, int mismatch, int go,
-                                                      int ge) {
-    const int b = blockIdx.x;
-    if (b >= nblocks) return;
-    const BlockInfo bi = blocks[b];
-    if (bi.h <= 0) return;
+// PB: the predecessor slab (LDS or HBM), QB: the block's query rows (LDS:
+// staged, HBM: Q + oi).  Returns the exit cell (xi, xj) of a free end in every lane.
+template <typename PB, typename QB>
+__device__ __forceinline__ int2 aff_pred_block(const BlockInfo& bi, QB qrow, const uint8_t* __restrict__ S, PB pred,
+                                               int match, int mismatch, int go, int ge) {
     const int lane = threadIdx.x;
     const int NEG = kAffNeg;
     const int bm = bi.smode;
@@ -2224,7 +2226,6 @@ __global__ __launch_bounds__(64) void aff_pred_kernel(BlockInfo* __restrict__ bl
     // exit candidates: per column the first row reaching its best (local), the last
     // row's value (semiglobal), the last column's first maximum (semiglobal)
     int xvA = -2147483647, xrA = 0, xvB = -2147483647, xrB = 0, cv = -2147483647, cr = 0;
-    uint16_t* out16 = reinterpret_cast<uint16_t*>(pred + bi.pred_base);
     const int nsteps = bi.h + 127;
     for (int d = 0; d < nsteps; ++d) {
         const int iA = d - jA, iB = d - jB;
@@ -2233,8 +2234,8 @@ __global__ __launch_bounds__(64) void aff_pred_kernel(BlockInfo* __restrict__ bl
         const int lE = wave_shr1(NEG, EB);
         const bool actA = iA >= 0 && iA < bi.h && jA < bi.w;
         const bool actB = iB >= 0 && iB < bi.h && jB < bi.w;
-        const int qA = (iA >= 0 && iA < bi.h) ? (int)Q[bi.oi + iA] : 0x200;
-        const int qB = (iB >= 0 && iB < bi.h) ? (int)Q[bi.oi + iB] : 0x200;
+        const int qA = (iA >= 0 && iA < bi.h) ? (int)qrow[iA] : 0x200;
+        const int qB = (iB >= 0 && iB < bi.h) ? (int)qrow[iB] : 0x200;
         // B (uses A's state before A's update: A at row iB)
         int pB = 0;
         int eB;
@@ -2296,7 +2297,7 @@ __global__ __launch_bounds__(64) void aff_pred_kernel(BlockInfo* __restrict__ bl
             }
         }
         const uint16_t pk = (uint16_t)((actA ? pA : 0) | ((actB ? pB : 0) << 8));
-        out16[(size_t)d * 64 + lane] = pk;
+        reinterpret_cast<uint16_t*>(pred)[d * 64 + lane] = pk;
     }
     if (xfree) {
         // best (value, row, column) of the lane: A before B (same row: smaller column)
@@ -2325,26 +2326,20 @@ __global__ __launch_bounds__(64) void aff_pred_kernel(BlockInfo* __restrict__ bl
                 c = bi.w - 1;
             }
         }
-        if (lane == 0) {
-            blocks[b].xi = r;
-            blocks[b].xj = c;
-        }
+        return make_int2(r, c);
     }
+    return make_int2(0, 0);
 }
 
-// One thread per block: walk from the block's end (bottom-right in state H or E,
-// or the free exit cell) back to its start (anchored: the corner through the
-// border's gap runs; free: a clamped cell or the border); sparse i+j+1 output.
-__global__ void aff_walk_kernel(const BlockInfo* __restrict__ blocks, int nblocks, const uint8_t* __restrict__ Q,
-                                const uint8_t* __restrict__ S, const uint8_t* __restrict__ pred, uint8_t* alq,
-                                uint8_t* als) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nblocks) return;
-    const BlockInfo bi = blocks[b];
-    if (bi.e_end == 2 && bi.h <= 0) return;   // the path ended at the block's corner
+// One thread: walk from the block's end (bottom-right in state H or E, or the
+// free exit cell x) back to its start (anchored: the corner through the border's
+// gap runs; free: a clamped cell or the border); sparse i+j+1 output.
+template <typename PB>
+__device__ __forceinline__ void aff_walk_block(const BlockInfo& bi, int2 x, const uint8_t* __restrict__ Q,
+                                               const uint8_t* __restrict__ S, PB pred, uint8_t* alq, uint8_t* als) {
     const bool free_start = bi.smode >= BM_FREE_LOCAL;
     const int64_t base = (int64_t)bi.oi + bi.oj;
-    int i = bi.e_end == 2 ? bi.xi : bi.h - 1, j = bi.e_end == 2 ? bi.xj : bi.w - 1;
+    int i = bi.e_end == 2 ? x.x : bi.h - 1, j = bi.e_end == 2 ? x.y : bi.w - 1;
     int st = bi.e_end == 1 ? 1 : 0;
     while (i >= 0 || j >= 0) {
         const int64_t pos = base + i + j + 1;
@@ -2361,7 +2356,7 @@ __global__ void aff_walk_kernel(const BlockInfo* __restrict__ blocks, int nblock
             }
             continue;
         }
-        const int pb = pred[bi.pred_base + (int64_t)(i + j) * 128 + j];
+        const int pb = pred[(i + j) * 128 + j];
         if (st == 0) {
             const int hs = pb & 3;
             if (hs == 3) break;   // clamped: the path starts after this cell
@@ -2384,6 +2379,44 @@ __global__ void aff_walk_kernel(const BlockInfo* __restrict__ blocks, int nblock
             st = (pb & 8) ? 2 : 0;
             --i;
         }
+    }
+}
+
+
+// Final level, one wave per 128-column block: predecessors (aff_pred_block), then
+// lane 0 walks them (aff_walk_block) in the same launch.  A block of h <=
+// kPredLdsRows rows keeps its query rows and its (h + 127) x 128 predecessor
+// bytes in LDS, so neither the sweep's query reads nor the walk's dependent reads
+// go to HBM; taller blocks (long vertical gaps) use the HBM slab at pred_base.
+__global__ __launch_bounds__(64) void aff_predwalk_kernel(BlockInfo* __restrict__ blocks, int nblocks,
+                                                          const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
+                                                          uint8_t* __restrict__ pred, int match, int mismatch, int go,
+                                                          int ge, uint8_t* alq, uint8_t* als) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t pw_lds[];
+    const int b = blockIdx.x;
+    if (b >= nblocks) return;
+    const BlockInfo bi = blocks[b];
+    if (bi.e_end == 2 && bi.h <= 0) return;   // the path ended at the block's corner
+    int2 x = make_int2(0, 0);
+    if (bi.h > 0 && bi.h <= kPredLdsRows) {
+        uint8_t* qs = pw_lds + (kPredLdsRows + 127) * 128;
+        for (int i = threadIdx.x; i < bi.h; i += 64) qs[i] = Q[bi.oi + i];
+        __syncthreads();
+        x = aff_pred_block(bi, (const uint8_t*)qs, S, pw_lds, match, mismatch, go, ge);
+        __syncthreads();
+        if (threadIdx.x == 0) aff_walk_block(bi, x, Q, S, (const uint8_t*)pw_lds, alq, als);
+    } else {
+        uint8_t* slab = pred + bi.pred_base;
+        if (bi.h > 0) {
+            x = aff_pred_block(bi, Q + bi.oi, S, slab, match, mismatch, go, ge);
+            __threadfence_block();
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) aff_walk_block(bi, x, Q, S, (const uint8_t*)slab, alq, als);
+    }
+    if (threadIdx.x == 0 && bi.e_end == 2) {
+        blocks[b].xi = x.x;
+        blocks[b].xj = x.y;
     }
 }
 
@@ -2526,19 +2559,12 @@ hipError_t anyseq_launch_aff_row_to_col(const void* jobs, int njobs, int maxn, i
     return hipGetLastError();
 }
 
-hipError_t anyseq_launch_aff_pred(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
-                                  int match, int mismatch, int go, int ge, hipStream_t st) {
+hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
+                                      int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als,
+                                      hipStream_t st) {
     if (nblocks > 0)
-        hipLaunchKernelGGL(anyseq::aff_pred_kernel, dim3(nblocks), dim3(64), 0, st, (anyseq::BlockInfo*)blocks,
-                           nblocks, Q, S, pred, match, mismatch, go, ge);
-    return hipGetLastError();
-}
-
-hipError_t anyseq_launch_aff_walk(const void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S,
-                                  const uint8_t* pred, uint8_t* alq, uint8_t* als, hipStream_t st) {
-    if (nblocks > 0)
-        hipLaunchKernelGGL(anyseq::aff_walk_kernel, dim3((nblocks + 63) / 64), dim3(64), 0, st,
-                           (const anyseq::BlockInfo*)blocks, nblocks, Q, S, pred, alq, als);
+        hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(nblocks), dim3(64), anyseq::kPredLdsBytes, st,
+                           (anyseq::BlockInfo*)blocks, nblocks, Q, S, pred, match, mismatch, go, ge, alq, als);
     return hipGetLastError();
 }
 

@@ -116,11 +116,12 @@ TA, TB = 96, 98                                   # fixed SGPR pairs for s_memre
 
 def wait(e, name, seen, target, addr, count=None, tmp=None):
     """Spin until seen >= target, refreshing `seen` from the LDS word at `addr`
-    (wave-uniform), with s_sleep between polls and a 10 s s_memrealtime limit
-    checked every 256 polls (-> L_timeout)."""
+    (wave-uniform), with s_sleep between polls.  The 10 s s_memrealtime limit
+    starts at the 256th poll and is checked every 256 polls (-> L_timeout): the
+    common case (ready within a few polls) issues no SMEM read, whose latency the
+    poll's lgkmcnt(0) would otherwise wait for on the hand-off's critical path."""
     e(f"s_cmp_ge_u32 {seen}, {target}")
     e(f"s_cbranch_scc1 L_{name}_ok_%=")
-    e(f"s_memrealtime s[{TA}:{TA + 1}]")
     e("s_mov_b32 %[x3], 0")
     e(f"L_{name}_loop_%=:")
     tmp = VT2 if tmp is None else tmp
@@ -136,6 +137,12 @@ def wait(e, name, seen, target, addr, count=None, tmp=None):
     e("s_add_u32 %[x3], %[x3], 1")
     e("s_and_b32 %[x2], %[x3], 255")
     e(f"s_cbranch_scc1 L_{name}_loop_%=")
+    e("s_cmp_eq_u32 %[x3], 256")
+    e(f"s_cbranch_scc0 L_{name}_chk_%=")
+    e(f"s_memrealtime s[{TA}:{TA + 1}]")
+    e("s_waitcnt lgkmcnt(0)")
+    e(f"s_branch L_{name}_loop_%=")
+    e(f"L_{name}_chk_%=:")
     e(f"s_memrealtime s[{TB}:{TB + 1}]")
     e("s_waitcnt lgkmcnt(0)")
     e(f"s_sub_u32 s{TB}, s{TB}, s{TA}")
@@ -149,6 +156,21 @@ def wait(e, name, seen, target, addr, count=None, tmp=None):
 
 
 SKB_ = 142   # second subject-word set (double buffer): v142..v149
+
+
+def throttle(e, k):
+    """Band 0 of a problem (the only band that waits for nothing) sleeps %[thr]
+    s_sleep-1 units per block: the chain then runs at band 0's slightly slower
+    pace, and every later band has slack to absorb its hand-off jitter instead of
+    adding it to the chain."""
+    e("s_mov_b32 %[x2], %[thr]")
+    e(f"L_thr{k}_%=:")
+    e("s_cmp_eq_u32 %[x2], 0")
+    e(f"s_cbranch_scc1 L_thrd{k}_%=")
+    e("s_sleep 1")
+    e("s_sub_u32 %[x2], %[x2], 1")
+    e(f"s_branch L_thr{k}_%=")
+    e(f"L_thrd{k}_%=:")
 
 
 def gen_loop2(kind, border, pub, ts=False):
@@ -189,6 +211,7 @@ def gen_loop2(kind, border, pub, ts=False):
             e(f"v_and_b32_e32 v{VT2}, 0x7ff, v{VT2}")
             e(f"v_add_u32_e32 v{VT2}, %[rb], v{VT2}")
             e(f"ds_write_b32 v{VT2}, v{VT}")
+            throttle(e, k)
         else:
             wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", "%[npr]" if ts else None)
         if ts:
@@ -344,6 +367,7 @@ def gen_loop_aff(kind, border, pub):
             e(f"v_add_u32_e32 v{AVA}, %[rb], v{AVA}")
             e(f"ds_write_b64 v{AVA}, v[{AVT}:{AVT + 1}]")
             e("s_waitcnt lgkmcnt(0)")
+            throttle(e, k)
         else:
             wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=AVT2)
         if pub == "lds":
