@@ -49,12 +49,14 @@ hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, co
                                      const int32_t* RH, const int32_t* RE, const int32_t* pbest, int go, int ge,
                                      int32_t* splits, int32_t* types, int32_t* score, hipStream_t st);
 hipError_t anyseq_launch_aff_row_to_col(const void* jobs, int njobs, int maxn, int nge, hipStream_t st);
+hipError_t anyseq_launch_fill_prep(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
+                                   void* sent, size_t sent_bytes, uint32_t sent_value, hipStream_t st);
 hipError_t anyseq_launch_aff_hb_join2(const void* parts, int nparts, int maxlen, int half, const int32_t* LH,
                                       const int32_t* LE, const int32_t* RH, const int32_t* RE, const int32_t* pbest,
                                       int go, int ge, void* partial, int32_t* splits, int32_t* types, int32_t* score,
                                       hipStream_t st);
 hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
-                                      int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als,
+                                      int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows,
                                       hipStream_t st);
 }
 
@@ -219,7 +221,8 @@ int waves_per_group() {
 // Prepares one batched fill launch over `probs` (host copies; device pointers set):
 // every allocation, upload and sentinel fill, enqueued on st.  No kernel yet.
 void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
-                  int grid_req) {
+                  int grid_req, const void* extra, size_t extra_bytes, int32_t* init, int init_words,
+                  int32_t init_value) {
     C.init();
     C.pending = false;
     const bool aff = fp.affine != 0;
@@ -255,50 +258,60 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
         flag_words += P.ngroups;
     }
     int32_t* rowbuf = (int32_t*)C.rowbuf.get(rowbuf_ints * 4);
-    uint32_t* flags = (uint32_t*)C.flags.get((flag_words + 4) * 4);
+    // group table: round-robin over problems so every sub-problem progresses
+    std::vector<GroupRef>& groups = C.h_groups;
+    groups.clear();
+    for (int k = 0; k < max_groups; ++k)
+        for (size_t p = 0; p < probs.size(); ++p)
+            if (k < probs[p].ngroups) groups.push_back(GroupRef{(int32_t)p, k, 0, 0});
+    // ONE device block per launch: [counters (32 words) | group flags | descriptors |
+    // group table | caller's extra payload], so the launch costs one upload and one
+    // memset besides the hand-off rows' sentinel fill
+    const size_t zb = ((32 + flag_words) * 4 + 255) & ~(size_t)255;
+    const size_t pb = probs.size() * sizeof(DPProblem), gb = groups.size() * sizeof(GroupRef);
+    const size_t eoff = (pb + gb + 15) & ~(size_t)15;
+    const size_t ub = eoff + extra_bytes;
+    char* meta = (char*)C.probs.get(zb + ub);
+    uint32_t* ctr = (uint32_t*)meta;   // [0] dequeue counter, [1] error word
+    uint32_t* flags = ctr + 32;
+    DPProblem* d_probs = (DPProblem*)(meta + zb);
+    GroupRef* d_groups = (GroupRef*)(meta + zb + pb);
+    C.d_extra = extra_bytes ? meta + zb + eoff : nullptr;
     size_t ro = 0, fo = 0;
     static std::atomic<int32_t> g_epoch{0};
     const int32_t epoch = (g_epoch.fetch_add(1) + 1) & 0x7ffff;
     for (size_t i = 0; i < probs.size(); ++i) probs[i].magic = kProbMagic ^ (int32_t)i ^ (epoch << 12);
+    for (auto& g : groups) g.epoch = epoch;
     for (auto& P : probs) {
         P.rowbuf = rowbuf + ro;
         P.flags = flags + fo;
         ro += (size_t)(P.ngroups > 1 ? P.nslots : 0) * P.wpad * vpc;
         fo += P.ngroups;
     }
-    // group table: round-robin over problems so every sub-problem progresses
-    std::vector<GroupRef>& groups = C.h_groups;
-    groups.clear();
-    for (int k = 0; k < max_groups; ++k)
-        for (size_t p = 0; p < probs.size(); ++p)
-            if (k < probs[p].ngroups) groups.push_back(GroupRef{(int32_t)p, k, epoch, 0});
     C.R = R;
     C.NW = NW;
+    C.h_probs = probs;
+    // staged in pinned memory (a truly asynchronous copy); the previous launch of this
+    // context has completed (fill_finish / fill_collect), so the staging area is free
+    char* pin = (char*)C.pin.get(64 + ub);
+    C.err_host = (uint32_t*)pin;
+    memcpy(pin + 64, C.h_probs.data(), pb);
+    memcpy(pin + 64 + pb, groups.data(), gb);
+    if (extra_bytes) memcpy(pin + 64 + eoff, extra, extra_bytes);
+    if (ub) HIPCHECK(hipMemcpyAsync(meta + zb, pin + 64, ub, hipMemcpyHostToDevice, st));
     if (groups.empty()) {
+        if (init_words) HIPCHECK(hipMemsetD32Async(init, init_value, (size_t)init_words, st));
         if (C.err_host) *C.err_host = 0u;   // (no copy targets it: the previous launch has completed)
         HIPCHECK(hipEventRecord(C.ev0, st));
         HIPCHECK(hipEventRecord(C.ev1, st));
         HIPCHECK(hipEventRecord(C.ev2, st));
         return;
     }
-    DPProblem* d_probs = (DPProblem*)C.probs.get(probs.size() * sizeof(DPProblem));
-    GroupRef* d_groups = (GroupRef*)C.groups.get(groups.size() * sizeof(GroupRef));
-    C.h_probs = probs;
-    // staged in pinned memory (a truly asynchronous copy); the previous launch of this
-    // context has completed (fill_finish / fill_collect), so the staging area is free
-    const size_t pb = probs.size() * sizeof(DPProblem), gb = groups.size() * sizeof(GroupRef);
-    char* pin = (char*)C.pin.get(64 + pb + gb);
-    C.err_host = (uint32_t*)pin;
-    memcpy(pin + 64, C.h_probs.data(), pb);
-    memcpy(pin + 64 + pb, groups.data(), gb);
-    HIPCHECK(hipMemcpyAsync(d_probs, pin + 64, pb, hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemcpyAsync(d_groups, pin + 64 + pb, gb, hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemsetAsync(flags, 0, flag_words * 4, st));
-    // group -> group hand-off rows start as a sentinel (the consumer polls the data):
-    // -1 for linear, 0x80808080 for affine
-    if (rowbuf_ints) HIPCHECK(hipMemsetAsync(rowbuf, aff ? 0x80 : 0xff, rowbuf_ints * 4, st));
-    uint32_t* ctr = (uint32_t*)C.ctr.get(128);
-    HIPCHECK(hipMemsetAsync(ctr, 0, 8, st));  // ctr[0] = dequeue counter, ctr[1] = error word
+    // counters and flags to 0, the caller's best cells to init_value, and the group ->
+    // group hand-off rows to the sentinel the consumer polls the data against (-1 for
+    // linear, 0x80808080 for affine): one launch
+    HIPCHECK(anyseq_launch_fill_prep(ctr, (int)(32 + flag_words), init, init_words, init_value, rowbuf,
+                                     rowbuf_ints * 4, aff ? 0x80808080u : 0xffffffffu, st));
     FillParams fpl = fp;
     fpl.epoch = epoch;
     fpl.prio = g_tuning.prio;
@@ -324,7 +337,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
 void fill_launch(FillCtx& C) {
     if (!C.pending) return;   // nothing to compute (events already recorded)
     C.pending = false;
-    uint32_t* ctr = (uint32_t*)C.ctr.p;
+    uint32_t* ctr = (uint32_t*)C.probs.p;   // the launch block's counters (fill_prepare)
     HIPCHECK(hipEventRecord(C.ev0, C.st));
     if (C.aff)
         HIPCHECK(anyseq_launch_fill_affine(C.NW, C.d_probs, C.d_groups, C.ngroups, ctr, ctr + 1, &C.fp, C.grid, C.st));
@@ -337,8 +350,9 @@ void fill_launch(FillCtx& C) {
 }
 
 void fill_async(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
-                int grid_req) {
-    fill_prepare(E, C, probs, fp, st, grid_req);
+                int grid_req, const void* extra, size_t extra_bytes, int32_t* init, int init_words,
+                int32_t init_value) {
+    fill_prepare(E, C, probs, fp, st, grid_req, extra, extra_bytes, init, init_words, init_value);
     fill_launch(C);
 }
 
@@ -362,6 +376,15 @@ std::string fill_summary(const FillCtx& C) {
         s += buf;
     }
     return s;
+}
+
+// The level's only synchronisation: poll the stream instead of a blocking wait, whose
+// wake-up (tens of microseconds) would sit between every two Hirschberg levels.
+hipError_t stream_wait_spin(hipStream_t st) {
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e == hipSuccess ? hipStreamSynchronize(st) : e;
+    }
 }
 
 void stage_check(hipStream_t st, const char* what) {
@@ -899,8 +922,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         const int half = pw / 2;
         const int parts = (m + half - 1) / pw;
         ++g_stage_level;
-        int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * parts * 4);
-        HIPCHECK(hipMemsetD32Async(pbest, kAffNegH, (size_t)2 * parts, st));
+        int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * parts * 4);   // (set by the level's first launch)
         std::vector<std::vector<DPProblem>> probs_of((size_t)nlaunch);
         std::vector<PartInfo>& pinfo = E.host_parts;
         pinfo.assign((size_t)parts, PartInfo{});
@@ -948,36 +970,51 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                          sfree ? pbest + 2 * p + 1 : nullptr, RH + off, RE + off);
         }
         // the level's parts and row-to-column jobs, staged together in pinned memory
-        const size_t jb = jobs.size() * sizeof(RowToColJob), pb = pinfo.size() * sizeof(PartInfo);
+        // (the jobs hold pointers: they start 16-byte aligned)
+        const size_t jb = jobs.size() * sizeof(RowToColJob), pb = (pinfo.size() * sizeof(PartInfo) + 15) & ~(size_t)15;
         char* up = (char*)E.pin_up.get(jb + pb + 16);
-        memcpy(up, pinfo.data(), pb);
+        memcpy(up, pinfo.data(), pinfo.size() * sizeof(PartInfo));
         memcpy(up + pb, jobs.data(), jb);
         // one fill launch per level is left running (collected after the level's single
         // synchronisation); local virtual ranks share the fill context, so all but the
-        // last of their launches complete in turn
+        // last of their launches complete in turn.  A single launch carries the parts and
+        // jobs in its own upload (fill_prepare's extra payload): one copy per level.
+        int nl = 0;
+        for (const auto& probs : probs_of) nl += probs.empty() ? 0 : 1;
         bool pending_fill = false;
+        const char* d_up = nullptr;
         for (size_t li = 0; li < probs_of.size(); ++li) {
             auto& probs = probs_of[li];
             if (probs.empty()) continue;
             if (pending_fill) fill_finish(E.fc);
-            fill_async(E, E.fc, probs, fp, st);
+            int32_t* init = pending_fill ? nullptr : pbest;   // the first launch of the level sets pbest
+            const int ninit = pending_fill ? 0 : 2 * parts;
+            if (nl == 1) {
+                fill_async(E, E.fc, probs, fp, st, 0, up, pb + jb, init, ninit, kAffNegH);
+                d_up = (const char*)E.fc.d_extra;
+            } else {
+                fill_async(E, E.fc, probs, fp, st, 0, nullptr, 0, init, ninit, kAffNegH);
+            }
             pending_fill = true;
+        }
+        if (!pending_fill) HIPCHECK(hipMemsetD32Async(pbest, kAffNegH, (size_t)2 * parts, st));
+        if (!d_up) {
+            char* d = (char*)E.parts.get(pb + jb + 16);
+            HIPCHECK(hipMemcpyAsync(d, up, pb + jb, hipMemcpyHostToDevice, st));
+            d_up = d;
         }
         stage_check(st, "affine fill");
         if (!jobs.empty()) {
             int maxn = 0;
             for (const auto& J : jobs) maxn = std::max(maxn, J.n);
-            void* d_jobs = E.jobs.get(jb);
-            HIPCHECK(hipMemcpyAsync(d_jobs, up + pb, jb, hipMemcpyHostToDevice, st));
-            HIPCHECK(anyseq_launch_aff_row_to_col(d_jobs, (int)jobs.size(), maxn, -sc.gap_extend, st));
+            HIPCHECK(anyseq_launch_aff_row_to_col(d_up + pb, (int)jobs.size(), maxn, -sc.gap_extend, st));
             stage_check(st, "aff_row_to_col");
         }
         if (shards && !shards->local) {   // every rank gets every part's columns and best cells
             for (int32_t* b : {LH, LE, RH, RE}) shards->sum_i32(b, (size_t)n, st);
             shards->max_i32(pbest, (size_t)2 * parts, st);
         }
-        PartInfo* d_parts = (PartInfo*)E.parts.get(pb);
-        HIPCHECK(hipMemcpyAsync(d_parts, up, pb, hipMemcpyHostToDevice, st));
+        const PartInfo* d_parts = (const PartInfo*)d_up;
         int maxlen = 0;
         for (const PartInfo& q : pinfo) maxlen = std::max(maxlen, (q.flags & 4) ? 0 : q.len);
         const size_t nsl = (size_t)std::max(1, (maxlen + 1 + 4095) / 4096);
@@ -987,7 +1024,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         stage_check(st, "aff_hb_join");
         HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + (level1 ? 1 : 0)) * 4, hipMemcpyDeviceToHost, st));
         {
-            const hipError_t e = hipStreamSynchronize(st);
+            const hipError_t e = stream_wait_spin(st);
             if (e != hipSuccess && pending_fill)
                 fail("fill failed: %s (%s)", hipGetErrorString(e), fill_summary(E.fc).c_str());
             HIPCHECK(e);
@@ -1017,6 +1054,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     std::vector<BlockInfo>& blocks = E.host_blocks;   // outlives the async upload
     blocks.clear();
     int64_t pred_bytes = 0;
+    int lds_rows = 1;   // the tallest block, up to kPredLdsMaxRows (its predecessors fit in LDS)
+    for (int b = 0; b < sp.nb; ++b)
+        if (!(tp(b - 1) == T_BEFORE || tp(b) == T_AFTER))
+            lds_rows = std::max(lds_rows, std::min(kPredLdsMaxRows, sp.at(b) - sp.at(b - 1)));
     for (int b = 0; b < sp.nb; ++b) {
         const int ts = tp(b - 1), te = tp(b);
         if (ts == T_BEFORE || te == T_AFTER) continue;   // the path does not touch the block
@@ -1030,7 +1071,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         bi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, bi.oj == 0);
         bi.e_end = te == T_H ? 0 : te == T_E ? 1 : 2;
         bi.flags = (local ? 1 : 0) | (bi.oj + bi.w == m ? 2 : 0);
-        if (bi.h > kPredLdsRows) pred_bytes += (int64_t)(bi.h + 127) * 128;   // (shorter blocks: LDS)
+        if (bi.h > lds_rows) pred_bytes += (int64_t)(bi.h + 127) * 128;   // (shorter blocks: LDS)
         blocks.push_back(bi);
     }
     if (blocks.empty()) {
@@ -1044,7 +1085,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     HIPCHECK(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, st));
     uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
     HIPCHECK(anyseq_launch_aff_predwalk(d_blocks, (int)blocks.size(), dq, ds, d_pred, sc.match, sc.mismatch,
-                                        sc.gap_open, sc.gap_extend, d_alq, d_als, st));
+                                        sc.gap_open, sc.gap_extend, d_alq, d_als, lds_rows, st));
     stage_check(st, "aff_predwalk");
     if (shards && !shards->local) {
         // blocks write disjoint positions over a ' ' prefill, and every written byte

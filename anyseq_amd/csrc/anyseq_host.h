@@ -75,7 +75,8 @@ extern Tuning g_tuning;
 // Buffers and events of one in-flight fill launch (one per concurrently running
 // fill: the engine has one, each local shard of the sharded driver its own).
 struct FillCtx {
-    DevBuf probs, groups, rowbuf, flags, ctr;
+    DevBuf probs;                           // launch block: counters | flags | descriptors | groups | extra
+    DevBuf groups, rowbuf, flags, ctr;      // (groups, flags: unused since the launch block; ctr: result words)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int R = 1, NW = 4;
     unsigned long long* stamps = nullptr;   // diagnostic build only
@@ -83,6 +84,7 @@ struct FillCtx {
     bool pending = false, aff = false;
     DPProblem* d_probs = nullptr;
     GroupRef* d_groups = nullptr;
+    void* d_extra = nullptr;                // the caller's extra payload in the launch block (fill_prepare)
     int ngroups = 0, grid = 0;
     int64_t cells = 0;                      // DP cells of the prepared launch (sum of h*w)
     FillParams fp{};
@@ -133,10 +135,12 @@ void check_value_range(const anyseq_scoring& sc, int64_t n, int64_t m);
 // synchronise the device, which must not happen while another shard's persistent
 // fill waits for this one) and fill_launch only enqueues the kernel.
 void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
-                  int grid = 0);
+                  int grid_req = 0, const void* extra = nullptr, size_t extra_bytes = 0, int32_t* init = nullptr,
+                  int init_words = 0, int32_t init_value = 0);
 void fill_launch(FillCtx& C);
 void fill_async(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
-                int grid = 0);
+                int grid_req = 0, const void* extra = nullptr, size_t extra_bytes = 0, int32_t* init = nullptr,
+                int init_words = 0, int32_t init_value = 0);
 // Waits for the launch of fill_async, accounts its time, checks the error word.
 void fill_finish(FillCtx& C);
 // The same without waiting: for a caller that has already synchronised the stream

@@ -133,10 +133,13 @@ struct BlockInfo {
     int32_t xi, xj;       // affine construct, free end: the exit cell (written by aff_pred_kernel)
 };
 
-// Affine final level (aff_predwalk_kernel): blocks of at most kPredLdsRows rows
-// keep their predecessor bytes and query rows in LDS; taller ones use an HBM slab.
-constexpr int kPredLdsRows = 376;
-constexpr int kPredLdsBytes = (kPredLdsRows + 127) * 128 + kPredLdsRows;   // 64760 <= 64 KiB
+// Affine final level (aff_predwalk_kernel): blocks of at most `lds_rows` rows (the
+// launch's tallest block, at most kPredLdsMaxRows) keep their predecessor bytes and
+// query rows and subject columns in LDS ((rows + 127) x 128 + rows + 128 bytes,
+// <= 160 KiB); taller ones use
+// an HBM slab.
+constexpr int kPredLdsMaxRows = 1140;
+inline int pred_lds_bytes(int rows) { return (rows + 127) * 128 + ((rows + 15) & ~15) + 128; }
 
 // Device-side error codes written to the error word.
 enum : uint32_t { ERR_NONE = 0, ERR_SPIN_TIMEOUT = 1, ERR_BAD_DESC = 0x100 };

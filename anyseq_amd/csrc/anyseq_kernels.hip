@@ -2334,9 +2334,10 @@ __device__ __forceinline__ int2 aff_pred_block(const BlockInfo& bi, QB qrow, con
 // One thread: walk from the block's end (bottom-right in state H or E, or the
 // free exit cell x) back to its start (anchored: the corner through the border's
 // gap runs; free: a clamped cell or the border); sparse i+j+1 output.
+// qrow / scol: the block's query rows and subject columns (LDS or HBM).
 template <typename PB>
-__device__ __forceinline__ void aff_walk_block(const BlockInfo& bi, int2 x, const uint8_t* __restrict__ Q,
-                                               const uint8_t* __restrict__ S, PB pred, uint8_t* alq, uint8_t* als) {
+__device__ __forceinline__ void aff_walk_block(const BlockInfo& bi, int2 x, const uint8_t* qrow,
+                                               const uint8_t* scol, PB pred, uint8_t* alq, uint8_t* als) {
     const bool free_start = bi.smode >= BM_FREE_LOCAL;
     const int64_t base = (int64_t)bi.oi + bi.oj;
     int i = bi.e_end == 2 ? x.x : bi.h - 1, j = bi.e_end == 2 ? x.y : bi.w - 1;
@@ -2347,10 +2348,10 @@ __device__ __forceinline__ void aff_walk_block(const BlockInfo& bi, int2 x, cons
             if (free_start) break;   // the path starts on the border
             if (i < 0) {
                 alq[pos] = '_';
-                als[pos] = S[bi.oj + j];
+                als[pos] = scol[j];
                 --j;
             } else {
-                alq[pos] = Q[bi.oi + i];
+                alq[pos] = qrow[i];
                 als[pos] = '_';
                 --i;
             }
@@ -2361,8 +2362,8 @@ __device__ __forceinline__ void aff_walk_block(const BlockInfo& bi, int2 x, cons
             const int hs = pb & 3;
             if (hs == 3) break;   // clamped: the path starts after this cell
             if (hs == 0) {
-                alq[pos] = Q[bi.oi + i];
-                als[pos] = S[bi.oj + j];
+                alq[pos] = qrow[i];
+                als[pos] = scol[j];
                 --i;
                 --j;
             } else {
@@ -2370,11 +2371,11 @@ __device__ __forceinline__ void aff_walk_block(const BlockInfo& bi, int2 x, cons
             }
         } else if (st == 1) {
             alq[pos] = '_';
-            als[pos] = S[bi.oj + j];
+            als[pos] = scol[j];
             st = (pb & 4) ? 1 : 0;
             --j;
         } else {
-            alq[pos] = Q[bi.oi + i];
+            alq[pos] = qrow[i];
             als[pos] = '_';
             st = (pb & 8) ? 2 : 0;
             --i;
@@ -2386,25 +2387,30 @@ __device__ __forceinline__ void aff_walk_block(const BlockInfo& bi, int2 x, cons
 // Final level, one wave per 128-column block: predecessors (aff_pred_block), then
 // lane 0 walks them (aff_walk_block) in the same launch.  A block of h <=
 // kPredLdsRows rows keeps its query rows and its (h + 127) x 128 predecessor
-// bytes in LDS, so neither the sweep's query reads nor the walk's dependent reads
-// go to HBM; taller blocks (long vertical gaps) use the HBM slab at pred_base.
+// bytes in LDS (lds_rows: the launch's tallest block, capped), so neither the
+// sweep's query reads nor the walk's dependent reads go to HBM; taller blocks (long
+// vertical gaps) use the HBM slab at pred_base.
 __global__ __launch_bounds__(64) void aff_predwalk_kernel(BlockInfo* __restrict__ blocks, int nblocks,
                                                           const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
                                                           uint8_t* __restrict__ pred, int match, int mismatch, int go,
-                                                          int ge, uint8_t* alq, uint8_t* als) {
+                                                          int ge, uint8_t* alq, uint8_t* als, int lds_rows) {
     extern __shared__ __attribute__((aligned(16))) uint8_t pw_lds[];
     const int b = blockIdx.x;
     if (b >= nblocks) return;
     const BlockInfo bi = blocks[b];
     if (bi.e_end == 2 && bi.h <= 0) return;   // the path ended at the block's corner
     int2 x = make_int2(0, 0);
-    if (bi.h > 0 && bi.h <= kPredLdsRows) {
-        uint8_t* qs = pw_lds + (kPredLdsRows + 127) * 128;
+    if (bi.h > 0 && bi.h <= lds_rows) {
+        uint8_t* qs = pw_lds + (lds_rows + 127) * 128;   // h query rows, then the 128 subject columns
+        uint8_t* ss = qs + ((bi.h + 15) & ~15);
         for (int i = threadIdx.x; i < bi.h; i += 64) qs[i] = Q[bi.oi + i];
+        for (int j = threadIdx.x; j < bi.w; j += 64) ss[j] = S[bi.oj + j];
         __syncthreads();
         x = aff_pred_block(bi, (const uint8_t*)qs, S, pw_lds, match, mismatch, go, ge);
         __syncthreads();
-        if (threadIdx.x == 0) aff_walk_block(bi, x, Q, S, (const uint8_t*)pw_lds, alq, als);
+        // (the walk's reads of predecessors and symbols are all LDS: its steps are
+        // dependent, and an HBM read per step would cost ~1 us each)
+        if (threadIdx.x == 0) aff_walk_block(bi, x, (const uint8_t*)qs, (const uint8_t*)ss, (const uint8_t*)pw_lds, alq, als);
     } else {
         uint8_t* slab = pred + bi.pred_base;
         if (bi.h > 0) {
@@ -2412,7 +2418,7 @@ __global__ __launch_bounds__(64) void aff_predwalk_kernel(BlockInfo* __restrict_
             __threadfence_block();
             __syncthreads();
         }
-        if (threadIdx.x == 0) aff_walk_block(bi, x, Q, S, (const uint8_t*)slab, alq, als);
+        if (threadIdx.x == 0) aff_walk_block(bi, x, Q + bi.oi, S + bi.oj, (const uint8_t*)slab, alq, als);
     }
     if (threadIdx.x == 0 && bi.e_end == 2) {
         blocks[b].xi = x.x;
@@ -2485,6 +2491,31 @@ hipError_t anyseq_launch_fill(int R, int CH, int NW, const anyseq::DPProblem* pr
     using namespace anyseq;
     if (CH == 16) return launch_fill_c<16>(R, NW, probs, groups, ngroups, dq, err, *fp, grid, st);
     return launch_fill_c<32>(R, NW, probs, groups, ngroups, dq, err, *fp, grid, st);
+}
+
+// One launch instead of three memsets ahead of a fill (each host API call costs
+// several microseconds on the level's critical path): zero the launch block's
+// counters and flags, set the caller's best cells to "minus infinity", and fill the
+// hand-off rows with the sentinel.
+namespace anyseq {
+__global__ __launch_bounds__(256) void fill_prep_kernel(uint32_t* zero, int nzero, int32_t* init, int ninit,
+                                                        int32_t init_value, uint4* sent, size_t nsent, uint32_t sv) {
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = tid; i < (size_t)nzero; i += nth) zero[i] = 0u;
+    for (size_t i = tid; i < (size_t)ninit; i += nth) init[i] = init_value;
+    const uint4 v = make_uint4(sv, sv, sv, sv);
+    for (size_t i = tid; i < nsent; i += nth) sent[i] = v;
+}
+}  // namespace anyseq
+
+hipError_t anyseq_launch_fill_prep(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
+                                   void* sent, size_t sent_bytes, uint32_t sent_value, hipStream_t st) {
+    const size_t n16 = sent_bytes / 16;   // (hand-off rows: whole 16-byte units)
+    const size_t work = std::max<size_t>(std::max<size_t>((size_t)nzero, (size_t)ninit), n16);
+    const int blocks = (int)std::max<size_t>(1, std::min<size_t>(2048, (work + 255) / 256));
+    hipLaunchKernelGGL(anyseq::fill_prep_kernel, dim3(blocks), dim3(256), 0, st, zero, nzero, init, ninit, init_value,
+                       (uint4*)sent, n16, sent_value);
+    return hipGetLastError();
 }
 
 // Affine fill launcher: NW compute waves per workgroup in {3, 4} (+1 I/O wave).
@@ -2560,11 +2591,20 @@ hipError_t anyseq_launch_aff_row_to_col(const void* jobs, int njobs, int maxn, i
 }
 
 hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
-                                      int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als,
+                                      int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows,
                                       hipStream_t st) {
-    if (nblocks > 0)
-        hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(nblocks), dim3(64), anyseq::kPredLdsBytes, st,
-                           (anyseq::BlockInfo*)blocks, nblocks, Q, S, pred, match, mismatch, go, ge, alq, als);
+    if (nblocks <= 0) return hipSuccess;
+    const int bytes = anyseq::pred_lds_bytes(lds_rows);
+    static int attr_set = 0;   // the kernel's dynamic-LDS limit, raised once to 160 KiB
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void*)anyseq::aff_predwalk_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 anyseq::pred_lds_bytes(anyseq::kPredLdsMaxRows));
+        if (e != hipSuccess) return e;
+        attr_set = 1;
+    }
+    hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(nblocks), dim3(64), bytes, st, (anyseq::BlockInfo*)blocks,
+                       nblocks, Q, S, pred, match, mismatch, go, ge, alq, als, lds_rows);
     return hipGetLastError();
 }
 
