@@ -50,7 +50,8 @@ hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, co
                                      int32_t* splits, int32_t* types, int32_t* score, hipStream_t st);
 hipError_t anyseq_launch_aff_row_to_col(const void* jobs, int njobs, int maxn, int nge, hipStream_t st);
 hipError_t anyseq_launch_fill_prep(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
-                                   void* sent, size_t sent_bytes, uint32_t sent_value, hipStream_t st);
+                                   void* sent, size_t sent_bytes, uint32_t sent_value, const void* up_src, void* up_dst,
+                                   size_t up_bytes, hipStream_t st);
 hipError_t anyseq_launch_aff_hb_join2(const void* parts, int nparts, int maxlen, int half, const int32_t* LH,
                                       const int32_t* LE, const int32_t* RH, const int32_t* RE, const int32_t* pbest,
                                       int go, int ge, void* partial, int32_t* splits, int32_t* types, int32_t* score,
@@ -293,13 +294,13 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     C.h_probs = probs;
     // staged in pinned memory (a truly asynchronous copy); the previous launch of this
     // context has completed (fill_finish / fill_collect), so the staging area is free
-    char* pin = (char*)C.pin.get(64 + ub);
+    char* pin = (char*)C.pin.get(64 + ub + 16);
     C.err_host = (uint32_t*)pin;
     memcpy(pin + 64, C.h_probs.data(), pb);
     memcpy(pin + 64 + pb, groups.data(), gb);
     if (extra_bytes) memcpy(pin + 64 + eoff, extra, extra_bytes);
-    if (ub) HIPCHECK(hipMemcpyAsync(meta + zb, pin + 64, ub, hipMemcpyHostToDevice, st));
     if (groups.empty()) {
+        if (ub) HIPCHECK(hipMemcpyAsync(meta + zb, pin + 64, ub, hipMemcpyHostToDevice, st));
         if (init_words) HIPCHECK(hipMemsetD32Async(init, init_value, (size_t)init_words, st));
         if (C.err_host) *C.err_host = 0u;   // (no copy targets it: the previous launch has completed)
         HIPCHECK(hipEventRecord(C.ev0, st));
@@ -310,8 +311,9 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     // counters and flags to 0, the caller's best cells to init_value, and the group ->
     // group hand-off rows to the sentinel the consumer polls the data against (-1 for
     // linear, 0x80808080 for affine): one launch
+    // (the kernel also copies the descriptors in from the pinned staging area)
     HIPCHECK(anyseq_launch_fill_prep(ctr, (int)(32 + flag_words), init, init_words, init_value, rowbuf,
-                                     rowbuf_ints * 4, aff ? 0x80808080u : 0xffffffffu, st));
+                                     rowbuf_ints * 4, aff ? 0x80808080u : 0xffffffffu, pin + 64, meta + zb, ub, st));
     FillParams fpl = fp;
     fpl.epoch = epoch;
     fpl.prio = g_tuning.prio;

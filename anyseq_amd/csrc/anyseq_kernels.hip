@@ -2499,8 +2499,12 @@ hipError_t anyseq_launch_fill(int R, int CH, int NW, const anyseq::DPProblem* pr
 // hand-off rows with the sentinel.
 namespace anyseq {
 __global__ __launch_bounds__(256) void fill_prep_kernel(uint32_t* zero, int nzero, int32_t* init, int ninit,
-                                                        int32_t init_value, uint4* sent, size_t nsent, uint32_t sv) {
+                                                        int32_t init_value, uint4* sent, size_t nsent, uint32_t sv,
+                                                        const uint4* up_src, uint4* up_dst, int nup) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    // the launch's descriptors, read straight from the host's pinned staging area (no
+    // separate copy operation in front of this kernel)
+    for (size_t i = tid; i < (size_t)nup; i += nth) up_dst[i] = up_src[i];
     for (size_t i = tid; i < (size_t)nzero; i += nth) zero[i] = 0u;
     for (size_t i = tid; i < (size_t)ninit; i += nth) init[i] = init_value;
     const uint4 v = make_uint4(sv, sv, sv, sv);
@@ -2509,12 +2513,14 @@ __global__ __launch_bounds__(256) void fill_prep_kernel(uint32_t* zero, int nzer
 }  // namespace anyseq
 
 hipError_t anyseq_launch_fill_prep(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
-                                   void* sent, size_t sent_bytes, uint32_t sent_value, hipStream_t st) {
+                                   void* sent, size_t sent_bytes, uint32_t sent_value, const void* up_src, void* up_dst,
+                                   size_t up_bytes, hipStream_t st) {
     const size_t n16 = sent_bytes / 16;   // (hand-off rows: whole 16-byte units)
-    const size_t work = std::max<size_t>(std::max<size_t>((size_t)nzero, (size_t)ninit), n16);
+    const int nup = (int)((up_bytes + 15) / 16);
+    const size_t work = std::max<size_t>(std::max<size_t>((size_t)nzero, (size_t)ninit), std::max<size_t>(n16, nup));
     const int blocks = (int)std::max<size_t>(1, std::min<size_t>(2048, (work + 255) / 256));
     hipLaunchKernelGGL(anyseq::fill_prep_kernel, dim3(blocks), dim3(256), 0, st, zero, nzero, init, ninit, init_value,
-                       (uint4*)sent, n16, sent_value);
+                       (uint4*)sent, n16, sent_value, (const uint4*)up_src, (uint4*)up_dst, nup);
     return hipGetLastError();
 }
 
