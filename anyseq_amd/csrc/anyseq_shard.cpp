@@ -59,13 +59,16 @@ namespace {
 
 constexpr int kComms = 4;   // top even/odd links, bottom even/odd links
 
-// Transport trigger: by default every chunk transfer is enqueued up front on the
-// direction's transport stream behind hipStreamWaitValue32 on the sender's progress
-// counter (signal memory): no host thread sits in the data path.  With
-// ANYSEQ_SHARD_WAITVALUE=0 a host thread per direction polls the counter in pinned
-// host memory instead and issues each chunk's transfer.  ANYSEQ_SHARD_DIRECT=1
-// (local shards only): the receiver polls the sender's out_col itself.
-bool use_wait_value() { return env_int("ANYSEQ_SHARD_WAITVALUE", 1) != 0; }
+// Transport trigger: a host thread per direction polls the sender's progress
+// counter in pinned host memory and issues each chunk's transfer.  With
+// ANYSEQ_SHARD_WAITVALUE=1 every chunk transfer is instead enqueued up front on the
+// direction's transport stream behind hipStreamWaitValue32 on the counter (signal
+// memory).  ANYSEQ_SHARD_DIRECT=1 (local shards only): the receiver polls the
+// sender's out_col itself.  Host-polled transport is the default (round 2, measured on MI355X with 2 and 4
+// in-process shards at 16384^2 semiglobal affine: host polling 0 failures in 80
+// runs at ~4 ms each; hipStreamWaitValue32 1 spin timeout in 80 runs and ~100 ms
+// each).  ANYSEQ_SHARD_WAITVALUE=1 selects the stream-wait transport.
+bool use_wait_value() { return env_int("ANYSEQ_SHARD_WAITVALUE", 0) != 0; }
 bool use_direct() { return env_int("ANYSEQ_SHARD_DIRECT", 0) != 0; }
 
 
@@ -494,7 +497,7 @@ void check_shard_shape(int kind, const anyseq_scoring& sc, int n, int m, int N) 
 
 int grid_per_shard(const Engine& E, int nshards) {
     // leave CUs for the transport (RCCL kernels / copy blits) next to the persistent fills
-    return std::max(8, (E.num_cus - 16) / nshards);
+    return std::max(8, (E.num_cus - env_int("ANYSEQ_SHARD_RESERVE", 16)) / nshards);
 }
 
 int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m, int N) {

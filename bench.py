@@ -172,6 +172,12 @@ def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: s
         "bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
         "traffic": traffic, "traffic_source": traffic_src,
+        # what the measured bytes mean against the same peak (the model above is the
+        # north star's notional scale; the kernel moves ~1 % of it)
+        "traffic_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic and kernel_ms > 0 else None,
+        "traffic_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic and kernel_ms > 0
+        else None,
+        "binding": "band-chain latency: per-step VALU issue x (steps + bands x per-hop lag), DESIGN.md 3.5",
         "kernel": kernel, "kernel_ms": round(kernel_ms, 4), "cells_per_launch": int(cells_per_launch),
         "bytes_model": f"{BYTES_PER_CELL} B/cell x DP cells per launch (SURVEY.md 8(d)); the kernel keeps cells "
                        "in VGPRs and stores only hand-off rows, so the measured traffic is far below the model "
