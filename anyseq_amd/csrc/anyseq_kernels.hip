@@ -2512,6 +2512,29 @@ __global__ __launch_bounds__(256) void fill_prep_kernel(uint32_t* zero, int nzer
 }
 }  // namespace anyseq
 
+// In-process sharded transport: one kernel per chunk copies the chunk's H rows (and
+// affine E rows) into the neighbour's left column, then sets the chunk's ready
+// flag with a release store after the data (one launch instead of two copies and
+// a memset through the runtime's copy paths).
+namespace anyseq {
+__global__ __launch_bounds__(256) void shard_chunk_copy_kernel(int32_t* __restrict__ dst, const int32_t* __restrict__ src,
+                                                               int n, int32_t* __restrict__ dst_e,
+                                                               const int32_t* __restrict__ src_e, int ne,
+                                                               uint32_t* flag) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    if (dst_e)
+        for (int i = threadIdx.x; i < ne; i += blockDim.x) dst_e[i] = src_e[i];
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace anyseq
+
+hipError_t anyseq_launch_shard_chunk_copy(int32_t* dst, const int32_t* src, int n, int32_t* dst_e,
+                                          const int32_t* src_e, int ne, uint32_t* flag, hipStream_t st) {
+    hipLaunchKernelGGL(anyseq::shard_chunk_copy_kernel, dim3(1), dim3(256), 0, st, dst, src, n, dst_e, src_e, ne, flag);
+    return hipGetLastError();
+}
+
 hipError_t anyseq_launch_fill_prep(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
                                    void* sent, size_t sent_bytes, uint32_t sent_value, const void* up_src, void* up_dst,
                                    size_t up_bytes, hipStream_t st) {

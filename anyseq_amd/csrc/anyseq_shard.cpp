@@ -37,6 +37,8 @@
 
 #include "anyseq_host.h"
 
+extern "C" hipError_t anyseq_launch_shard_chunk_copy(int32_t* dst, const int32_t* src, int n, int32_t* dst_e,
+                                                     const int32_t* src_e, int ne, uint32_t* flag, hipStream_t st);
 extern "C" hipError_t anyseq_launch_shard_aff_combine(int kind, const void* rowT, int h1, const void* rowB, int h2,
                                                       int w, int go, int ge, const int32_t* lT, const int32_t* lTf,
                                                       int sT, const int32_t* lB, const int32_t* lBf, int sB, int last,
@@ -331,11 +333,8 @@ void run_xfer(Xfer* x) {
                 NCCLCHECK(ncclSend(src, (size_t)(r1 - r0), ncclInt32, x->peer, x->comm, x->src->s_send));
                 if (src_e) NCCLCHECK(ncclSend(src_e, ne, ncclInt32, x->peer, x->comm, x->src->s_send));
             } else {
-                HIPCHECK(hipMemcpyAsync(x->dst + r0, src, (size_t)(r1 - r0) * 4, hipMemcpyDeviceToDevice,
-                                        x->src->s_send));
-                if (src_e)
-                    HIPCHECK(hipMemcpyAsync(x->dst_e + r0, src_e, ne * 4, hipMemcpyDeviceToDevice, x->src->s_send));
-                HIPCHECK(hipMemsetD32Async(x->flag + r0 / CR, 1u, 1, x->src->s_send));
+                HIPCHECK(anyseq_launch_shard_chunk_copy(x->dst + r0, src, r1 - r0, src_e ? x->dst_e + r0 : nullptr,
+                                                        src_e, (int)ne, x->flag + r0 / CR, x->src->s_send));
             }
         }
     } catch (const Failure& f) {
@@ -496,8 +495,21 @@ void check_shard_shape(int kind, const anyseq_scoring& sc, int n, int m, int N) 
 }
 
 int grid_per_shard(const Engine& E, int nshards) {
-    // leave CUs for the transport (RCCL kernels / copy blits) next to the persistent fills
-    return std::max(8, (E.num_cus - env_int("ANYSEQ_SHARD_RESERVE", 16)) / nshards);
+    // One shard per GPU (the RCCL path): leave CUs for the transport (RCCL kernels)
+    // next to the persistent fill.
+    if (nshards <= 1) return std::max(8, E.num_cus - env_int("ANYSEQ_SHARD_RESERVE", 16));
+    // Several persistent fills on one GPU that wait for each other (the in-process
+    // transport): each fill workgroup needs a CU of its own (LDS), a launch spreads its
+    // workgroups round-robin over the 8 XCDs, and a launch that cannot place all of its
+    // workgroups holds back the dispatch of the launches behind it.  With (CUs-16)/N
+    // workgroups per fill (60 at N = 4) the XCDs that get 8 of every launch's were full
+    // (32 of 32 CUs) and about 1 % of 4-shard runs deadlocked until the 10 s spin limit
+    // (DESIGN.md §8); at most (CUs/8 - 8)/N per XCD per fill leaves 8 CUs per XCD free:
+    // 0 failures in 3200 runs.
+    const int xcds = 8, per_xcd = E.num_cus / xcds;
+    const int reserve = env_int("ANYSEQ_SHARD_RESERVE", 0);
+    if (reserve > 0) return std::max(8, (E.num_cus - reserve) / nshards);
+    return std::max(8, xcds * std::max(1, (per_xcd - 8) / nshards));
 }
 
 int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m, int N) {
@@ -606,16 +618,25 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
                 int32_t lv[4] = {0, 0, 0, 0}, oc[4] = {0, 0, 0, 0};
                 if (f->left_in.p) (void)hipMemcpy(lv, f->left_in.p, 4 * std::min(4, f->h), hipMemcpyDeviceToHost);
                 (void)hipMemcpy(oc, f->out_col.p, 4 * std::min(4, f->h), hipMemcpyDeviceToHost);
-                fprintf(stderr, "shard %d %s: progress %u left_in %d %d %d %d out_col %d %d %d %d\n", g,
+                fprintf(stderr, "shard %d %s: progress %u left_in %d %d %d %d out_col %d %d %d %d flags", g,
                         f == &shards[g].top ? "top" : "bot", pv, lv[0], lv[1], lv[2], lv[3], oc[0], oc[1], oc[2],
                         oc[3]);
+                if (f->left_flag.p) {
+                    const int nfl = (f->h + chunk_rows() - 1) / chunk_rows();
+                    std::vector<uint32_t> fl((size_t)nfl);
+                    (void)hipMemcpy(fl.data(), f->left_flag.p, (size_t)nfl * 4, hipMemcpyDeviceToHost);
+                    for (uint32_t x : fl) fprintf(stderr, " %u", x);
+                }
+                fprintf(stderr, "\n");
             }
     }
     finish_xfers(th, xs, sp, ok);
-    if (!ok) fail("%s", err.c_str());
+    // every transfer drains before returning, also after a failure: a copy still in
+    // flight would land in the next call's freshly reset left columns and flags
     for (int g = 0; g < N; ++g)
         for (Front* f : {&shards[g].top, &shards[g].bot})
             if (f->s_send) wait_stream(f->s_send, 30.0, "shard transport");
+    if (!ok) fail("%s", err.c_str());
     for (int g = 0; g < N; ++g) enqueue_combine(shards[g], N, kind, sc, m, h1, h2, res);
     int32_t v = 0;
     for (int g = 0; g < N; ++g) HIPCHECK(hipStreamSynchronize(shards[g].st));

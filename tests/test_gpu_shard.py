@@ -63,3 +63,16 @@ def test_shard_rejects_bad_shapes(anyseq):
         anyseq.shard_score_local("global", "A", "ACGT", 2)        # one query row: no two fronts
     with pytest.raises(anyseq.AnySeqError):
         anyseq.shard_score_local("global", "ACGT", "AC", 3)       # fewer columns than shards
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_shard_local_dispatch_no_deadlock(anyseq, kind):
+    """Regression (round 2): 4 concurrent in-process persistent fills of (CUs-16)/4
+    workgroups filled some XCDs to 32 of 32 CUs; a fill that could not place all of its
+    workgroups held back the next shard's launch and about 1 % of 4-shard runs hung until
+    the 10 s spin limit.  The shard grid is XCD-aware now; 60 repetitions
+    per kind (the flake would show in ~45 % of suite runs)."""
+    q, s = anyseq.main_random_pair(16384, 16384)
+    ref = anyseq.score(kind, q, s, gap_open=-2, gap_extend=-1)
+    for _ in range(60):
+        assert anyseq.shard_score_local(kind, q, s, 4, gap_open=-2, gap_extend=-1) == ref
