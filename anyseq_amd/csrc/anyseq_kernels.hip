@@ -2201,113 +2201,109 @@ __global__ void aff_row_to_col_kernel(const RowToCol* __restrict__ jobs, int nge
 // the block holds it) if strictly greater -> blocks[b].xi / xj.
 // PB: the predecessor slab (LDS or HBM), QB: the block's query rows (LDS:
 // staged, HBM: Q + oi).  Returns the exit cell (xi, xj) of a free end in every lane.
-template <typename PB, typename QB>
-__device__ __forceinline__ int2 aff_pred_block(const BlockInfo& bi, QB qrow, const uint8_t* __restrict__ S, PB pred,
+// XFREE / XLOCAL: the block holds a free end (e_end 2), local (first maximum of
+// all cells) or semiglobal (last row, then the last column).  The sweep is
+// branch-free (selects), and a lane's query byte for the next step is read one
+// step ahead (B's row is A's row of the previous step).
+template <bool XFREE, bool XLOCAL, typename PB, typename QB>
+__device__ __forceinline__ int2 aff_pred_sweep(const BlockInfo& bi, QB qrow, const uint8_t* __restrict__ S, PB pred,
                                                int match, int mismatch, int go, int ge) {
     const int lane = threadIdx.x;
     const int NEG = kAffNeg;
     const int bm = bi.smode;
     const bool clamp = bm == BM_FREE_LOCAL;
     const int C = (bm == BM_EFREE || bm == BM_EPAID) ? NEG : 0;
+    const bool lnormal = bm == BM_NORMAL, lzero = bm == BM_FREE_LOCAL || bm == BM_FREE_SEMI_OPEN;
     auto top = [&](int j) { return j < 0 ? C : aff_top_h(bm, j, go, ge); };
-    auto left = [&](int i) {
-        if (i < 0) return C;
-        if (bm == BM_NORMAL) return go + (i + 1) * ge;
-        return (bm == BM_FREE_LOCAL || bm == BM_FREE_SEMI_OPEN) ? 0 : NEG;
-    };
-    const bool xfree = bi.e_end == 2, xlocal = bi.flags & 1, xlastcol = bi.flags & 2;
+    const bool xlastcol = bi.flags & 2;
+    const int h = bi.h, w = bi.w;
     const int jA = 2 * lane, jB = 2 * lane + 1;
-    const int sA = jA < bi.w ? (int)S[bi.oj + jA] : 0x100;
-    const int sB = jB < bi.w ? (int)S[bi.oj + jB] : 0x100;
+    const bool colA = jA < w, colB = jB < w;
+    const int sA = colA ? (int)S[bi.oj + jA] : 0x100;
+    const int sB = colB ? (int)S[bi.oj + jB] : 0x100;
     int HA = top(jA), FA = NEG, EA = NEG;   // A's current row state (row -1: the top border)
     int HB = top(jB), FB = NEG, EB = NEG;
     int HAo = top(jA);                       // A one step earlier: B's diagonal
-    int dA = left(-1);                       // A's diagonal (lane 0: the left border)
-    // exit candidates: per column the first row reaching its best (local), the last
-    // row's value (semiglobal), the last column's first maximum (semiglobal)
+    int dA = C;                              // A's diagonal (lane 0: the left border, row -1)
     int xvA = -2147483647, xrA = 0, xvB = -2147483647, xrB = 0, cv = -2147483647, cr = 0;
-    const int nsteps = bi.h + 127;
+    const int nsteps = h + 127;
+    int qA_next = (-jA >= 0 && -jA < h) ? (int)qrow[-jA] : 0x200;
+    int qA_prev = 0x200;
     for (int d = 0; d < nsteps; ++d) {
-        const int iA = d - jA, iB = d - jB;
+        const int iA = d - jA, iB = iA - 1;
+        const int qA = qA_next, qB = qA_prev;   // rows iA and iB (= iA of the previous step)
+        qA_prev = qA;
+        qA_next = (iA + 1 >= 0 && iA + 1 < h) ? (int)qrow[iA + 1] : 0x200;
         // A's left neighbour = lane l-1's B at row iA (lane 0: the left border)
-        const int lH = wave_shr1(left(iA), HB);
+        const int lb = iA < 0 ? C : (lnormal ? go + (iA + 1) * ge : (lzero ? 0 : NEG));
+        const int lH = wave_shr1(lb, HB);
         const int lE = wave_shr1(NEG, EB);
-        const bool actA = iA >= 0 && iA < bi.h && jA < bi.w;
-        const bool actB = iB >= 0 && iB < bi.h && jB < bi.w;
-        const int qA = (iA >= 0 && iA < bi.h) ? (int)qrow[iA] : 0x200;
-        const int qB = (iB >= 0 && iB < bi.h) ? (int)qrow[iB] : 0x200;
+        const bool actA = colA && iA >= 0 && iA < h;
+        const bool actB = colB && iB >= 0 && iB < h;
         // B (uses A's state before A's update: A at row iB)
-        int pB = 0;
-        int eB;
-        {
-            const int e1 = EA + ge, e2 = HA + go + ge;
-            if (e1 > e2) { eB = e1; pB |= 4; } else eB = e2;
-        }
-        int fB;
-        {
-            const int f1 = FB + ge, f2 = HB + go + ge;
-            if (f1 > f2) { fB = f1; pB |= 8; } else fB = f2;
-        }
-        int hB = HAo + (qB == sB ? match : mismatch);
-        if (eB > hB) { hB = eB; pB = (pB & ~3) | 1; }
-        if (fB > hB) { hB = fB; pB = (pB & ~3) | 2; }
-        if (clamp && 0 > hB) { hB = 0; pB |= 3; }
+        const int e1B = EA + ge, e2B = HA + go + ge;
+        const int eB = e1B > e2B ? e1B : e2B;
+        const int f1B = FB + ge, f2B = HB + go + ge;
+        const int fB = f1B > f2B ? f1B : f2B;
+        int hB = HAo + (qB == sB ? match : mismatch), sB3 = 0;
+        if (eB > hB) { hB = eB; sB3 = 1; }
+        if (fB > hB) { hB = fB; sB3 = 2; }
+        if (clamp && 0 > hB) { hB = 0; sB3 = 3; }
+        const int pB = sB3 | (e1B > e2B ? 4 : 0) | (f1B > f2B ? 8 : 0);
         // A
-        int pA = 0;
-        int eA;
-        {
-            const int e1 = lE + ge, e2 = lH + go + ge;
-            if (e1 > e2) { eA = e1; pA |= 4; } else eA = e2;
-        }
-        int fA;
-        {
-            const int f1 = FA + ge, f2 = HA + go + ge;
-            if (f1 > f2) { fA = f1; pA |= 8; } else fA = f2;
-        }
-        int hA = dA + (qA == sA ? match : mismatch);
-        if (eA > hA) { hA = eA; pA = (pA & ~3) | 1; }
-        if (fA > hA) { hA = fA; pA = (pA & ~3) | 2; }
-        if (clamp && 0 > hA) { hA = 0; pA |= 3; }
+        const int e1A = lE + ge, e2A = lH + go + ge;
+        const int eA = e1A > e2A ? e1A : e2A;
+        const int f1A = FA + ge, f2A = HA + go + ge;
+        const int fA = f1A > f2A ? f1A : f2A;
+        int hA = dA + (qA == sA ? match : mismatch), sA3 = 0;
+        if (eA > hA) { hA = eA; sA3 = 1; }
+        if (fA > hA) { hA = fA; sA3 = 2; }
+        if (clamp && 0 > hA) { hA = 0; sA3 = 3; }
+        const int pA = sA3 | (e1A > e2A ? 4 : 0) | (f1A > f2A ? 8 : 0);
         dA = lH;   // next step's diagonal of A: lane l-1's B at row iA
-        if (actB) {
-            HB = hB;
-            FB = fB;
-            EB = eB;
-            if (xfree) {
-                if (xlocal) {
-                    if (hB > xvB) { xvB = hB; xrB = iB; }
-                } else {
-                    if (iB == bi.h - 1) xvB = hB;
-                    if (xlastcol && jB == bi.w - 1 && hB > cv) { cv = hB; cr = iB; }
-                }
+        HB = actB ? hB : HB;
+        FB = actB ? fB : FB;
+        EB = actB ? eB : EB;
+        if constexpr (XFREE) {
+            if constexpr (XLOCAL) {
+                const bool u = actB && hB > xvB;
+                xvB = u ? hB : xvB;
+                xrB = u ? iB : xrB;
+            } else {
+                xvB = (actB && iB == h - 1) ? hB : xvB;
+                const bool u = xlastcol && actB && jB == w - 1 && hB > cv;
+                cv = u ? hB : cv;
+                cr = u ? iB : cr;
             }
         }
         HAo = HA;
-        if (actA) {
-            HA = hA;
-            FA = fA;
-            EA = eA;
-            if (xfree) {
-                if (xlocal) {
-                    if (hA > xvA) { xvA = hA; xrA = iA; }
-                } else {
-                    if (iA == bi.h - 1) xvA = hA;
-                    if (xlastcol && jA == bi.w - 1 && hA > cv) { cv = hA; cr = iA; }
-                }
+        HA = actA ? hA : HA;
+        FA = actA ? fA : FA;
+        EA = actA ? eA : EA;
+        if constexpr (XFREE) {
+            if constexpr (XLOCAL) {
+                const bool u = actA && hA > xvA;
+                xvA = u ? hA : xvA;
+                xrA = u ? iA : xrA;
+            } else {
+                xvA = (actA && iA == h - 1) ? hA : xvA;
+                const bool u = xlastcol && actA && jA == w - 1 && hA > cv;
+                cv = u ? hA : cv;
+                cr = u ? iA : cr;
             }
         }
         const uint16_t pk = (uint16_t)((actA ? pA : 0) | ((actB ? pB : 0) << 8));
         reinterpret_cast<uint16_t*>(pred)[d * 64 + lane] = pk;
     }
-    if (xfree) {
+    if constexpr (XFREE) {
         // best (value, row, column) of the lane: A before B (same row: smaller column)
-        int v = xvA, r = xlocal ? xrA : bi.h - 1, c = jA;
-        if (xvB > v || (xvB == v && xlocal && xrB < r)) {
+        int v = xvA, r = XLOCAL ? xrA : h - 1, c = jA;
+        if (xvB > v || (xvB == v && XLOCAL && xrB < r)) {
             v = xvB;
-            r = xlocal ? xrB : bi.h - 1;
+            r = XLOCAL ? xrB : h - 1;
             c = jB;
         }
-        if (jA >= bi.w) v = -2147483647;
+        if (!colA) v = -2147483647;
         // first maximum over lanes: larger value, then smaller row, then smaller column
         for (int o = 32; o >= 1; o >>= 1) {
             const int v2 = __shfl_xor(v, o), r2 = __shfl_xor(r, o), c2 = __shfl_xor(c, o);
@@ -2317,18 +2313,26 @@ __device__ __forceinline__ int2 aff_pred_block(const BlockInfo& bi, QB qrow, con
                 c = c2;
             }
         }
-        if (!xlocal && xlastcol) {   // the last column's first maximum, if strictly greater
-            const int owner = (bi.w - 1) >> 1;
+        if (!XLOCAL && xlastcol) {   // the last column's first maximum, if strictly greater
+            const int owner = (w - 1) >> 1;
             const int cv0 = __shfl(cv, owner), cr0 = __shfl(cr, owner);
             if (cv0 > v) {
                 v = cv0;
                 r = cr0;
-                c = bi.w - 1;
+                c = w - 1;
             }
         }
         return make_int2(r, c);
     }
     return make_int2(0, 0);
+}
+
+template <typename PB, typename QB>
+__device__ __forceinline__ int2 aff_pred_block(const BlockInfo& bi, QB qrow, const uint8_t* __restrict__ S, PB pred,
+                                               int match, int mismatch, int go, int ge) {
+    if (bi.e_end != 2) return aff_pred_sweep<false, false>(bi, qrow, S, pred, match, mismatch, go, ge);
+    if (bi.flags & 1) return aff_pred_sweep<true, true>(bi, qrow, S, pred, match, mismatch, go, ge);
+    return aff_pred_sweep<true, false>(bi, qrow, S, pred, match, mismatch, go, ge);
 }
 
 // One thread: walk from the block's end (bottom-right in state H or E, or the
