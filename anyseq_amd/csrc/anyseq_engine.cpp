@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -920,6 +921,11 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         StageScope() { g_stage = "affine construct", g_stage_level = 0; }
         ~StageScope() { g_stage = "fill", g_stage_level = -1; }
     } stage_scope;
+    static const int level_timing = env_int("ANYSEQ_LEVEL_TIMING", 0);   // diagnostics: host phases per level
+    auto now_us = [] {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    double t_wake = now_us();
     while (pw > MIN_PART_WIDTH_HB) {
         const int half = pw / 2;
         const int parts = (m + half - 1) / pw;
@@ -985,6 +991,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         for (const auto& probs : probs_of) nl += probs.empty() ? 0 : 1;
         bool pending_fill = false;
         const char* d_up = nullptr;
+        const double t_built = now_us();
         for (size_t li = 0; li < probs_of.size(); ++li) {
             auto& probs = probs_of[li];
             if (probs.empty()) continue;
@@ -1006,6 +1013,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             d_up = d;
         }
         stage_check(st, "affine fill");
+        const double t_launched = now_us();
         if (!jobs.empty()) {
             int maxn = 0;
             for (const auto& J : jobs) maxn = std::max(maxn, J.n);
@@ -1026,7 +1034,13 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         stage_check(st, "aff_hb_join");
         HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + (level1 ? 1 : 0)) * 4, hipMemcpyDeviceToHost, st));
         {
+            const double t_enq = now_us();
             const hipError_t e = stream_wait_spin(st);
+            const double t_w = now_us();
+            if (level_timing)
+                fprintf(stderr, "level %d: build %.1f us, fill launch %.1f us, join enqueue %.1f us, wait %.1f us\n",
+                        g_stage_level, t_built - t_wake, t_launched - t_built, t_enq - t_launched, t_w - t_enq);
+            t_wake = t_w;
             if (e != hipSuccess && pending_fill)
                 fail("fill failed: %s (%s)", hipGetErrorString(e), fill_summary(E.fc).c_str());
             HIPCHECK(e);
