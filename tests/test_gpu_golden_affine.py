@@ -40,3 +40,22 @@ def test_config3_semiglobal_affine_prefix(anyseq):
     g = json.load(open(path))
     q, s = genome.synthetic_related_pair(4_641_652, 0.9)
     check(anyseq, g, q[:g["lq"]], s[:g["ls"]])
+
+
+def test_config3_genome_length_construct(anyseq):
+    """configs[3] and configs[4] at full genome length (4.64 Mbp x 4.64 Mbp, synthetic related
+    pair; the oracle cannot reach this size, so parity is by properties): the construct's
+    strings re-score to its score, their residues are substrings of the inputs, and the
+    score equals the score-only fill's and the 2-shard column-blocked fill's (configs[4]'s
+    path, in-process transport)."""
+    import numpy as np
+    from anyseq_amd import genome
+    q, s = genome.synthetic_related_pair(4_641_652, 0.9)
+    v, aq, as_ = anyseq.construct("semiglobal", q, s, gap_open=-2, gap_extend=-1)
+    assert genome.affine_rescore(aq, as_) == v
+    for al, seq in ((aq, q), (as_, s)):
+        a = np.frombuffer(al, dtype=np.uint8)
+        res = a[(a != ord(" ")) & (a != ord("_"))].tobytes()
+        assert len(res) > 0.9 * len(seq) and seq.find(res) >= 0
+    assert anyseq.score("semiglobal", q, s, gap_open=-2, gap_extend=-1) == v
+    assert anyseq.shard_score_local("semiglobal", q, s, 2, gap_open=-2, gap_extend=-1) == v
