@@ -85,17 +85,92 @@ void set_last_error(const std::string& m) { g_last_error = m; }
     throw Failure{buf};
 }
 
+// ------------------------------------------------------------- buffers --
+// Live allocations (for the ANYSEQ_CHECK_PTRS audit) and retired ones (freed by
+// release_retired at a point where nothing of ours is in flight).
+namespace {
+struct Alloc {
+    const void* owner;
+    uintptr_t lo, hi;
+};
+std::mutex g_alloc_mu;
+std::vector<Alloc> g_live;                   // owner -> current block
+std::vector<std::pair<void*, bool>> g_retired;   // (block, pinned)
+std::vector<std::pair<uintptr_t, uintptr_t>> g_extern;   // caller buffers of the current call
+
+void note_live(const void* owner, void* p, size_t cap) {
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    for (Alloc& a : g_live)
+        if (a.owner == owner) {
+            a.lo = (uintptr_t)p;
+            a.hi = (uintptr_t)p + cap;
+            return;
+        }
+    g_live.push_back(Alloc{owner, (uintptr_t)p, (uintptr_t)p + cap});
+}
+void retire(const void* owner, void* p, bool pinned) {
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    if (p) g_retired.emplace_back(p, pinned);
+    for (size_t i = 0; i < g_live.size(); ++i)
+        if (g_live[i].owner == owner) {
+            g_live.erase(g_live.begin() + (long)i);
+            break;
+        }
+}
+}  // namespace
+
+void release_retired() {
+    std::vector<std::pair<void*, bool>> r;
+    {
+        std::lock_guard<std::mutex> lk(g_alloc_mu);
+        if (g_retired.empty()) return;
+        r.swap(g_retired);
+    }
+    // (an API entry: none of this library's work is in flight; the device-wide wait
+    // also covers a caller's stream that may still read a retired block)
+    (void)hipDeviceSynchronize();
+    for (auto& b : r) {
+        if (b.second) (void)hipHostFree(b.first);
+        else (void)hipFree(b.first);
+    }
+}
+
+bool check_ptrs_enabled() {
+    static const int on = env_int("ANYSEQ_CHECK_PTRS", 0);
+    return on != 0;
+}
+void register_static_range(const void* p, size_t bytes) { note_live(p, const_cast<void*>(p), bytes); }
+void register_extern_range(const void* p, size_t bytes) {
+    if (!p || !check_ptrs_enabled()) return;
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    g_extern.emplace_back((uintptr_t)p, (uintptr_t)p + bytes);
+}
+void clear_extern_ranges() {
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    g_extern.clear();
+}
+void check_range(const void* p, size_t bytes, const char* what) {
+    if (!p) return;
+    const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    for (const Alloc& a : g_live)
+        if (lo >= a.lo && hi <= a.hi) return;
+    for (const auto& e : g_extern)
+        if (lo >= e.first && hi <= e.second) return;
+    fail("pointer audit: %s %p + %zu bytes lies outside every live allocation", what, p, bytes);
+}
+
 void* DevBuf::get(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes > cap) {
-        static const int no_free = env_int("ANYSEQ_NO_FREE", 0);
-        if (p && !no_free) HIPCHECK(hipFree(p));
+        retire(this, p, false);
         p = nullptr;
         size_t c = std::max(bytes, cap * 3 / 2);
         c = (c + 255) & ~size_t(255);
         if (uncached) HIPCHECK(hipExtMallocWithFlags(&p, c, hipDeviceMallocUncached));
         else HIPCHECK(hipMalloc(&p, c));
         cap = c;
+        note_live(this, p, c);
     }
     return p;
 }
@@ -103,12 +178,13 @@ void* DevBuf::get(size_t bytes) {
 void* PinBuf::get(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes > cap) {
-        if (p) HIPCHECK(hipHostFree(p));
+        retire(this, p, true);
         p = nullptr;
         size_t c = std::max(bytes, cap * 3 / 2);
         c = (c + 4095) & ~size_t(4095);
-        HIPCHECK(hipHostMalloc(&p, c, hipHostMallocDefault));
+        HIPCHECK(hipHostMalloc(&p, c, hipHostMallocCoherent));
         cap = c;
+        note_live(this, p, c);
     }
     return p;
 }
@@ -116,6 +192,16 @@ void* PinBuf::get(size_t bytes) {
 int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return (v && *v) ? atoi(v) : dflt;
+}
+
+// H2D upload through a pinned staging buffer (never from pageable memory, which the
+// runtime may read after the call returns).  `pb` must not be rewritten before the
+// stream has passed the copy: every call site reuses it only after a synchronisation.
+void upload_pinned(PinBuf& pb, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (!bytes) return;
+    void* h = pb.get(bytes);
+    memcpy(h, src, bytes);
+    HIPCHECK(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, st));
 }
 
 void FillCtx::init() {
@@ -174,6 +260,7 @@ Engine::Engine(int dev) : device(dev) {
     HIPCHECK(hipGetDeviceProperties(&prop, dev));
     num_cus = prop.multiProcessorCount;
     HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HIPCHECK(hipEventCreateWithFlags(&ev_order, hipEventDisableTiming));
     fc.init();
 }
 
@@ -210,7 +297,19 @@ Engine& engine() {
     if ((int)g_engines.size() < ndev) g_engines.resize(ndev);
     if (!g_engines[g_device]) g_engines[g_device].reset(new Engine(g_device));
     HIPCHECK(hipSetDevice(g_device));
+    release_retired();
     return *g_engines[g_device];
+}
+
+// A caller's stream runs the engine's work for the device API: it first waits for
+// everything already queued on the engine's own stream (explicit order instead of
+// the assumption that the previous call drained it), and the caller's buffers are
+// registered for the pointer audit.
+hipStream_t caller_stream(Engine& E, void* stream) {
+    if (!stream || (hipStream_t)stream == E.stream) return E.stream;
+    HIPCHECK(hipEventRecord(E.ev_order, E.stream));
+    HIPCHECK(hipStreamWaitEvent((hipStream_t)stream, E.ev_order, 0));
+    return (hipStream_t)stream;
 }
 
 int rows_per_lane() { return g_tuning.R == 2 ? 2 : (g_tuning.R >= 4 ? 4 : 1); }
@@ -222,6 +321,30 @@ int waves_per_group() {
 // ---------------------------------------------------------------- fill --
 // Prepares one batched fill launch over `probs` (host copies; device pointers set):
 // every allocation, upload and sentinel fill, enqueued on st.  No kernel yet.
+// ANYSEQ_CHECK_PTRS: every pointer of every descriptor, with the extent the fill
+// kernels address through it, inside a live allocation.
+void audit_probs(const std::vector<DPProblem>& probs, bool aff) {
+    const size_t vb = aff ? 8 : 4;   // bytes per hand-off row element
+    for (const DPProblem& P : probs) {
+        const int64_t qlo = std::min<int64_t>(P.q_off, P.q_off + (int64_t)P.q_step * (P.h - 1));
+        const int64_t slo = std::min<int64_t>(P.s_off, P.s_off + (int64_t)P.s_step * (P.w - 1));
+        if (P.h > 0) check_range(P.q + qlo, (size_t)P.h, "query rows");
+        if (P.w > 0) check_range(P.s + slo, (size_t)P.w, "subject columns");
+        check_range(P.out_col, (size_t)P.h * 4, "out_col");
+        check_range(P.out_col_e, (size_t)P.h * 4, "out_col_e");
+        check_range(P.out_row, (size_t)P.wpad * vb, "out_row");
+        if (P.ngroups > 1) check_range(P.rowbuf, (size_t)P.nslots * P.wpad * vb, "hand-off rows");
+        check_range(P.flags, (size_t)P.ngroups * 4, "group flags");
+        check_range(P.best, 4, "best cell");
+        check_range(P.left_in, (size_t)P.h * 4, "left_in");
+        check_range(P.left_in_e, (size_t)P.h * 4, "left_in_e");
+        check_range(P.out_f_last, 4, "out_f_last");
+        if (P.left_flag && P.left_chunk > 0)
+            check_range(P.left_flag, (size_t)((P.h + P.left_chunk - 1) / P.left_chunk) * 4, "left_flag");
+        check_range(P.progress, 4, "progress");
+    }
+}
+
 void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
                   int grid_req, const void* extra, size_t extra_bytes, int32_t* init, int init_words,
                   int32_t init_value) {
@@ -282,14 +405,22 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     size_t ro = 0, fo = 0;
     static std::atomic<int32_t> g_epoch{0};
     const int32_t epoch = (g_epoch.fetch_add(1) + 1) & 0x7ffff;
-    for (size_t i = 0; i < probs.size(); ++i) probs[i].magic = kProbMagic ^ (int32_t)i ^ (epoch << 12);
-    for (auto& g : groups) g.epoch = epoch;
+    for (auto& g : groups) {
+        g.epoch = epoch;
+        g.check = group_check(g.prob, g.group, epoch);
+    }
     for (auto& P : probs) {
         P.rowbuf = rowbuf + ro;
         P.flags = flags + fo;
         ro += (size_t)(P.ngroups > 1 ? P.nslots : 0) * P.wpad * vpc;
         fo += P.ngroups;
     }
+    // the digest covers every word of the final descriptor (pointers included)
+    for (size_t i = 0; i < probs.size(); ++i) {
+        probs[i].pad_ = 0;
+        probs[i].magic = prob_magic(&probs[i], (int)i, epoch);
+    }
+    if (check_ptrs_enabled()) audit_probs(probs, aff);
     C.R = R;
     C.NW = NW;
     C.h_probs = probs;
@@ -704,7 +835,7 @@ void construct_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t*
     sp.v[0] = 0;
     sp.v[sp.nb] = n;
     int32_t* d_spl = (int32_t*)E.spl.get(sp.v.size() * 4);
-    HIPCHECK(hipMemcpyAsync(d_spl, sp.v.data(), sp.v.size() * 4, hipMemcpyHostToDevice, st));
+    upload_pinned(E.pin_down, d_spl, sp.v.data(), sp.v.size() * 4, st);
     int32_t* dL = (int32_t*)E.L.get((size_t)std::max(n, 1) * 4);
     int32_t* dR = (int32_t*)E.R.get((size_t)std::max(n, 1) * 4);
 
@@ -752,7 +883,7 @@ void construct_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t*
         const int bwh = std::min(CPU_BLOCK_WIDTH, half * 2);
         const int bpp_h = half * 2 / bwh;
         PartInfo* d_parts = (PartInfo*)E.parts.get(pinfo.size() * sizeof(PartInfo));
-        HIPCHECK(hipMemcpyAsync(d_parts, pinfo.data(), pinfo.size() * sizeof(PartInfo), hipMemcpyHostToDevice, st));
+        upload_pinned(E.pin_up, d_parts, pinfo.data(), pinfo.size() * sizeof(PartInfo), st);
         int32_t* d_bmax = (int32_t*)E.bmax.get((size_t)parts * bpp_h * 4);
         int32_t* d_bind = (int32_t*)E.bind.get((size_t)parts * bpp_h * 4);
         HIPCHECK(anyseq_launch_hb_sum(d_parts, parts, bpp_h, half, dL, dR, kind, sc.gap_extend, d_bmax, d_bind, d_spl,
@@ -776,7 +907,7 @@ void construct_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t*
         if (bi.h > 0) pred_bytes += (int64_t)(bi.h + 127) * 128;
     }
     BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
-    HIPCHECK(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, st));
+    upload_pinned(E.pin_blocks, d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), st);
     uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
     HIPCHECK(anyseq_launch_pred(d_blocks, sp.nb, dq, ds, d_pred, &fp, st));
     HIPCHECK(anyseq_launch_walk(d_blocks, sp.nb, dq, ds, d_pred, kind, d_alq, d_als, st));
@@ -1098,7 +1229,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         return score;
     }
     BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
-    HIPCHECK(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), hipMemcpyHostToDevice, st));
+    upload_pinned(E.pin_blocks, d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), st);
     uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
     HIPCHECK(anyseq_launch_aff_predwalk(d_blocks, (int)blocks.size(), dq, ds, d_pred, sc.match, sc.mismatch,
                                         sc.gap_open, sc.gap_extend, d_alq, d_als, lds_rows, st));
@@ -1204,6 +1335,15 @@ int64_t construct_fulltb_host(const anyseq_scoring& sc, const char* q, int n, co
 
 const anyseq_scoring kAbiScoring = {2, -1, 0, -1};  // linear_scoring_scheme(2,-1,-1)
 
+// The caller's device buffers of one device-API call, registered for the pointer
+// audit while the call runs.
+struct ExternRanges {
+    explicit ExternRanges(std::initializer_list<std::pair<const void*, size_t>> r) {
+        for (const auto& x : r) register_extern_range(x.first, x.second);
+    }
+    ~ExternRanges() { clear_extern_ranges(); }
+};
+
 int64_t abi_score(int kind, const char* q, int n, const char* s, int m) {
     try {
         return score_host(kind, kAbiScoring, q, n, s, m);
@@ -1307,7 +1447,8 @@ int anyseq_score_device(int kind, const anyseq_scoring* sc, const uint8_t* d_que
         check_value_range(s, lenq, lens);
         Engine& E = engine();
         std::lock_guard<std::mutex> lk(E.mu);
-        hipStream_t st = stream ? (hipStream_t)stream : E.stream;
+        hipStream_t st = caller_stream(E, stream);
+        ExternRanges xr({{d_query, (size_t)std::max(lenq, 0)}, {d_subject, (size_t)std::max(lens, 0)}});
         const int64_t v = score_dev(E, kind, s, d_query, lenq, d_subject, lens, st);
         if (score) *score = v;
         return 0;
@@ -1347,7 +1488,10 @@ int anyseq_construct_device(int kind, const anyseq_scoring* sc, const uint8_t* d
         if (lenq < 0 || lens < 0) fail("negative sequence length");
         Engine& E = engine();
         std::lock_guard<std::mutex> lk(E.mu);
-        hipStream_t st = stream ? (hipStream_t)stream : E.stream;
+        hipStream_t st = caller_stream(E, stream);
+        const size_t L = (size_t)std::max(lenq, 0) + (size_t)std::max(lens, 0);
+        ExternRanges xr({{d_query, (size_t)std::max(lenq, 0)}, {d_subject, (size_t)std::max(lens, 0)},
+                         {d_alQuery, L}, {d_alSubject, L}});
         int64_t v;
         if (s.gap_open != 0) {
             v = construct_affine_dev(E, kind, s, d_query, lenq, d_subject, lens, d_alQuery, d_alSubject, st);

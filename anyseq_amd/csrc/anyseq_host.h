@@ -36,6 +36,9 @@ struct Failure {
 // Grow-only device buffer.  uncached: MTYPE UC (hipDeviceMallocUncached), for
 // words that a running kernel polls while another kernel or engine writes them:
 // per-XCD L2s are not coherent, an uncached line is never served stale.
+// Growth never frees the old allocation on the spot: work queued on another stream
+// (a shard's transport, a caller's stream) may still reference it.  The old block is
+// retired and released by release_retired() once the device is idle.
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -45,12 +48,29 @@ struct DevBuf {
 
 // Grow-only pinned host buffer: the source / destination of truly asynchronous copies
 // (a pageable hipMemcpyAsync stages through the runtime and may block).  Callers must
-// not rewrite it before the stream has passed the copy.
+// not rewrite it before the stream has passed the copy.  Allocated COHERENT
+// (fine-grained, never cached in a GPU L2): kernels read the staged descriptors
+// straight from it (fill_prep_kernel), and the host rewrites the same bytes for the
+// next launch, so a non-coherent line cached by an earlier launch would be read
+// stale.  Retired like DevBuf on growth.
 struct PinBuf {
     void* p = nullptr;
     size_t cap = 0;
     void* get(size_t bytes);
 };
+
+// Frees the allocations retired by DevBuf / PinBuf growth after a device-wide
+// synchronisation.  Called at API entry, when no work of this library is in flight.
+void release_retired();
+
+// Debug pointer audit (ANYSEQ_CHECK_PTRS=1): every pointer a fill descriptor carries
+// must lie, with its extent, inside a live library allocation or a caller buffer
+// registered for the current call.  A violation fails the call before any launch.
+bool check_ptrs_enabled();
+void register_extern_range(const void* p, size_t bytes);   // caller buffers of this call
+void register_static_range(const void* p, size_t bytes);   // allocations outside DevBuf / PinBuf
+void clear_extern_ranges();
+void check_range(const void* p, size_t bytes, const char* what);
 
 int env_int(const char* name, int dflt);
 // Diagnostics (ANYSEQ_FAULT_INFO): name a buffer for the GPU memory-fault report.
@@ -103,13 +123,15 @@ struct Engine {
     int device = 0;
     int num_cus = 256;
     hipStream_t stream = nullptr;
+    hipEvent_t ev_order = nullptr;   // orders a caller's stream behind the engine's stream
     std::mutex mu;
     FillCtx fc;
     DevBuf q, s, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq, als;
     DevBuf LE, RE, typ, pos;   // affine construct
     DevBuf status;             // affine construct: splits | types | score of a level (one download)
     DevBuf joinbuf;            // affine construct: per-slice partial maxima of the level's joins
-    PinBuf pin_up, pin_down;   // affine construct: staged uploads / downloads of a level
+    PinBuf pin_up, pin_down;   // construct: staged uploads / downloads of a level
+    PinBuf pin_blocks;         // construct: the final level's block table
     std::vector<int32_t> host_i32;
     std::vector<BlockInfo> host_blocks;
     std::vector<PartInfo> host_parts;

@@ -8,6 +8,7 @@
 //     (align.impala:69-79, the clamp at 0 folded into one saturating subtract).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace anyseq {
@@ -67,6 +68,21 @@ struct DPProblem {
 };
 constexpr int32_t kProbMagic = 0x5eb1a700;
 
+// Digest of a descriptor's words before `magic` (FNV-1a over 32-bit words).  magic =
+// kProbMagic ^ index ^ (epoch << 12) ^ digest: a fill group recomputes it from the
+// descriptor it read, so a descriptor that is stale or torn in ANY word (not only in
+// its magic) raises ERR_BAD_DESC instead of running on its pointers.
+__host__ __device__ inline uint32_t desc_digest(const uint32_t* w, int nwords) {
+    uint32_t h = 0x811c9dc5u;
+    for (int i = 0; i < nwords; ++i) h = (h ^ w[i]) * 16777619u;
+    return h;
+}
+constexpr int kDescWords = (int)(offsetof(DPProblem, magic) / 4);
+__host__ __device__ inline int32_t prob_magic(const DPProblem* P, int index, int epoch) {
+    return (int32_t)((uint32_t)kProbMagic ^ (uint32_t)index ^ ((uint32_t)epoch << 12) ^
+                     desc_digest(reinterpret_cast<const uint32_t*>(P), kDescWords));
+}
+
 // Affine border modes (H space; oracle bm_corner / bm_top / bm_left):
 //   NORMAL     the scheme's global borders (corner 0, gaps paid from it);
 //   EFREE      the path continues a horizontal gap (corner and left -inf, top
@@ -95,8 +111,12 @@ struct GroupRef {
     int32_t prob;
     int32_t group;
     int32_t epoch;   // FillParams::epoch of the launch that uploaded it
-    int32_t pad_;
+    int32_t check;   // group_check(prob, group, epoch): a torn entry is detected
 };
+__host__ __device__ inline int32_t group_check(int32_t prob, int32_t group, int32_t epoch) {
+    return (int32_t)(((uint32_t)prob * 0x9e3779b1u) ^ ((uint32_t)group * 0x85ebca6bu) ^ ((uint32_t)epoch * 0xc2b2ae35u) ^
+                     0x27d4eb2fu);
+}
 
 struct FillParams {
     int32_t kind;

@@ -945,8 +945,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
         if (gi >= ngroups_total || err_set(err)) break;
         const GroupRef g = groups[gi];
         const DPProblem P = probs[g.prob];
-        if (g.epoch != fp.epoch || P.magic != (kProbMagic ^ g.prob ^ (fp.epoch << 12)) ||
-            g.group >= P.ngroups) {
+        if (g.epoch != fp.epoch || g.check != group_check(g.prob, g.group, g.epoch) ||
+            P.magic != prob_magic(&probs[g.prob], g.prob, fp.epoch) || g.group >= P.ngroups) {
             if (threadIdx.x == 0) atomicOr(err, ERR_BAD_DESC);
             break;
         }
@@ -1499,8 +1499,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
         if (gi >= ngroups_total || err_set(err)) break;
         const GroupRef gr = groups[gi];
         const DPProblem P = probs[gr.prob];
-        if (gr.epoch != fp.epoch || P.magic != (kProbMagic ^ gr.prob ^ (fp.epoch << 12)) ||
-            gr.group >= P.ngroups) {
+        if (gr.epoch != fp.epoch || gr.check != group_check(gr.prob, gr.group, gr.epoch) ||
+            P.magic != prob_magic(&probs[gr.prob], gr.prob, fp.epoch) || gr.group >= P.ngroups) {
             if (threadIdx.x == 0) atomicOr(err, ERR_BAD_DESC);
             break;
         }

@@ -116,8 +116,10 @@ struct Shard {
             f->progress_h = (uint32_t*)p;
             void* d = nullptr;
             HIPCHECK(hipHostGetDevicePointer(&d, p, 0));
+            register_static_range(d, 64);
             HIPCHECK(hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory));
             f->progress_sig = (uint32_t*)p;
+            register_static_range(p, 8);
             f->progress = use_wait_value() ? f->progress_sig : (uint32_t*)d;
         }
         fc.init();
@@ -517,6 +519,11 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
     Engine& E = engine();
     std::lock_guard<std::mutex> lk(E.mu);
     static std::vector<Shard> shards;   // kept: streams, counters, buffers are reused
+    // every local shard's persistent fill must be co-resident with the others (they
+    // wait for each other): grid_per_shard gives each at least one workgroup per XCD
+    // and keeps 8 CUs per XCD free, so at most CUs/8 - 8 shards fit (24 on MI355X)
+    const int max_local = std::max(1, E.num_cus / 8 - 8);
+    if (N > max_local) fail("sharded fill: at most %d local shards on this device (got %d)", max_local, N);
     if (N > 64) fail("sharded fill: at most 64 local shards");
     if (shards.capacity() < 64) shards.reserve(64);   // shards never move (buffers are registered by address)
     if ((int)shards.size() < N) shards.resize(N);
@@ -808,6 +815,16 @@ static int64_t sharded_construct(int kind, const anyseq_scoring& s, const char* 
     check_value_range(s, lenq, lens);
     if (s.gap_open == 0) fail("sharded construct: affine gaps only (gap_open < 0)");
     if (lenq < 0 || lens < 0) fail("negative sequence length");
+    // the ranks' strings merge by a byte-wise MAX over a ' ' prefill: every written
+    // byte must sort above ' ' ('_' does), so sequence bytes <= 0x20 are refused
+    if (shards.world > 1) {
+        for (int i = 0; i < lenq; ++i)
+            if ((unsigned char)query[i] <= 0x20) fail("sharded construct: query byte %d is <= 0x20 (0x%02x)", i,
+                                                      (unsigned char)query[i]);
+        for (int i = 0; i < lens; ++i)
+            if ((unsigned char)subject[i] <= 0x20) fail("sharded construct: subject byte %d is <= 0x20 (0x%02x)", i,
+                                                        (unsigned char)subject[i]);
+    }
     Engine& E = engine();
     std::lock_guard<std::mutex> lk(E.mu);
     hipStream_t st = E.stream;

@@ -85,9 +85,18 @@ def main_1024(A):
 
 
 def main_65536(A):
+    """configs[1] pair: the three scores, and the reference-semantics construct_*
+    (export.impala:19-34,75-90,131-147: 9 Hirschberg levels with hb_sum's stride-class
+    candidate order) as return value + SHA-256 of both sparse strings (~5 s each)."""
+    import hashlib
     q, s = A.main_random_pair(65536, 65536)
     O.set_threads(8)
-    ent = {"args": [65536, 65536], "score": {k: O.score(k, q, s) for k in KINDS}}
+    ent = {"args": [65536, 65536], "score": {k: O.score(k, q, s) for k in KINDS}, "construct": {}}
+    for k in KINDS:
+        r, aq, as_ = O.construct(k, q, s)
+        ent["construct"][k] = {"ret": r, "sha256_alq": hashlib.sha256(aq).hexdigest(),
+                               "sha256_als": hashlib.sha256(as_).hexdigest(), "n_blank": aq.count(b" "),
+                               "n_gap_q": aq.count(b"_"), "n_gap_s": as_.count(b"_")}
     O.set_threads(4)
     return ent
 
@@ -100,6 +109,9 @@ if __name__ == "__main__":
     json.dump(oracle_cases(), open(os.path.join(HERE, "oracle_cases.json"), "w"))
     json.dump({"source": "oracle on main.cpp `-r 1024 1024` inputs (configs[0])", **main_1024(A)},
               open(os.path.join(HERE, "main_1024.json"), "w"))
-    json.dump({"source": "oracle on main.cpp `-r 65536 65536` inputs (configs[1]); scores only", **main_65536(A)},
+    json.dump({"source": "oracle on main.cpp `-r 65536 65536` inputs (configs[1]); scores, and the reference-"
+                         "semantics construct_* (export.impala:19-34,75-90,131-147; hb_sum stride classes, "
+                         "traceback_lintime.impala:44-135) as return value + SHA-256 of both sparse strings",
+               **main_65536(A)},
               open(os.path.join(HERE, "main_65536.json"), "w"))
     print("golden fixtures written")

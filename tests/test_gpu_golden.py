@@ -72,3 +72,20 @@ def test_main_65536_global_construct_properties(anyseq):
     assert dq.replace(b"_", b"") == q and ds.replace(b"_", b"") == s
     sc = sum(-1 if (a == 95 or b == 95) else (2 if a == b else -1) for a, b in zip(dq, ds))
     assert sc == g["score"]["global"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_main_65536_construct_bit_exact(anyseq, kind):
+    """The reference-semantics construct_* (export.impala:19-34,75-90,131-147) at full
+    configs[1] size through the six-symbol ABI: return value and both n+m-byte sparse
+    strings bit-exact with the oracle (SHA-256 pins; 9 Hirschberg levels whose hb_sum
+    follows the CPU BLOCK_WIDTH stride-class candidate order, traceback_lintime.impala:44-135)."""
+    import hashlib
+    g = load("main_65536.json")["construct"][kind]
+    q, s = anyseq.main_random_pair(65536, 65536)
+    r, aq, as_ = getattr(anyseq, f"construct_{kind}_alignment")(q, s)
+    assert len(aq) == len(as_) == len(q) + len(s)
+    assert r == g["ret"]
+    assert (aq.count(b" "), aq.count(b"_"), as_.count(b"_")) == (g["n_blank"], g["n_gap_q"], g["n_gap_s"])
+    assert hashlib.sha256(aq).hexdigest() == g["sha256_alq"]
+    assert hashlib.sha256(as_).hexdigest() == g["sha256_als"]

@@ -76,3 +76,17 @@ def test_shard_local_dispatch_no_deadlock(anyseq, kind):
     ref = anyseq.score(kind, q, s, gap_open=-2, gap_extend=-1)
     for _ in range(60):
         assert anyseq.shard_score_local(kind, q, s, 4, gap_open=-2, gap_extend=-1) == ref
+
+
+def test_shard_max_local_count(anyseq, oracle):
+    """The largest accepted local shard count under the suite's GPU_MAX_HW_QUEUES = 24
+    (3N - 2 transport + fill streams + 2 <= 24: N = 8) runs, co-resident and correct;
+    more shards than the device keeps co-resident (CUs/8 - 8 = 24 on MI355X) are refused
+    instead of deadlocking in dispatch."""
+    rng = random.Random(31)
+    q, s = rnd(rng, 2000), rnd(rng, 4000)
+    for kind in KINDS:
+        assert anyseq.shard_score_local(kind, q, s, 8, gap_open=-2, gap_extend=-1) == \
+            oracle.affine_score(kind, q, s, 2, -1, -2, -1), kind
+    with pytest.raises(anyseq.AnySeqError, match="at most 24 local shards"):
+        anyseq.shard_score_local("global", q, s, 25)

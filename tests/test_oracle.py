@@ -153,3 +153,21 @@ def test_main_1024_golden(oracle, anyseq):
         r, aq, as_ = oracle.construct(k, q, s)
         assert (r, aq.decode(), as_.decode()) == (g["construct"][k]["ret"], g["construct"][k]["alq"],
                                                   g["construct"][k]["als"])
+
+
+def test_main_65536_construct_golden(oracle, anyseq):
+    """The oracle regenerates the full-size configs[1] construct pins (SHA-256 of both
+    sparse strings; ~13 s at 8 threads): the fixture the GPU test compares against is
+    the restatement's own output, not a stale file."""
+    import hashlib
+    g = load("main_65536.json")["construct"]
+    q, s = anyseq.main_random_pair(65536, 65536)
+    oracle.set_threads(8)
+    try:
+        for k in KINDS:
+            r, aq, as_ = oracle.construct(k, q, s)
+            assert r == g[k]["ret"]
+            assert hashlib.sha256(aq).hexdigest() == g[k]["sha256_alq"]
+            assert hashlib.sha256(as_).hexdigest() == g[k]["sha256_als"]
+    finally:
+        oracle.set_threads(4)
