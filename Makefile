@@ -33,7 +33,7 @@ oracle:
 stamps: anyseq_amd/libanyseq_stamps.so
 anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o $(SRC)/anyseq_internal.h $(SRC)/anyseq_block_asm.inc
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_stamps.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
 clean:
 	rm -f $(SRC)/*.o $(LIB) anyseq_amd/libanyseq_*.so

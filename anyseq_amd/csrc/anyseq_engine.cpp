@@ -57,6 +57,11 @@ hipError_t anyseq_launch_aff_hb_join2(const void* parts, int nparts, int maxlen,
                                       const int32_t* LE, const int32_t* RH, const int32_t* RE, const int32_t* pbest,
                                       int go, int ge, void* partial, int32_t* splits, int32_t* types, int32_t* score,
                                       hipStream_t st);
+hipError_t anyseq_launch_view_reduce_i32(int32_t* base, size_t stride, int nviews, size_t n, int op, hipStream_t st);
+hipError_t anyseq_launch_view_max_u8(uint8_t* dst, const uint8_t* others, size_t stride, int nothers, size_t n,
+                                     hipStream_t st);
+hipError_t anyseq_launch_seq_codes(const uint8_t* q, int n, const uint8_t* s, int m, uint32_t* mask, uint8_t* table,
+                                   int32_t* alpha, uint8_t* out, hipStream_t st);
 hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
                                       int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows,
                                       hipStream_t st);
@@ -284,6 +289,7 @@ void init_tuning_locked() {
     g_tuning.thr = env_int("ANYSEQ_THROTTLE", g_tuning.thr);
     g_tuning.NWa = env_int("ANYSEQ_NWA", g_tuning.NWa);
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
+    g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning_init = true;
 }
 
@@ -582,8 +588,10 @@ void fill_collect(FillCtx& C) {
                 unsigned long long t0 = ~0ull;
                 for (size_t i = 0; i < t.size(); i += 4) if (t[i] && t[i] < t0) t0 = t[i];
                 for (size_t i = 0; i < t.size(); i += 4)
-                    if (t[i]) fprintf(f, "%zu %.2f %.2f %.2f\n", i / 4, (t[i] - t0) / 100.0,
-                                      t[i + 1] ? (t[i + 1] - t0) / 100.0 : -1.0, (t[i + 2] - t0) / 100.0);
+                    if (t[i]) fprintf(f, "%zu %.2f %.2f %.2f %.2f\n", i / 4, (t[i] - t0) / 100.0,
+                                      t[i + 1] ? (t[i + 1] - t0) / 100.0 : -1.0, (t[i + 2] - t0) / 100.0,
+                                      t[i + 3] && t[i + 3] >= t0 ? (t[i + 3] - t0) / 100.0
+                                                                 : (t[i + 3] < (1ull << 32) ? -2.0 - (double)t[i + 3] : -1.0));
                 fclose(f);
             }
         }
@@ -597,6 +605,21 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
     fill_finish(E.fc);
 }
 
+// Alphabet codes of the pair: q ++ s recoded into E.codes (n + m
+// bytes), the symbol count in device memory.  The affine fills compare codes; the
+// kernel reads the count itself (no host synchronisation).
+SeqCodes prepare_codes(Engine& E, const uint8_t* dq, int n, const uint8_t* ds, int m, hipStream_t st) {
+    const bool fresh = E.codemeta.p == nullptr;
+    char* meta = (char*)E.codemeta.get(512);
+    uint32_t* mask = (uint32_t*)meta;
+    uint8_t* table = (uint8_t*)(meta + 64);
+    int32_t* alpha = (int32_t*)(meta + 320);
+    if (fresh) HIPCHECK(hipMemsetAsync(mask, 0, 32, st));   // (the recode kernel clears it after each use)
+    uint8_t* out = (uint8_t*)E.codes.get((size_t)std::max(n, 0) + (size_t)std::max(m, 0) + 16);
+    HIPCHECK(anyseq_launch_seq_codes(dq, std::max(n, 0), ds, std::max(m, 0), mask, table, alpha, out, st));
+    return SeqCodes{out, out + std::max(n, 0), alpha};
+}
+
 FillParams make_params(int kind, const anyseq_scoring& sc) {
     FillParams fp;
     memset(&fp, 0, sizeof fp);
@@ -608,8 +631,15 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.gap_extend = sc.gap_extend;
     fp.affine = sc.gap_open != 0;
     fp.dbg = nullptr;
-    // affine_asm bit 0: asm steady state, bit 1: scalar row stores, bit 2: asm prologue (diagnostics)
-    fp.pad = ((g_tuning.affasm & 1) ? 0 : 1) | (g_tuning.affasm & 2) | ((g_tuning.affasm & 4) ? 0 : 4);
+    // affine_asm bit 0: asm steady state, bit 1: scalar row stores (diagnostics)
+    fp.pad = ((g_tuning.affasm & 1) ? 0 : 1) | (g_tuning.affasm & 2);
+    // the LUT weights (G space sub - 2 ge, X space sub - ge) must fit int8
+    const int nge = -sc.gap_extend;
+    const int ws[4] = {sc.match + 2 * nge, sc.mismatch + 2 * nge, sc.match + nge, sc.mismatch + nge};
+    fp.lut_ok = g_tuning.afflut ? 1 : 0;
+    for (int w : ws)
+        if (w < -128 || w > 127) fp.lut_ok = 0;
+    fp.alpha = nullptr;
     return fp;
 }
 
@@ -727,9 +757,12 @@ int64_t score_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* 
 // Affine (Gotoh) score: the same one- or two-front scheme as score_dev over
 // fill_affine_kernel; rows are (G, F) pairs, so the combine also joins a vertical
 // gap that crosses the split row (aff_reduce_kernel).
-int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds,
-                         int m, hipStream_t st) {
-    const FillParams fp = make_params(kind, sc);
+int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq_raw, int n,
+                         const uint8_t* ds_raw, int m, hipStream_t st) {
+    FillParams fp = make_params(kind, sc);
+    const SeqCodes cd = prepare_codes(E, dq_raw, n, ds_raw, m, st);
+    fp.alpha = cd.alpha;
+    const uint8_t *dq = cd.q, *ds = cd.s;
     const int wpad = (m + 63) & ~63;
     const int NW = g_tuning.NWa == 3 ? 3 : 4;
     int32_t* res = (int32_t*)E.fc.ctr.get(128) + 4;
@@ -971,6 +1004,7 @@ struct RowToColJob {   // anyseq_kernels.hip RowToCol
     int32_t* H;
     int32_t* E;
     int32_t n, hlast;
+    int32_t xs, pad_;     // the row holds X-space values (amode != 0)
 };
 
 // One Hirschberg half: rows qoff + qstep*r (r < h) of the query against columns
@@ -993,7 +1027,7 @@ void add_half(std::vector<DPProblem>& probs, std::vector<RowToColJob>& jobs, int
         P.out_row = rowpool;
         rowpool += (size_t)((h + 63) & ~63) * 2;
         probs.push_back(P);
-        jobs.push_back(RowToColJob{P.out_row, H, E, h, w - 1});
+        jobs.push_back(RowToColJob{P.out_row, H, E, h, w - 1, P.amode != 0 ? 1 : 0, 0});
         return;
     }
     DPProblem P = aff_problem(dq, qoff, qstep, h, ds, soff, sstep, w);
@@ -1009,14 +1043,29 @@ void add_half(std::vector<DPProblem>& probs, std::vector<RowToColJob>& jobs, int
 // Returns the level-1 join value (the optimal score) or INT64_MIN if m <= 128
 // (no level).  kind != global with a level-1 value <= 0 stops there (empty
 // alignment).
+//
+// Sharded: the half fills of every level and the final blocks are
+// dealt round-robin to `world` ranks.  A rank fills only its halves into ZEROED level
+// columns, the columns are SUM-reduced and the free-end best cells MAX-reduced over the
+// ranks (rows a rank did not fill are 0), so every rank joins every part; a rank walks
+// only its final blocks into ' '-filled strings, which merge by a byte-wise MAX.  The
+// RCCL path holds one rank view per process and reduces with RCCL; local mode holds
+// all `world` views in this process (each with its own columns, best cells and
+// strings) and reduces them with device kernels -- the same data flow on one GPU.
 int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds,
                          int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st, const ConstructShards* shards) {
-    const FillParams fp = make_params(KIND_GLOBAL, sc);
-    // Sharded construct: half fills and final blocks are dealt round-robin
-    // to the ranks (virtual ranks: one launch each, in turn); every rank joins every part.
+    FillParams fp = make_params(KIND_GLOBAL, sc);
+    // the level fills compare alphabet codes; the final blocks emit the raw bytes
+    const SeqCodes cd = prepare_codes(E, dq, n, ds, m, st);
+    fp.alpha = cd.alpha;
+    const uint8_t *cq = cd.q, *cs = cd.s;
     const int world = shards ? shards->world : 1;
-    const int nlaunch = shards && shards->local ? world : 1;   // launches per level (local mode)
+    const bool sharded = world > 1;
+    const bool emulate = shards && shards->local && sharded;   // all ranks' views in this process
+    const int nviews = emulate ? world : 1;
+    const int my_rank = shards && !shards->local ? shards->rank : 0;
     auto owner = [&](int idx) { return idx % world; };
+    auto view_rank = [&](int v) { return emulate ? v : my_rank; };
     const bool local = kind == KIND_LOCAL;
     HostSplits sp;
     sp.nb = (m + MIN_PART_WIDTH_HB - 1) / MIN_PART_WIDTH_HB;
@@ -1041,9 +1090,26 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     memcpy(h_status, sp.v.data(), nsv * 4);
     memcpy(h_status + nsv, typ.data(), nsv * 4);
     HIPCHECK(hipMemcpyAsync(d_status, h_status, 2 * nsv * 4, hipMemcpyHostToDevice, st));
-    const size_t nn = (size_t)std::max(n, 1) * 4;
-    int32_t *LH = (int32_t*)E.L.get(nn), *LE = (int32_t*)E.LE.get(nn);
-    int32_t *RH = (int32_t*)E.R.get(nn), *RE = (int32_t*)E.RE.get(nn);
+    // level columns: view v's LH / LE / RH / RE at + v * nn
+    const size_t nn = (size_t)std::max(n, 1);
+    int32_t *LH0 = (int32_t*)E.L.get(nviews * nn * 4), *LE0 = (int32_t*)E.LE.get(nviews * nn * 4);
+    int32_t *RH0 = (int32_t*)E.R.get(nviews * nn * 4), *RE0 = (int32_t*)E.RE.get(nviews * nn * 4);
+    // emulated ranks' strings (view 0 writes the output itself)
+    const size_t L = (size_t)n + (size_t)m;
+    uint8_t* vstr = nullptr;
+    if (emulate) {
+        vstr = (uint8_t*)E.vstr.get((size_t)(nviews - 1) * 2 * std::max<size_t>(L, 1));
+        HIPCHECK(hipMemsetAsync(vstr, ' ', (size_t)(nviews - 1) * 2 * L, st));
+    }
+    auto view_str = [&](int v, uint8_t*& aq, uint8_t*& as) {
+        if (v == 0) {
+            aq = d_alq;
+            as = d_als;
+        } else {
+            aq = vstr + (size_t)(v - 1) * 2 * L;
+            as = aq + L;
+        }
+    };
     HIPCHECK(hipStreamSynchronize(st));   // h_status is rewritten by the first level's download
     auto tp = [&](int idx) { return typ[idx + 1]; };
     int64_t score = INT64_MIN;
@@ -1061,14 +1127,15 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         const int half = pw / 2;
         const int parts = (m + half - 1) / pw;
         ++g_stage_level;
-        int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * parts * 4);   // (set by the level's first launch)
-        std::vector<std::vector<DPProblem>> probs_of((size_t)nlaunch);
+        // free-end best cells, 2 per part, per view
+        int32_t* pbest0 = (int32_t*)E.bmax.get((size_t)nviews * 2 * parts * 4);
+        std::vector<std::vector<DPProblem>> probs_of((size_t)nviews);
         std::vector<PartInfo>& pinfo = E.host_parts;
         pinfo.assign((size_t)parts, PartInfo{});
         std::vector<RowToColJob> jobs;
         int half_index = 0;   // the level's half fills in part order: left 2k, right 2k+1
-        if (shards && !shards->local) {   // rows this rank does not fill are zero in the SUM reduction
-            for (int32_t* b : {LH, LE, RH, RE}) HIPCHECK(hipMemsetAsync(b, 0, nn, st));
+        if (sharded) {   // rows a rank does not fill are zero in the SUM reduction
+            for (int32_t* b : {LH0, LE0, RH0, RE0}) HIPCHECK(hipMemsetAsync(b, 0, nviews * nn * 4, st));
         }
         // transposed halves' bottom rows: sum of part heights <= n (parts' rows are disjoint)
         int32_t* rowpool = (int32_t*)E.outrow.get((size_t)2 * ((size_t)n + 64 * (size_t)parts) * 2 * 4);
@@ -1098,15 +1165,18 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             const int best_bits = local ? AM_BEST_ALL : AM_BEST_LAST;
             // (half_index advances on every rank, so all ranks agree on the owners)
             const int ol = owner(half_index++), orr = owner(half_index++);
-            if (!shards || shards->local || ol == shards->rank)
-                add_half(probs_of[shards && shards->local ? ol : 0], jobs, rowpool, dq, off, 1, len, ds, hoj_l, 1,
-                         half, pi.smode, (pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0),
-                         efree ? pbest + 2 * p : nullptr, LH + off, LE + off);
-            if (!shards || shards->local || orr == shards->rank)
-                add_half(probs_of[shards && shards->local ? orr : 0], jobs, rowpool, dq, off + len - 1, -1, len, ds,
-                         hoj_r + hw - 1, -1, hw, pi.emode,
-                         (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0),
-                         sfree ? pbest + 2 * p + 1 : nullptr, RH + off, RE + off);
+            for (int v = 0; v < nviews; ++v) {
+                const size_t vo = (size_t)v * nn;
+                int32_t* pb = pbest0 + (size_t)v * 2 * parts;
+                if (!sharded || ol == view_rank(v))
+                    add_half(probs_of[v], jobs, rowpool, cq, off, 1, len, cs, hoj_l, 1, half, pi.smode,
+                             (pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0),
+                             efree ? pb + 2 * p : nullptr, LH0 + vo + off, LE0 + vo + off);
+                if (!sharded || orr == view_rank(v))
+                    add_half(probs_of[v], jobs, rowpool, cq, off + len - 1, -1, len, cs, hoj_r + hw - 1, -1, hw,
+                             pi.emode, (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0),
+                             sfree ? pb + 2 * p + 1 : nullptr, RH0 + vo + off, RE0 + vo + off);
+            }
         }
         // the level's parts and row-to-column jobs, staged together in pinned memory
         // (the jobs hold pointers: they start 16-byte aligned)
@@ -1114,30 +1184,30 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         char* up = (char*)E.pin_up.get(jb + pb + 16);
         memcpy(up, pinfo.data(), pinfo.size() * sizeof(PartInfo));
         memcpy(up + pb, jobs.data(), jb);
-        // one fill launch per level is left running (collected after the level's single
-        // synchronisation); local virtual ranks share the fill context, so all but the
-        // last of their launches complete in turn.  A single launch carries the parts and
-        // jobs in its own upload (fill_prepare's extra payload): one copy per level.
+        // one fill launch per view with work; all but the last complete in turn (they share
+        // the fill context), the last is collected after the level's single synchronisation.
+        // A single launch carries the parts and jobs in its own upload (one copy per level).
         int nl = 0;
         for (const auto& probs : probs_of) nl += probs.empty() ? 0 : 1;
         bool pending_fill = false;
         const char* d_up = nullptr;
         const double t_built = now_us();
-        for (size_t li = 0; li < probs_of.size(); ++li) {
-            auto& probs = probs_of[li];
-            if (probs.empty()) continue;
+        for (int v = 0; v < nviews; ++v) {
+            auto& probs = probs_of[v];
+            int32_t* pbv = pbest0 + (size_t)v * 2 * parts;
+            if (probs.empty()) {
+                HIPCHECK(hipMemsetD32Async(pbv, kAffNegH, (size_t)2 * parts, st));
+                continue;
+            }
             if (pending_fill) fill_finish(E.fc);
-            int32_t* init = pending_fill ? nullptr : pbest;   // the first launch of the level sets pbest
-            const int ninit = pending_fill ? 0 : 2 * parts;
             if (nl == 1) {
-                fill_async(E, E.fc, probs, fp, st, 0, up, pb + jb, init, ninit, kAffNegH);
+                fill_async(E, E.fc, probs, fp, st, 0, up, pb + jb, pbv, 2 * parts, kAffNegH);
                 d_up = (const char*)E.fc.d_extra;
             } else {
-                fill_async(E, E.fc, probs, fp, st, 0, nullptr, 0, init, ninit, kAffNegH);
+                fill_async(E, E.fc, probs, fp, st, 0, nullptr, 0, pbv, 2 * parts, kAffNegH);
             }
             pending_fill = true;
         }
-        if (!pending_fill) HIPCHECK(hipMemsetD32Async(pbest, kAffNegH, (size_t)2 * parts, st));
         if (!d_up) {
             char* d = (char*)E.parts.get(pb + jb + 16);
             HIPCHECK(hipMemcpyAsync(d, up, pb + jb, hipMemcpyHostToDevice, st));
@@ -1151,16 +1221,23 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             HIPCHECK(anyseq_launch_aff_row_to_col(d_up + pb, (int)jobs.size(), maxn, -sc.gap_extend, st));
             stage_check(st, "aff_row_to_col");
         }
-        if (shards && !shards->local) {   // every rank gets every part's columns and best cells
-            for (int32_t* b : {LH, LE, RH, RE}) shards->sum_i32(b, (size_t)n, st);
-            shards->max_i32(pbest, (size_t)2 * parts, st);
+        if (sharded) {   // every rank gets every part's columns and best cells
+            if (emulate) {
+                for (int32_t* b : {LH0, LE0, RH0, RE0})
+                    HIPCHECK(anyseq_launch_view_reduce_i32(b, nn, nviews, nn, 0, st));
+                HIPCHECK(anyseq_launch_view_reduce_i32(pbest0, (size_t)2 * parts, nviews, (size_t)2 * parts, 1, st));
+            } else {
+                for (int32_t* b : {LH0, LE0, RH0, RE0}) shards->sum_i32(b, (size_t)n, st);
+                shards->max_i32(pbest0, (size_t)2 * parts, st);
+            }
         }
         const PartInfo* d_parts = (const PartInfo*)d_up;
         int maxlen = 0;
         for (const PartInfo& q : pinfo) maxlen = std::max(maxlen, (q.flags & 4) ? 0 : q.len);
         const size_t nsl = (size_t)std::max(1, (maxlen + 1 + 4095) / 4096);
         void* partial = E.joinbuf.get((size_t)parts * nsl * 8);
-        HIPCHECK(anyseq_launch_aff_hb_join2(d_parts, parts, maxlen, half, LH, LE, RH, RE, pbest, sc.gap_open,
+        // (view 0's columns: after the reduction every view holds the same)
+        HIPCHECK(anyseq_launch_aff_hb_join2(d_parts, parts, maxlen, half, LH0, LE0, RH0, RE0, pbest0, sc.gap_open,
                                             sc.gap_extend, partial, d_spl, d_typ, level1 ? d_score : nullptr, st));
         stage_check(st, "aff_hb_join");
         HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + (level1 ? 1 : 0)) * 4, hipMemcpyDeviceToHost, st));
@@ -1198,47 +1275,60 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         pw /= 2;
         sp.bpp /= 2;
     }
+    // final 128-column blocks: each view walks its own into its strings
     std::vector<BlockInfo>& blocks = E.host_blocks;   // outlives the async upload
     blocks.clear();
+    std::vector<int> vbeg((size_t)nviews + 1, 0);
     int64_t pred_bytes = 0;
     int lds_rows = 1;   // the tallest block, up to kPredLdsMaxRows (its predecessors fit in LDS)
     for (int b = 0; b < sp.nb; ++b)
         if (!(tp(b - 1) == T_BEFORE || tp(b) == T_AFTER))
             lds_rows = std::max(lds_rows, std::min(kPredLdsMaxRows, sp.at(b) - sp.at(b - 1)));
-    for (int b = 0; b < sp.nb; ++b) {
-        const int ts = tp(b - 1), te = tp(b);
-        if (ts == T_BEFORE || te == T_AFTER) continue;   // the path does not touch the block
-        if (shards && !shards->local && owner(b) != shards->rank) continue;   // another rank walks it
-        BlockInfo bi{};
-        bi.oi = sp.at(b - 1);
-        bi.h = sp.at(b) - bi.oi;
-        bi.oj = b * MIN_PART_WIDTH_HB;
-        bi.w = std::min(MIN_PART_WIDTH_HB, m - bi.oj);
-        bi.pred_base = pred_bytes;
-        bi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, bi.oj == 0);
-        bi.e_end = te == T_H ? 0 : te == T_E ? 1 : 2;
-        bi.flags = (local ? 1 : 0) | (bi.oj + bi.w == m ? 2 : 0);
-        if (bi.h > lds_rows) pred_bytes += (int64_t)(bi.h + 127) * 128;   // (shorter blocks: LDS)
-        blocks.push_back(bi);
-    }
-    if (blocks.empty()) {
-        if (shards && !shards->local) {
-            shards->max_u8(d_alq, (size_t)n + m, st);
-            shards->max_u8(d_als, (size_t)n + m, st);
+    for (int v = 0; v < nviews; ++v) {
+        vbeg[v] = (int)blocks.size();
+        for (int b = 0; b < sp.nb; ++b) {
+            const int ts = tp(b - 1), te = tp(b);
+            if (ts == T_BEFORE || te == T_AFTER) continue;        // the path does not touch the block
+            if (sharded && owner(b) != view_rank(v)) continue;    // another rank walks it
+            BlockInfo bi{};
+            bi.oi = sp.at(b - 1);
+            bi.h = sp.at(b) - bi.oi;
+            bi.oj = b * MIN_PART_WIDTH_HB;
+            bi.w = std::min(MIN_PART_WIDTH_HB, m - bi.oj);
+            bi.pred_base = pred_bytes;
+            bi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, bi.oj == 0);
+            bi.e_end = te == T_H ? 0 : te == T_E ? 1 : 2;
+            bi.flags = (local ? 1 : 0) | (bi.oj + bi.w == m ? 2 : 0);
+            if (bi.h > lds_rows) pred_bytes += (int64_t)(bi.h + 127) * 128;   // (shorter blocks: LDS)
+            blocks.push_back(bi);
         }
-        return score;
     }
-    BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
-    upload_pinned(E.pin_blocks, d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), st);
-    uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
-    HIPCHECK(anyseq_launch_aff_predwalk(d_blocks, (int)blocks.size(), dq, ds, d_pred, sc.match, sc.mismatch,
-                                        sc.gap_open, sc.gap_extend, d_alq, d_als, lds_rows, st));
-    stage_check(st, "aff_predwalk");
-    if (shards && !shards->local) {
+    vbeg[nviews] = (int)blocks.size();
+    if (!blocks.empty()) {
+        BlockInfo* d_blocks = (BlockInfo*)E.blocks.get(blocks.size() * sizeof(BlockInfo));
+        upload_pinned(E.pin_blocks, d_blocks, blocks.data(), blocks.size() * sizeof(BlockInfo), st);
+        uint8_t* d_pred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(pred_bytes, 16));
+        for (int v = 0; v < nviews; ++v) {
+            const int nb = vbeg[v + 1] - vbeg[v];
+            if (nb <= 0) continue;
+            uint8_t *aq, *as;
+            view_str(v, aq, as);
+            HIPCHECK(anyseq_launch_aff_predwalk(d_blocks + vbeg[v], nb, dq, ds, d_pred, sc.match, sc.mismatch,
+                                                sc.gap_open, sc.gap_extend, aq, as, lds_rows, st));
+            stage_check(st, "aff_predwalk");
+        }
+    }
+    if (sharded) {
         // blocks write disjoint positions over a ' ' prefill, and every written byte
-        // ('_' or a symbol) is above ' ': a byte-wise MAX merges the ranks' strings
-        shards->max_u8(d_alq, (size_t)n + m, st);
-        shards->max_u8(d_als, (size_t)n + m, st);
+        // ('_' or a symbol; sharded_construct refuses bytes <= ' ') is above ' ': a
+        // byte-wise MAX merges the ranks' strings
+        if (emulate) {
+            HIPCHECK(anyseq_launch_view_max_u8(d_alq, vstr, 2 * L, nviews - 1, L, st));
+            HIPCHECK(anyseq_launch_view_max_u8(d_als, vstr + L, 2 * L, nviews - 1, L, st));
+        } else {
+            shards->max_u8(d_alq, L, st);
+            shards->max_u8(d_als, L, st);
+        }
     }
     return score;
 }
@@ -1543,6 +1633,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_transpose") g_tuning.afft = value;
     else if (n == "priority") g_tuning.prio = value;
     else if (n == "throttle") g_tuning.thr = value;
+    else if (n == "affine_lut") g_tuning.afflut = value;
     else return -1;
     return 0;
 }

@@ -89,6 +89,7 @@ struct Tuning {
     int afft = 1;        // affine construct: run Hirschberg halves taller than wide transposed
     int prio = 0;        // compute waves at s_setprio 3 (the I/O wave stays at 0)
     int thr = 0;         // band 0 of every problem sleeps thr s_sleep-1 units per block (chain pace)
+    int afflut = 1;      // affine fill: v_perm weight table when the pair has <= 8 symbols
 };
 extern Tuning g_tuning;
 
@@ -137,8 +138,18 @@ struct Engine {
     std::vector<PartInfo> host_parts;
     std::vector<uint8_t> host_jobs;
     DevBuf jobs;
+    DevBuf codes, codemeta;    // alphabet codes of the current pair (prepare_codes)
+    DevBuf vstr;               // sharded construct, emulated ranks: their ' '-filled strings
     explicit Engine(int dev);
 };
+
+// A pair recoded to alphabet codes.
+struct SeqCodes {
+    const uint8_t* q;
+    const uint8_t* s;
+    const int32_t* alpha;   // device: number of distinct symbols
+};
+SeqCodes prepare_codes(Engine& E, const uint8_t* dq, int n, const uint8_t* ds, int m, hipStream_t st);
 
 Engine& engine();
 int rows_per_lane();

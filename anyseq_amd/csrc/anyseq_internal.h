@@ -128,6 +128,12 @@ struct FillParams {
     int32_t epoch;                    // launch counter: descriptors carry it (stale uploads are detected)
     int32_t prio;                     // compute waves raise their issue priority (s_setprio 3) when set
     int32_t throttle;                 // s_sleep 1 units per block in a problem's band 0 (chain pace)
+    // Affine fill: alpha -> number of distinct symbols of the pair when q / s
+    // hold alphabet codes 0 .. n-1 (seq_code_kernel), else null; lut_ok: the diagonal weights
+    // of both value spaces fit int8 (the v_perm weight table).
+    const int32_t* alpha;
+    int32_t lut_ok;
+    int32_t pad2_;
 };
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).

@@ -841,6 +841,16 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             for (int b = sk_next; b < lim; ++b) {
                 uint32_t d[8];
                 load_sbytes<32>(s_ring, (32 * b - 1 - lane) & (kSRing - 1), d);
+                // columns left of 0 (virtual prologue lanes): code 0xFF, which matches no
+                // query code (the LUT weight of 0xFF is -1)
+                const int cneg = 32 * b - 1 - lane;
+                if (cneg < 0) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+#pragma unroll
+                        for (int kb = 0; kb < 4; ++kb)
+                            if (cneg + 4 * i + kb < 0) d[i] |= 0xffu << (8 * kb);
+                }
                 uint32_t* dst = skew + (b % kSkewBlocks) * 8 * 64 + lane;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) dst[64 * i] = d[i];
@@ -1036,8 +1046,10 @@ struct AffK {
     int wm, wx;   // diagonal weight sub - 2 ge
     int go;       // gap open (<= 0): added to a cell to open a gap (G space)
     int nge;      // -ge > 0
-    int flags;    // bit 0: no asm steady state, bit 2: no asm prologue (diagnostics)
+    int flags;    // bit 0: no asm steady state (diagnostics)
     int thr;      // FillParams::throttle
+    bool codes;   // q / s hold alphabet codes (0xFF never a code): the virtual prologue may clamp
+    bool lut;     // codes 0..7 and int8 weights: the v_perm weight table
 };
 
 // Borders of a problem in G space (H border values by border mode, see
@@ -1102,7 +1114,8 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
         const int2 top = u == 0 ? tf : rv[u - 1];
         const int upg = wave_shr1(top.x, g);
         const int fin = wave_shr1(top.y, fdn);
-        const int sb = (int)((sw[u >> 2] >> (8 * (u & 3))) & 0xffu);
+        // virtual columns (< 0) hold a code that matches no query code
+        const int sb = (VIRT && c0 + u < 0) ? 0x1ff : (int)((sw[u >> 2] >> (8 * (u & 3))) & 0xffu);
         const int wgt = q == sb ? k.wm : k.wx;
         const int en = max(e, hg);
         int v = max(max(dg + wgt, en), fin);
@@ -1133,6 +1146,25 @@ struct AffLoopArgs {
     uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs;
     uint64_t gp;
 };
+#ifdef ANYSEQ_STAMPS   // diagnostic build: first steady block start / loop end times
+#define AFF_LOOP_NAME(NAME) NAME##_TS
+#define AFF_TS_OUT , [ts] "+s"(ts_v), [te] "+s"(te_v), [tsf] "+s"(ts_f)
+#else
+#define AFF_LOOP_NAME(NAME) NAME
+#define AFF_TS_OUT
+#endif
+#define AFF_ASM_TS(NAME)                                                                                        \
+    asm volatile(NAME                                                                                          \
+                 : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
+                   [hg] "+v"(hg), [best] "+v"(best), [z] "+s"(z), [zb] "+s"(zb), [b] "+s"(b), [sp] "+s"(sp),     \
+                   [sf] "+s"(sf), [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), \
+                   [x3] "=&s"(x3), [x4] "=&s"(x4) AFF_TS_OUT                                                   \
+                 : [be] "s"(be), [q] "v"(q), [wm] "v"(k.wm), [wx] "v"(k.wx), [go] "v"(k.go), [nge] "s"(nge),     \
+                   [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp),          \
+                   [anc] "v"(la.anc), [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo),  \
+                   [lid8] "v"(la.lid8), [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp),           \
+                   [thr] "s"(thr)                                                                              \
+                 : ANYSEQ_AFF_ASM_CLOBBERS, "memory")
 #define AFF_ASM(NAME)                                                                                           \
     asm volatile(NAME                                                                                          \
                  : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
@@ -1149,7 +1181,8 @@ struct AffLoopArgs {
 template <bool L, bool BORDER, int PUB>
 __device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                  const AffLoopArgs& la, int q, int& g, int& fdn, int& dg, int2& tf,
-                                                 int& e, int& hg, int& best, uint32_t& z, uint32_t& zb, const AffK& k) {
+                                                 int& e, int& hg, int& best, uint32_t& z, uint32_t& zb, const AffK& k,
+                                                 uint64_t& ts_v, uint64_t& te_v, uint32_t& ts_f) {
     uint32_t st, x0, x1, x2, x3, x4;
     const uint64_t hm = 0xffffffff00000000ull;
 #define RFL(x) __builtin_amdgcn_readfirstlane(x)
@@ -1164,20 +1197,29 @@ __device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint3
     const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
 #undef RFL
     int tfg = tf.x, tff = tf.y;
+#ifdef ANYSEQ_STAMPS
+    ts_f = __builtin_amdgcn_readfirstlane(ts_f);
+    ts_v = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ts_v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ts_v);
+    te_v = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(te_v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)te_v);
+#else
+    (void)ts_v, (void)te_v, (void)ts_f;
+#endif
     if constexpr (L) {
-        if constexpr (BORDER && PUB == 0) AFF_ASM(ANYSEQ_AFF_L_B1_NONE);
-        if constexpr (BORDER && PUB == 1) AFF_ASM(ANYSEQ_AFF_L_B1_LDS);
-        if constexpr (BORDER && PUB == 2) AFF_ASM(ANYSEQ_AFF_L_B1_GLOB);
-        if constexpr (!BORDER && PUB == 0) AFF_ASM(ANYSEQ_AFF_L_B0_NONE);
-        if constexpr (!BORDER && PUB == 1) AFF_ASM(ANYSEQ_AFF_L_B0_LDS);
-        if constexpr (!BORDER && PUB == 2) AFF_ASM(ANYSEQ_AFF_L_B0_GLOB);
+        if constexpr (BORDER && PUB == 0) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B1_NONE));
+        if constexpr (BORDER && PUB == 1) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B1_LDS));
+        if constexpr (BORDER && PUB == 2) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B1_GLOB));
+        if constexpr (!BORDER && PUB == 0) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B0_NONE));
+        if constexpr (!BORDER && PUB == 1) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B0_LDS));
+        if constexpr (!BORDER && PUB == 2) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B0_GLOB));
     } else {
-        if constexpr (BORDER && PUB == 0) AFF_ASM(ANYSEQ_AFF_G_B1_NONE);
-        if constexpr (BORDER && PUB == 1) AFF_ASM(ANYSEQ_AFF_G_B1_LDS);
-        if constexpr (BORDER && PUB == 2) AFF_ASM(ANYSEQ_AFF_G_B1_GLOB);
-        if constexpr (!BORDER && PUB == 0) AFF_ASM(ANYSEQ_AFF_G_B0_NONE);
-        if constexpr (!BORDER && PUB == 1) AFF_ASM(ANYSEQ_AFF_G_B0_LDS);
-        if constexpr (!BORDER && PUB == 2) AFF_ASM(ANYSEQ_AFF_G_B0_GLOB);
+        if constexpr (BORDER && PUB == 0) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B1_NONE));
+        if constexpr (BORDER && PUB == 1) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B1_LDS));
+        if constexpr (BORDER && PUB == 2) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B1_GLOB));
+        if constexpr (!BORDER && PUB == 0) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B0_NONE));
+        if constexpr (!BORDER && PUB == 1) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B0_LDS));
+        if constexpr (!BORDER && PUB == 2) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B0_GLOB));
     }
     tf = make_int2(tfg, tff);
     return st;
@@ -1218,8 +1260,80 @@ __device__ __forceinline__ uint32_t aff_prologue_asm(uint32_t& sp, uint32_t& sf,
 }
 #undef AFF_ASM
 
+// Round-3 steady state (tools/gen_block_asm.py gen_aff2): blocks b .. be-1, kind
+// L = X space (clamp / best) or G space, weights by LUT or compare.  pf: the first
+// half of block b's top row is already in the TOP registers (never on entry from
+// C++: 0).  Returns 0, or 1 on a spin timeout.
+struct Aff2Args {
+    uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs;
+    uint64_t gp;
+    int q, wm, wx, ll, lh, zlp;
+};
+#ifdef ANYSEQ_STAMPS
+#define AF2_NAME(NAME) NAME##_TS
+#define AF2_TS_OUT , [ts] "+s"(ts_v), [te] "+s"(te_v), [tsf] "+s"(ts_f), [nmiss] "+s"(nmiss)
+#else
+#define AF2_NAME(NAME) NAME
+#define AF2_TS_OUT
+#endif
+#define AF2_ASM(NAME)                                                                                           \
+    asm volatile(NAME                                                                                          \
+                 : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
+                   [hg] "+v"(hg), [best] "+v"(bx), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf), [sc] "+s"(sc),     \
+                   [pf] "+s"(pf), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3), \
+                   [x4] "=&s"(x4) AF2_TS_OUT                                                                   \
+                 : [be] "s"(be), [q] "v"(a.q), [wm] "v"(a.wm), [wx] "v"(a.wx), [ll] "v"(a.ll), [lh] "v"(a.lh),   \
+                   [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
+                   [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
+                   [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
+                   [hm] "s"(hm), [gp] "s"(gp)                                                                  \
+                 : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
+template <bool L, bool BORDER, int PUB, bool LUT>
+__device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
+                                                  const Aff2Args& a, int go, int nge, int& g, int& fdn, int& dg,
+                                                  int2& tf, int& e, int& hg, int& bx, uint64_t& ts_v, uint64_t& te_v,
+                                                  uint32_t& ts_f, uint32_t& nmiss) {
+    uint32_t st, x0, x1, x2, x3, x4, pf = 0;
+    const uint64_t hm = 0xffffffff00000000ull;
+#define RFL(x) __builtin_amdgcn_readfirstlane(x)
+    b = RFL(b);
+    sp = RFL(sp);
+    sf = RFL(sf);
+    sc = RFL(sc);
+    be = RFL(be);
+    const uint32_t rb = RFL(a.rb), nb = RFL(a.nb), bvs = RFL(a.bvs);
+    const int ge = RFL(-nge);
+    const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(a.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)a.gp);
+#ifdef ANYSEQ_STAMPS
+    ts_f = RFL(ts_f);
+    nmiss = RFL(nmiss);
+    ts_v = ((uint64_t)(uint32_t)RFL((uint32_t)(ts_v >> 32)) << 32) | (uint32_t)RFL((uint32_t)ts_v);
+    te_v = ((uint64_t)(uint32_t)RFL((uint32_t)(te_v >> 32)) << 32) | (uint32_t)RFL((uint32_t)te_v);
+#else
+    (void)ts_v, (void)te_v, (void)ts_f, (void)nmiss;
+#endif
+#undef RFL
+    int tfg = tf.x, tff = tf.y;
+#define AF2_SEL(K, U)                                                                   \
+    if constexpr (BORDER && PUB == 0) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B1_NONE_U##U));          \
+    if constexpr (BORDER && PUB == 1) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B1_LDS_U##U));           \
+    if constexpr (BORDER && PUB == 2) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B1_GLOB_U##U));          \
+    if constexpr (!BORDER && PUB == 0) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B0_NONE_U##U));         \
+    if constexpr (!BORDER && PUB == 1) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B0_LDS_U##U));          \
+    if constexpr (!BORDER && PUB == 2) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B0_GLOB_U##U));
+    if constexpr (L && LUT) { AF2_SEL(L, 1) }
+    if constexpr (L && !LUT) { AF2_SEL(L, 0) }
+    if constexpr (!L && LUT) { AF2_SEL(G, 1) }
+    if constexpr (!L && !LUT) { AF2_SEL(G, 0) }
+#undef AF2_SEL
+    tf = make_int2(tfg, tff);
+    return st;
+}
+#undef AF2_ASM
+
 template <bool PARTIAL>
-__device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k) {
+__device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k,
+                             unsigned long long* dbg) {
     constexpr int CH = 32;
     constexpr int IRM = kSlots * CH - 1;
     constexpr int LAG = 2;   // lane 63 finishes column c at step c + 64: chunk j is complete after block j + 2
@@ -1229,18 +1343,30 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     const bool clamp = amode & 1;
     const int bestmode = (amode >> 1) & 3;
     const AffBorder B(bm, go);
+    // X space: a problem with the clamp or a best-cell output runs its
+    // asm steady state in X = H + (r+2)|ge| (a per-row shift: the clamp bound is a
+    // per-lane constant folded into E, the best cell is max X).  Its rings, hand-off
+    // rows and out_row hold X values; the C++ blocks compute in G space (X + c|ge|) and
+    // convert what they read and publish.
+    const bool xs = amode != 0;
+    auto to_g = [nge](int v, int c) { return v + c * nge; };
+    auto to_x = [nge](int v, int c) { return v - c * nge; };
     // column-block shard: the left border column (H and E of column
     // -1, H space, sender's frame + left_shift) arrives from the neighbour shard;
-    // such a band runs the masked prologue on the received values
+    // such a band runs the masked C++ prologue on the received values
     const bool shard_left = P.left_in != nullptr;
-    // VIRT (the scheme's borders): lanes left of column 0 compute virtual cells from
-    // "minus infinity" states; lane 0's top value at column -1 is (G[rb-1][-1], go),
-    // so column -1 computes G = F = go, the left border, and E at column 0 = 2 go, as
-    // the oracle's.  The prologue then runs in the asm loop.  Other borders keep the
-    // masked C++ prologue.
-    constexpr bool VIRT_OK = !PARTIAL;
-    // (not with a best-cell output: the virtual border column would count as a cell)
-    const bool virt = VIRT_OK && bm == BM_NORMAL && !shard_left && !(amode & (AM_BEST_ALL | AM_BEST_LAST));
+    // Virtual prologue: lanes left of column 0 compute virtual cells from "minus
+    // infinity" states (subject code 0xFF there matches nothing), and lane 0's top value
+    // at column -1 is the left border of the row above, so column -1 reproduces the
+    // border: NORMAL / FPAID a vertical gap paid from the corner, FFREE a continuing
+    // one, FREE_LOCAL zeros by the clamp, the -inf borders -inf.  Not for a zero left
+    // border without clamp (FREE_SEMI_OPEN / _T), nor where a finite border cell could
+    // win a last-row best (the border is no candidate there).
+    constexpr bool ASM_OK = !PARTIAL;
+    const bool zero_open = bm == BM_FREE_SEMI_OPEN || bm == BM_FREE_SEMI_T;
+    const bool finite_left = bm == BM_NORMAL || bm == BM_FFREE || bm == BM_FPAID;
+    const bool virt = ASM_OK && !shard_left && !zero_open && !(bestmode == 2 && finite_left) &&
+                      !(bestmode == 1 && !clamp) && (!clamp || k.codes) && !(k.flags & 1);
     const int rb = band * 64;
     const int row = rb + lane;
     const bool dead = row >= h;
@@ -1266,7 +1392,11 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         g = kAffNeg;
         hg = kAffNeg;
         dg = kAffNeg;
-        tf = make_int2(B.left(rb - 1, nge), rb == 0 ? B.cg + go : B.lg);
+        // (G, F-down) of the left border cell of row rb-1 (the corner for rb = 0)
+        const int tg = B.left(rb - 1, nge);
+        const int tff = (bm == BM_NORMAL || bm == BM_FPAID) ? (rb == 0 ? B.cg + go : go)
+                        : bm == BM_FFREE ? 0 : bm == BM_FREE_LOCAL ? tg + go : kAffNeg;
+        tf = make_int2(tg, bm == BM_FPAID && rb == 0 ? go : tff);
     } else {
         g = B.left(row, nge);
         hg = g + go;   // the next column's E candidate: G[r][-1] + go
@@ -1278,10 +1408,15 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     const int nblocks = nchunks + LAG;
     const int fe = w >= CH - 1 ? (w - (CH - 1)) / CH + 1 : 0;   // full blocks: 32b + 30 < w
     uint32_t seen_prod = 0, seen_sfill = 0, seen_cons = 0;
+    uint64_t ts_v = 0, te_v = 0;   // diagnostic build: steady-state start / end (s_memrealtime)
+    uint32_t ts_f = 0, nmiss = 0;  // diagnostic build: + blocks without a prefetched top row
+#ifdef ANYSEQ_STAMPS
+    uint64_t t_b0 = 0;             // diagnostic build: C++ block 0 start
+#endif
     // clamp bound far below any cell when the problem does not clamp
     const int zoff = clamp ? 0 : 2 * kAffNeg;
-    AffLoopArgs la;
-    if constexpr (VIRT_OK) {
+    Aff2Args la;
+    if constexpr (ASM_OK) {
         la.rb = lds_addr(io.my_ring);
         la.nb = io.out_lds ? lds_addr(io.next_ring) : 0u;
         la.apr = lds_addr(io.my_prod);
@@ -1293,76 +1428,83 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         la.skb = lds_addr(io.skew) + 4u * lane;
         la.lo = 8u * (lane - 32);
         la.lid8 = 8u * lane;
-        la.bvb = (uint32_t)B.top(lane, nge);
-        la.bvs = (uint32_t)(B.top(1, nge) - B.top(0, nge));
+        // band 0's top border (value, value + go) in the loop's space
+        la.bvb = (uint32_t)(xs ? to_x(B.top(lane, nge), lane) : B.top(lane, nge));
+        la.bvs = (uint32_t)(B.top(1, nge) - B.top(0, nge) - (xs ? nge : 0));
         la.gp = (uint64_t)(size_t)io.gout;
+        // diagonal weights in the loop's space: G adds sub - 2 ge, X adds sub - ge
+        const int wm = xs ? k.wm - nge : k.wm, wx = xs ? k.wx - nge : k.wx;
+        la.q = q;
+        la.wm = wm;
+        la.wx = wx;
+        uint32_t ll = 0, lh = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            ll |= (uint32_t)((q == c ? wm : wx) & 0xff) << (8 * c);
+            lh |= (uint32_t)((q == c + 4 ? wm : wx) & 0xff) << (8 * c);
+        }
+        la.ll = (int)ll;
+        la.lh = (int)lh;
+        la.zlp = clamp ? (row + 3) * nge : 2 * kAffNeg;   // X-space clamp bound - ge
     }
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
-        if constexpr (VIRT_OK) {
-            if (b == 0 && !virt && !shard_left && fe >= 2 && !(k.flags & 5)) {
-                // blocks 0, 1 in asm under a growing exec mask (no virtual lanes)
-                uint32_t zb = (uint32_t)((rb + 1) * nge);
-                uint32_t z = zb + (uint32_t)zoff;
-                const int role = (io.in_border ? 2 : 0) + (io.trailing ? 1 : 0);
-                uint32_t st = 0;
-#define AP_CALL(LV, BD, TR) \
-    st = aff_prologue_asm<LV, BD, TR>(seen_prod, seen_sfill, seen_cons, la, q, g, fdn, dg, tf, e, hg, best, z, zb, k)
-                if (amode) {
-                    switch (role) {
-                        case 0: AP_CALL(true, false, false); break;
-                        case 1: AP_CALL(true, false, true); break;
-                        case 2: AP_CALL(true, true, false); break;
-                        default: AP_CALL(true, true, true); break;
-                    }
-                } else {
-                    switch (role) {
-                        case 0: AP_CALL(false, false, false); break;
-                        case 1: AP_CALL(false, false, true); break;
-                        case 2: AP_CALL(false, true, false); break;
-                        default: AP_CALL(false, true, true); break;
-                    }
-                }
-#undef AP_CALL
-                if (st) {
-                    atomicOr(err, ERR_SPIN_TIMEOUT);
-                    return;
-                }
-                b = 1;   // ++b of the for: the steady state from block 2
-                continue;
-            }
+        if constexpr (ASM_OK) {
             if ((virt || t0 >= 64) && b < fe && !(k.flags & 1)) {
+                // one block of slack: block b starts once chunk b+1 is published, so in the
+                // steady state the loop's poll (step 16) already sees the next chunk and
+                // prefetches its top row -- no wait on the band chain's critical path
+                if (!io.in_border) {
+                    const uint32_t need = (uint32_t)min(b + 2, nchunks);
+                    if (seen_prod < need && !(seen_prod = spin_lds_ge(io.my_prod, need, err))) return;
+                }
+                // state into the loop's space: the lane's cell of step t0-1 is column t0-2-lane
+                const int cs = t0 - 2 - lane;
+                int bx = kAffNeg;
+                if (xs) {
+                    g = to_x(g, cs);
+                    hg = to_x(hg, cs);
+                    e = to_x(e, cs);
+                    fdn = to_x(fdn, cs);
+                    dg = to_x(dg, cs);
+                    tf = make_int2(to_x(tf.x, t0 - 1), to_x(tf.y, t0 - 1));
+                }
                 uint32_t bb = (uint32_t)b;
-                uint32_t zb = (uint32_t)((rb + t0 + 1) * nge);
-                uint32_t z = zb + (uint32_t)zoff;
                 const int role = (io.in_border ? 3 : 0) + (io.out_lds ? 1 : (io.gout ? 2 : 0));
                 uint32_t st = 0;
-#define AF_CALL(LV, BD, PB)                                                                                    \
-    st = aff_loop_asm<LV, BD, PB>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, q, g, fdn, dg, tf, e, \
-                                  hg, best, z, zb, k)
-                if (amode) {
-                    switch (role) {
-                        case 0: AF_CALL(true, false, 0); break;
-                        case 1: AF_CALL(true, false, 1); break;
-                        case 2: AF_CALL(true, false, 2); break;
-                        case 3: AF_CALL(true, true, 0); break;
-                        case 4: AF_CALL(true, true, 1); break;
-                        default: AF_CALL(true, true, 2); break;
-                    }
+#define AF2_CALL(LV, BD, PB, LU)                                                                               \
+    st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, fdn, \
+                                       dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss)
+#define AF2_ROLES(LV, LU)                          \
+    switch (role) {                                \
+        case 0: AF2_CALL(LV, false, 0, LU); break; \
+        case 1: AF2_CALL(LV, false, 1, LU); break; \
+        case 2: AF2_CALL(LV, false, 2, LU); break; \
+        case 3: AF2_CALL(LV, true, 0, LU); break;  \
+        case 4: AF2_CALL(LV, true, 1, LU); break;  \
+        default: AF2_CALL(LV, true, 2, LU); break; \
+    }
+                if (xs) {
+                    if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
                 } else {
-                    switch (role) {
-                        case 0: AF_CALL(false, false, 0); break;
-                        case 1: AF_CALL(false, false, 1); break;
-                        case 2: AF_CALL(false, false, 2); break;
-                        case 3: AF_CALL(false, true, 0); break;
-                        case 4: AF_CALL(false, true, 1); break;
-                        default: AF_CALL(false, true, 2); break;
-                    }
+                    if (k.lut) { AF2_ROLES(false, true) } else { AF2_ROLES(false, false) }
                 }
-#undef AF_CALL
+#undef AF2_ROLES
+#undef AF2_CALL
                 if (st) {
                     atomicOr(err, ERR_SPIN_TIMEOUT);
                     return;
+                }
+                // back to G space for the C++ epilogue; the loop's best (X) to H
+                const int t1 = (int)bb * CH, ce = t1 - 2 - lane;
+                if (xs) {
+                    g = to_g(g, ce);
+                    hg = to_g(hg, ce);
+                    e = to_g(e, ce);
+                    fdn = to_g(fdn, ce);
+                    dg = to_g(dg, ce);
+                    tf = make_int2(to_g(tf.x, t1 - 1), to_g(tf.y, t1 - 1));
+                    best = max(best, bx - (row + 2) * nge);
                 }
                 b = (int)bb - 1;   // ++b of the for
                 continue;
@@ -1377,7 +1519,8 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         if (b < nchunks) {
             if (io.in_border) {
                 const int bv = B.top(t0 + lane, nge);
-                io.my_ring[(t0 + lane) & IRM] = make_int2(bv, bv + go);
+                const int bvr = xs ? to_x(bv, t0 + lane) : bv;   // rings hold the loop's space
+                io.my_ring[(t0 + lane) & IRM] = make_int2(bvr, bvr + go);
             } else if (seen_prod < (uint32_t)(b + 1)) {
                 if (!(seen_prod = spin_lds_ge(io.my_prod, (uint32_t)(b + 1), err))) return;
             }
@@ -1387,6 +1530,10 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 const int4 v = src[i];
                 rv[2 * i] = make_int2(v.x, v.y);
                 rv[2 * i + 1] = make_int2(v.z, v.w);
+            }
+            if (xs) {
+#pragma unroll
+                for (int u = 0; u < CH; ++u) rv[u] = make_int2(to_g(rv[u].x, t0 + u), to_g(rv[u].y, t0 + u));
             }
         } else {
 #pragma unroll
@@ -1401,6 +1548,9 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
             }
         }
         int og[CH], of[CH];
+#ifdef ANYSEQ_STAMPS
+        if (b == 0) t_b0 = __builtin_amdgcn_s_memrealtime();   // block 0's inputs are ready
+#endif
         const int c0 = t0 - 1 - lane;
         const int zb = (rb + t0 + 1) * nge;
         const int zc = zb + zoff;
@@ -1420,6 +1570,14 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                                                     best, og, of, k);
         }
         tf = rv[CH - 1];
+        if (xs) {
+            // lane 63's cell of step t0+u is column t0+u-64 (the published chunk j)
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                og[u] = to_x(og[u], t0 + u - 64);
+                of[u] = to_x(of[u], t0 + u - 64);
+            }
+        }
         if (pub && lane == 63) {
             int4* dst = reinterpret_cast<int4*>(io.next_ring + ((j * CH) & IRM));
 #pragma unroll
@@ -1451,6 +1609,16 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     }
     if (!io.in_border) lds_st(io.my_cons, (uint32_t)(nchunks + kSlots));
     if (io.trailing) lds_st(io.tail, 0x7fffffffu);
+#ifdef ANYSEQ_STAMPS
+    // timeline: slot 0 = first steady-state block start, 1 = steady-state end, 2 = band end
+    if (dbg && lane == 0 && band < 2048 && ts_f) {
+        const int slot = 16 + 4 * (band + (P.q_step < 0 ? 2048 : 0));
+        dbg[slot] = ts_v;
+        dbg[slot + 1] = te_v;
+        dbg[slot + 2] = __builtin_amdgcn_s_memrealtime();
+        dbg[slot + 3] = t_b0 ? t_b0 : (uint64_t)nmiss;   // (asm path: prefetch misses)
+    }
+#endif
     if (!dead) {
         if (P.out_col) gmem(P.out_col)[row] = aff_to_h(g, row, w - 1, nge);
         if (P.out_col_e) gmem(P.out_col_e)[row] = aff_to_h(e, row, w - 1, nge);
@@ -1483,6 +1651,11 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
     k.wx = fp.mismatch + 2 * k.nge;
     k.flags = fp.pad;
     k.thr = fp.throttle;
+    // alphabet codes: *fp.alpha is the number of distinct symbols of the
+    // pair, which q / s hold as codes 0 .. n-1
+    const int nsym = fp.alpha ? __builtin_amdgcn_readfirstlane(*fp.alpha) : 0;
+    k.codes = nsym > 0 && nsym < 255;
+    k.lut = nsym > 0 && nsym <= 8 && fp.lut_ok;
     if (fp.prio && wave < NW) __builtin_amdgcn_s_setprio(3);   // compute waves before the I/O wave
     for (;;) {
         if (threadIdx.x == 0) {
@@ -1535,8 +1708,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                 io.next_prod = band < last ? &sh.prod[wave + 1] : nullptr;
                 io.next_cons = band < last ? &sh.cons[wave + 1] : nullptr;
                 io.gout = band < last ? nullptr : g_out;
-                if ((band + 1) * 64 > P.h) run_band_aff<true>(P, band, lane, io, err, k);
-                else run_band_aff<false>(P, band, lane, io, err, k);
+                if ((band + 1) * 64 > P.h) run_band_aff<true>(P, band, lane, io, err, k, fp.dbg);
+                else run_band_aff<false>(P, band, lane, io, err, k, fp.dbg);
             }
         }
         __syncthreads();
@@ -1554,7 +1727,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
 __global__ void aff_reduce_kernel(int kind, int two, const int2* __restrict__ rowF, int h1,
                                   const int2* __restrict__ rowB, int h2, int m, int go, int ge,
                                   const int32_t* __restrict__ colF, const int32_t* __restrict__ colB, int32_t* out) {
-    auto toh = [&](int v, int r, int c) { return v + (r + c + 2) * ge; };   // all kinds run in G space
+    // global / semiglobal fronts run in G space, local ones (clamp + best) in X space
+    auto toh = [&](int v, int r, int c) { return v + (r + (kind == KIND_LOCAL ? 0 : c) + 2) * ge; };
     const int NEG2 = 2 * kAffNeg;
     int best = kind == KIND_SEMIGLOBAL ? 0 : -2147483647;
     const int tid = threadIdx.x + blockIdx.x * blockDim.x, nth = blockDim.x * gridDim.x;
@@ -1681,7 +1855,8 @@ __global__ void shard_aff_combine_kernel(int kind, const int2* __restrict__ rowT
                                          const int32_t* __restrict__ lBf, int sB, int last,
                                          const int32_t* __restrict__ colT, const int32_t* __restrict__ colB, int adj,
                                          int32_t* out) {
-    auto toh = [&](int v, int r, int c) { return v + (r + c + 2) * ge; };
+    // global / semiglobal fronts run in G space, local ones (clamp + best) in X space
+    auto toh = [&](int v, int r, int c) { return v + (r + (kind == KIND_LOCAL ? 0 : c) + 2) * ge; };
     const int NEG2 = 2 * kAffNeg;
     int best = kind == KIND_SEMIGLOBAL ? 0 : -2147483647;
     const int bt = kind == KIND_GLOBAL ? go + h1 * ge : 0;   // H[h1-1][-1] of the whole matrix
@@ -2180,12 +2355,14 @@ struct RowToCol {
     int32_t* E;
     int32_t n;      // columns of the transposed problem (rows of the original)
     int32_t hlast;  // last row of the transposed problem
+    int32_t xs;     // the row holds X-space values (DPProblem::amode != 0)
+    int32_t pad_;
 };
 __global__ void aff_row_to_col_kernel(const RowToCol* __restrict__ jobs, int nge) {
     const RowToCol J = jobs[blockIdx.y];
     for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < J.n; c += blockDim.x * gridDim.x) {
         const int2 v = J.row[c];
-        const int z = (J.hlast + c + 2) * nge;
+        const int z = (J.hlast + (J.xs ? 0 : c) + 2) * nge;
         J.H[c] = v.x - z;
         J.E[c] = v.y - z;
     }
@@ -2515,6 +2692,105 @@ __global__ __launch_bounds__(256) void fill_prep_kernel(uint32_t* zero, int nzer
     for (size_t i = tid; i < nsent; i += nth) sent[i] = v;
 }
 }  // namespace anyseq
+
+// Alphabet codes of a sequence pair.  The affine fill compares codes,
+// which are equal iff the bytes are (raw byte equality, align.impala:130-133); with at
+// most 8 distinct symbols its steady state reads the diagonal weights of 4 steps from a
+// per-lane table with one v_perm_b32.  Code 0xFF is never a code of a pair with fewer
+// than 255 symbols: the virtual prologue's columns left of 0 use it.
+namespace anyseq {
+__global__ __launch_bounds__(256) void seq_presence_kernel(const uint8_t* __restrict__ q, int n,
+                                                           const uint8_t* __restrict__ s, int m, uint32_t* mask) {
+    __shared__ uint32_t sm[8];
+    if (threadIdx.x < 8) sm[threadIdx.x] = 0;
+    __syncthreads();
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    const size_t total = (size_t)n + (size_t)m;
+    for (size_t i = tid; i < total; i += nth) {
+        const uint32_t b = i < (size_t)n ? q[i] : s[i - n];
+        const uint32_t bit = 1u << (b & 31);
+        // (a repeated symbol only reads: the first lanes of a symbol set its bit)
+        if (!(__hip_atomic_load(&sm[b >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bit))
+            atomicOr(&sm[b >> 5], bit);
+    }
+    __syncthreads();
+    if (threadIdx.x < 8 && sm[threadIdx.x]) atomicOr(&mask[threadIdx.x], sm[threadIdx.x]);
+}
+// One block of 256: code(byte) = rank of the byte among the present bytes; alpha[0] =
+// number of symbols.
+__global__ __launch_bounds__(256) void seq_code_kernel(const uint32_t* __restrict__ mask, uint8_t* table,
+                                                       int32_t* alpha) {
+    const int t = threadIdx.x;
+    const uint32_t w = mask[t >> 5];
+    int rank = __popc(w & ((1u << (t & 31)) - 1u));
+    for (int k = 0; k < (t >> 5); ++k) rank += __popc(mask[k]);
+    table[t] = ((w >> (t & 31)) & 1u) ? (uint8_t)rank : (uint8_t)0xfe;
+    if (t == 0) {
+        int tot = 0;
+        for (int k = 0; k < 8; ++k) tot += __popc(mask[k]);
+        *alpha = tot;
+    }
+}
+// q ++ s -> their codes (one buffer of n + m bytes); clears the presence mask for the
+// next pair.
+__global__ __launch_bounds__(256) void seq_recode_kernel(const uint8_t* __restrict__ q, int n,
+                                                         const uint8_t* __restrict__ s, int m,
+                                                         const uint8_t* __restrict__ table, uint8_t* out,
+                                                         uint32_t* mask) {
+    __shared__ uint8_t tb[256];
+    tb[threadIdx.x] = table[threadIdx.x];
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < 8) mask[threadIdx.x] = 0u;
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    const size_t total = (size_t)n + (size_t)m;
+    for (size_t i = tid; i < total; i += nth) out[i] = tb[i < (size_t)n ? q[i] : s[i - n]];
+}
+}  // namespace anyseq
+
+hipError_t anyseq_launch_seq_codes(const uint8_t* q, int n, const uint8_t* s, int m, uint32_t* mask, uint8_t* table,
+                                   int32_t* alpha, uint8_t* out, hipStream_t st) {
+    const size_t total = (size_t)n + (size_t)m;
+    const int blocks = (int)std::max<size_t>(1, std::min<size_t>(1024, (total + 4095) / 4096));
+    hipLaunchKernelGGL(anyseq::seq_presence_kernel, dim3(blocks), dim3(256), 0, st, q, n, s, m, mask);
+    hipLaunchKernelGGL(anyseq::seq_code_kernel, dim3(1), dim3(256), 0, st, mask, table, alpha);
+    hipLaunchKernelGGL(anyseq::seq_recode_kernel, dim3(blocks), dim3(256), 0, st, q, n, s, m, table, out, mask);
+    return hipGetLastError();
+}
+
+// Emulated ranks of the sharded construct (local mode): the views'
+// level columns / best cells reduced over the views in place (op 0 SUM, 1 MAX), as the
+// RCCL all-reduce does across processes; strings merged by a byte-wise MAX.
+namespace anyseq {
+__global__ void view_reduce_i32_kernel(int32_t* base, size_t stride, int nviews, size_t n, int op) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        int32_t a = base[i];
+        for (int v = 1; v < nviews; ++v) {
+            const int32_t x = base[(size_t)v * stride + i];
+            a = op ? max(a, x) : a + x;
+        }
+        for (int v = 0; v < nviews; ++v) base[(size_t)v * stride + i] = a;
+    }
+}
+__global__ void view_max_u8_kernel(uint8_t* dst, const uint8_t* others, size_t stride, int nothers, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint8_t a = dst[i];
+        for (int v = 0; v < nothers; ++v) a = max(a, others[(size_t)v * stride + i]);
+        dst[i] = a;
+    }
+}
+}  // namespace anyseq
+
+hipError_t anyseq_launch_view_reduce_i32(int32_t* base, size_t stride, int nviews, size_t n, int op, hipStream_t st) {
+    const int blocks = (int)std::max<size_t>(1, std::min<size_t>(1024, (n + 255) / 256));
+    hipLaunchKernelGGL(anyseq::view_reduce_i32_kernel, dim3(blocks), dim3(256), 0, st, base, stride, nviews, n, op);
+    return hipGetLastError();
+}
+hipError_t anyseq_launch_view_max_u8(uint8_t* dst, const uint8_t* others, size_t stride, int nothers, size_t n,
+                                     hipStream_t st) {
+    const int blocks = (int)std::max<size_t>(1, std::min<size_t>(1024, (n + 255) / 256));
+    hipLaunchKernelGGL(anyseq::view_max_u8_kernel, dim3(blocks), dim3(256), 0, st, dst, others, stride, nothers, n);
+    return hipGetLastError();
+}
 
 // In-process sharded transport: one kernel per chunk copies the chunk's H rows (and
 // affine E rows) into the neighbour's left column, then sets the chunk's ready

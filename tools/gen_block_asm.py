@@ -317,7 +317,7 @@ ASK0, ASK1 = 196, 204       # subject words, double buffered
 AVT, AVT2, AVA, AVB = 212, 213, 214, 215
 
 
-def gen_loop_aff(kind, border, pub):
+def gen_loop_aff(kind, border, pub, ts=False):
     """Affine (Gotoh, G-space) steady-state loop over full blocks b .. be-1 of a
     band; same LDS protocol as gen_loop2 with (G, F) pairs in the rings.
     Per step (kind G: global / semiglobal; L: local adds the clamp and the best):
@@ -370,6 +370,14 @@ def gen_loop_aff(kind, border, pub):
             throttle(e, k)
         else:
             wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=AVT2)
+        if ts:
+            # diagnostic build: the time the band's first steady-state block starts
+            e("s_cmp_lg_u32 %[tsf], 0")
+            e(f"s_cbranch_scc1 L_nots{k}_%=")
+            e("s_memrealtime %[ts]")
+            e("s_waitcnt lgkmcnt(0)")
+            e("s_mov_b32 %[tsf], 1")
+            e(f"L_nots{k}_%=:")
         if pub == "lds":
             e("s_cmp_lt_u32 %[b], 17")
             e(f"s_cbranch_scc1 L_nobp{k}_%=")
@@ -483,6 +491,9 @@ def gen_loop_aff(kind, border, pub):
     e("s_cmp_lt_u32 %[b], %[be]")
     e("s_cbranch_scc1 L_top_%=")
     e("L_done_%=:")
+    if ts:
+        e("s_memrealtime %[te]")
+        e("s_waitcnt lgkmcnt(0)")
     e("s_mov_b32 %[st], 0")
     e("s_branch L_end_%=")
     e("L_timeout_%=:")
@@ -599,6 +610,254 @@ def gen_prologue_aff(kind, border, trailing):
     return out
 
 
+
+# ------------------------------------------------------- affine, round 3 --
+# Registers of gen_aff2 (TOP pairs / cell pairs as gen_loop_aff).
+B_AW, B_AA, B_AT, B_AP = 192, 193, 194, 195   # cmp weight, diag + weight, temp, poll result
+B_SK0, B_SK1 = 196, 204                          # subject words (codes), double buffered
+B_VT, B_VT2, B_VA, B_VB = 212, 213, 214, 215    # temps / LDS addresses
+B_WB = 216                                       # LUT weight bytes of 4 steps
+
+
+def gen_aff2(kind, border, pub, lut, ts=False):
+    """Affine steady-state loop, round 3: full blocks b .. be-1.
+    kind G: G space (X_G = X + (r+c+2)|ge|), no clamp, no best (amode 0).
+    kind L: X space (X = H + (r+2)|ge|, a per-ROW shift): the local clamp H >= 0 is
+            X >= zl, a per-lane constant, folded into the E update
+            (E' = max3(E, X_left + go, zl - ge) + ge keeps E' = max(E, 0)), and the
+            best cell is max X per lane (H = X - (r+2)|ge| after the loop): no
+            per-step offset, no SALU in the step.
+    lut: the diagonal weight of 4 steps from ONE v_perm_b32 of the lane's 8-entry
+         weight table (query code against subject codes 0..7; code 0xFF -> -1)
+         and a byte-select SDWA add; else v_cmp + v_cndmask (any codes).
+    Per block: the top row's second half is read at the block start, the first
+    half was prefetched in the previous block (when the producer's counter, polled
+    at step 16, already covered the next chunk: bands start one block later than
+    the structural minimum, so in the steady state no poll waits); subject codes of
+    the next block at step 8; publishing as gen_loop_aff (shift register)."""
+    L = kind == "L"
+    trailing = pub != "lds"
+    out = []
+    e = out.append
+    sets = (B_SK0, B_SK1)
+
+    def top_reads(first, dst_b):
+        """8 ds_read_b128 of top-row pairs [16*first, 16*first+16) of block dst_b
+        (register x2 = dst_b's ring byte offset already in VB)."""
+        for i in range(8):
+            reg = AT0 + 32 * first + 4 * i
+            e(f"ds_read_b128 v[{reg}:{reg + 3}], v{B_VB} offset:{128 * first + 16 * i}")
+
+    def ring_addr(breg):
+        # ring byte address of chunk `breg` into VB: rb + ((breg << 8) & 4095)
+        e(f"s_lshl_b32 %[x2], {breg}, 8")
+        e("s_and_b32 %[x2], %[x2], 4095")
+        e("s_add_u32 %[x2], %[x2], %[rb]")
+        e(f"v_mov_b32_e32 v{B_VB}, %[x2]")
+
+    def border_write(breg):
+        # band 0: lanes write the top border (value, value + go) of columns 32*breg + lane
+        e(f"s_lshl_b32 %[x0], {breg}, 5")
+        e("s_mul_i32 %[x2], %[x0], %[bvs]")
+        e(f"v_add_u32_e32 v{B_VT}, %[x2], %[bvb]")
+        e(f"v_add_u32_e32 v{B_VT2}, %[go], v{B_VT}")
+        e("s_lshl_b32 %[x2], %[x0], 3")
+        e(f"v_add_u32_e32 v{B_VA}, %[x2], %[lid8]")
+        e(f"v_and_b32_e32 v{B_VA}, 0xfff, v{B_VA}")
+        e(f"v_add_u32_e32 v{B_VA}, %[rb], v{B_VA}")
+        e(f"ds_write_b64 v{B_VA}, v[{B_VT}:{B_VT2}]")
+
+    def body(k):
+        cs, ns = sets[k], sets[1 - k]
+        e("s_add_u32 %[x1], %[b], 1")
+        # ---- this block's top row
+        e("s_cmp_eq_u32 %[pf], 0")
+        e(f"s_cbranch_scc0 L_pfd{k}_%=")
+        if ts:
+            e("s_add_u32 %[nmiss], %[nmiss], 1")   # diagnostic: blocks whose top row was not prefetched
+        if border:
+            border_write("%[b]")
+            e("s_waitcnt lgkmcnt(0)")
+        else:
+            wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=B_VT2)
+        ring_addr("%[b]")
+        top_reads(0, "%[b]")
+        e(f"L_pfd{k}_%=:")
+        ring_addr("%[b]")
+        top_reads(1, "%[b]")
+        e("s_mov_b32 %[pf], 0")
+        if ts:
+            e("s_cmp_lg_u32 %[tsf], 0")
+            e(f"s_cbranch_scc1 L_nots{k}_%=")
+            e("s_memrealtime %[ts]")
+            e("s_waitcnt lgkmcnt(0)")
+            e("s_mov_b32 %[tsf], 1")
+            e(f"L_nots{k}_%=:")
+        if pub == "lds":
+            # the next band's ring slot of chunk b-2 is free once it consumed chunk b-17
+            e("s_cmp_lt_u32 %[b], 17")
+            e(f"s_cbranch_scc1 L_nobp{k}_%=")
+            e("s_sub_u32 %[x4], %[b], 17")
+            wait(e, f"bp{k}", "%[sc]", "%[x4]", "%[anc]", tmp=B_VT2)
+            e(f"L_nobp{k}_%=:")
+        g, f, dg = "%[cur]", "%[fd]", "%[dg]"
+        issued_s = False
+        issued_p = False
+        for u in range(32):
+            if u == 8:
+                # next block's subject codes (other register set) and, band 0, its border.
+                # The reads are issued in every block (after the last one they read a stale
+                # slot, unused): the counted lgkmcnt waits below assume they are in flight.
+                e("s_cmp_ge_u32 %[x1], %[be]")
+                e(f"s_cbranch_scc1 L_nopf{k}_%=")
+                e("s_add_u32 %[x4], %[b], 2")
+                wait(e, f"sf{k}", "%[sf]", "%[x4]", "%[asf]", tmp=B_VT2)
+                e(f"L_nopf{k}_%=:")
+                e("s_and_b32 %[x2], %[x1], 31")
+                e("s_lshl_b32 %[x2], %[x2], 11")
+                e(f"v_add_u32_e32 v{B_VA}, %[x2], %[skb]")
+                for i in range(4):
+                    e(f"ds_read2st64_b32 v[{ns + 2 * i}:{ns + 2 * i + 1}], v{B_VA} offset0:{2 * i} offset1:{2 * i + 1}")
+                if border:
+                    border_write("%[x1]")
+                issued_s = True
+            if u == 16 and not border:
+                # poll the producer's counter for the next chunk (result used at step 24)
+                e(f"ds_read_b32 v{B_AP}, %[apr]")
+                issued_p = True
+            if u == 24:
+                e("s_waitcnt lgkmcnt(0)")
+                e("s_cmp_ge_u32 %[x1], %[be]")
+                e(f"s_cbranch_scc1 L_noq{k}_%=")
+                if not border:
+                    e(f"v_readfirstlane_b32 %[x2], v{B_AP}")
+                    e("s_max_u32 %[sp], %[sp], %[x2]")
+                    e("s_add_u32 %[x4], %[b], 2")
+                    e("s_cmp_ge_u32 %[sp], %[x4]")
+                    e(f"s_cbranch_scc0 L_noq{k}_%=")
+                ring_addr("%[x1]")
+                top_reads(0, "%[x1]")
+                e("s_mov_b32 %[pf], 1")
+                e(f"L_noq{k}_%=:")
+            if 1 <= u <= 23 and u % 2 == 1:
+                ns_ = (5 if border else 4) if issued_s else 0   # subject reads (+ border write)
+                if u <= 15:
+                    i = (u + 1) // 2                       # first-half read holding T(u-1)
+                    allowed = (8 - i) + 8 + ns_
+                else:
+                    i = (u - 15) // 2                      # second-half read holding T(u-1)
+                    allowed = (8 - i) + ns_ + (1 if issued_p else 0)
+                e(f"s_waitcnt lgkmcnt({min(15, allowed)})")
+            sw = v(cs + u // 4)
+            tg = "%[tfg]" if u == 0 else TG_(u - 1)
+            tf = "%[tff]" if u == 0 else TF_(u - 1)
+            if lut:
+                if u % 4 == 0:
+                    e(f"v_perm_b32 v{B_WB}, %[lh], %[ll], {sw}")
+                e(f"v_add_u32_sdwa v{B_AA}, {dg}, sext(v{B_WB}) dst_sel:DWORD dst_unused:UNUSED_PAD "
+                  f"src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+            else:
+                e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+                e(f"v_cndmask_b32_e32 v{B_AW}, %[wx], %[wm], vcc")
+                e(f"v_add_u32_e32 v{B_AA}, {dg}, v{B_AW}")
+            if L:
+                e("v_max3_i32 %[e], %[e], %[hg], %[zlp]")
+                e("v_add_u32_e32 %[e], %[ge], %[e]")
+            else:
+                e("v_max_i32_e32 %[e], %[e], %[hg]")
+            e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_max3_i32 {OG_(u)}, v{B_AA}, %[e], {tf}")
+            e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
+            e(f"v_max_i32_e32 {OF_(u)}, {tf}, %[hg]")
+            if L and u % 2 == 1:
+                e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
+            if u >= 2 and pub != "none":
+                e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            g, f, dg = OG_(u), OF_(u), tg
+        e(f"v_mov_b32_e32 %[cur], {OG_(31)}")
+        e(f"v_mov_b32_e32 %[fd], {OF_(31)}")
+        e(f"v_mov_b32_e32 %[dg], {TG_(30)}")
+        if pub != "none":
+            e(f"v_mov_b32_dpp {OG_(31)}, {OG_(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_mov_b32_dpp {OF_(31)}, {OF_(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+        e(f"v_mov_b32_e32 %[tfg], {TG_(31)}")
+        e(f"v_mov_b32_e32 %[tff], {TF_(31)}")
+        if pub != "none":
+            e("s_cmp_lt_u32 %[b], 2")
+            e(f"s_cbranch_scc1 L_nopub{k}_%=")
+            e("s_sub_u32 %[x2], %[b], 2")
+            e("s_lshl_b32 %[x2], %[x2], 8")
+            if pub == "lds":
+                e("s_and_b32 %[x2], %[x2], 4095")
+                e("s_add_u32 %[x2], %[x2], %[nb]")
+            e(f"v_add_u32_e32 v{B_VT}, %[x2], %[lo]")
+            e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
+            e("s_mov_b64 exec, %[hm]")
+            if pub == "lds":
+                e(f"ds_write_b64 v{B_VT}, v[{AO0 + 62}:{AO0 + 63}]")
+            else:
+                e(f"global_store_dwordx2 v{B_VT}, v[{AO0 + 62}:{AO0 + 63}], %[gp] sc1")
+            e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
+            if pub == "lds":
+                e("s_sub_u32 %[x2], %[b], 1")
+                e(f"v_mov_b32_e32 v{B_VT2}, %[x2]")
+                e(f"ds_write_b32 %[anp], v{B_VT2}")
+            e(f"L_nopub{k}_%=:")
+        e(f"v_mov_b32_e32 v{B_VT2}, %[x1]")
+        if not border:
+            e(f"ds_write_b32 %[acn], v{B_VT2}")
+        if trailing:
+            e(f"ds_write_b32 %[atl], v{B_VT2}")
+        e("s_mov_b32 %[b], %[x1]")
+
+    # the first block's subject codes into set 0
+    e("s_add_u32 %[x1], %[b], 1")
+    wait(e, "sfp", "%[sf]", "%[x1]", "%[asf]", tmp=B_VT2)
+    e("s_and_b32 %[x2], %[b], 31")
+    e("s_lshl_b32 %[x2], %[x2], 11")
+    e(f"v_add_u32_e32 v{B_VA}, %[x2], %[skb]")
+    for i in range(4):
+        e(f"ds_read2st64_b32 v[{B_SK0 + 2 * i}:{B_SK0 + 2 * i + 1}], v{B_VA} offset0:{2 * i} offset1:{2 * i + 1}")
+    e("s_waitcnt lgkmcnt(0)")
+    e("L_top_%=:")
+    body(0)
+    e("s_cmp_lt_u32 %[b], %[be]")
+    e("s_cbranch_scc0 L_done_%=")
+    body(1)
+    e("s_cmp_lt_u32 %[b], %[be]")
+    e("s_cbranch_scc1 L_top_%=")
+    e("L_done_%=:")
+    e("s_waitcnt lgkmcnt(0)")
+    if ts:
+        e("s_memrealtime %[te]")
+        e("s_waitcnt lgkmcnt(0)")
+    e("s_mov_b32 %[st], 0")
+    e("s_branch L_end_%=")
+    e("L_timeout_%=:")
+    e("s_waitcnt lgkmcnt(0)")
+    e("s_mov_b32 %[st], 1")
+    e("L_end_%=:")
+    return out
+
+
+def TG_(u):
+    return v(AT0 + 2 * u)
+
+
+def TF_(u):
+    return v(AT0 + 2 * u + 1)
+
+
+def OG_(u):
+    return v(AO0 + 2 * u)
+
+
+def OF_(u):
+    return v(AO0 + 2 * u + 1)
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
     dst = os.path.join(here, "..", "anyseq_amd", "csrc", "anyseq_block_asm.inc")
@@ -628,11 +887,22 @@ def main():
     for kind in ("G", "L"):
         for border in (0, 1):
             for pub in ("none", "lds", "glob"):
-                name = f"ANYSEQ_AFF_{kind}_B{border}_{pub.upper()}"
-                lines.append(f"#define {name} \\")
-                for ln in gen_loop_aff(kind, border, pub):
-                    lines.append(f'    "{ln}\\n" \\')
-                lines.append("")
+                for ts in (False, True):
+                    name = f"ANYSEQ_AFF_{kind}_B{border}_{pub.upper()}" + ("_TS" if ts else "")
+                    lines.append(f"#define {name} \\")
+                    for ln in gen_loop_aff(kind, border, pub, ts):
+                        lines.append(f'    "{ln}\\n" \\')
+                    lines.append("")
+    for kind in ("G", "L"):
+        for border in (0, 1):
+            for pub in ("none", "lds", "glob"):
+                for lut in (0, 1):
+                    for ts in (False, True):
+                        name = f"ANYSEQ_AF2_{kind}_B{border}_{pub.upper()}_U{lut}" + ("_TS" if ts else "")
+                        lines.append(f"#define {name} \\")
+                        for ln in gen_aff2(kind, border, pub, lut, ts):
+                            lines.append(f'    "{ln}\\n" \\')
+                        lines.append("")
     for kind in ("G", "L"):
         for border in (0, 1):
             for trailing in (0, 1):
@@ -644,6 +914,8 @@ def main():
     clob = ", ".join(f'"v{n}"' for n in range(AT0, AVB + 1))
     sclob = ", ".join(f'"s{n}"' for n in range(TA, TB + 2))
     lines.append(f"#define ANYSEQ_AFF_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
+    clob = ", ".join(f'"v{n}"' for n in range(AT0, B_WB + 1))
+    lines.append(f"#define ANYSEQ_AF2_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, A + 1))
     lines.append(f"#define ANYSEQ_BLOCK_ASM_CLOBBERS {clob}, \"vcc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, SKB_ + 8))
