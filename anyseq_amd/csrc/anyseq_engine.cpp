@@ -290,6 +290,7 @@ void init_tuning_locked() {
     g_tuning.NWa = env_int("ANYSEQ_NWA", g_tuning.NWa);
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
+    g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
     g_tuning_init = true;
 }
 
@@ -456,6 +457,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     fpl.epoch = epoch;
     fpl.prio = g_tuning.prio;
     fpl.throttle = g_tuning.thr;
+    fpl.slack = g_tuning.slack;
     unsigned long long* dbg = nullptr;
     static DevBuf stamp_buf;
     if (getenv("ANYSEQ_STAMPS")) {
@@ -1634,6 +1636,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "priority") g_tuning.prio = value;
     else if (n == "throttle") g_tuning.thr = value;
     else if (n == "affine_lut") g_tuning.afflut = value;
+    else if (n == "slack") g_tuning.slack = value;
     else return -1;
     return 0;
 }

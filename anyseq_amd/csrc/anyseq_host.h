@@ -90,6 +90,7 @@ struct Tuning {
     int prio = 0;        // compute waves at s_setprio 3 (the I/O wave stays at 0)
     int thr = 0;         // band 0 of every problem sleeps thr s_sleep-1 units per block (chain pace)
     int afflut = 1;      // affine fill: v_perm weight table when the pair has <= 8 symbols
+    int slack = 1;       // affine fill: blocks a band starts behind the structural minimum
 };
 extern Tuning g_tuning;
 

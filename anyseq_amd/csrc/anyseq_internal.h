@@ -133,7 +133,7 @@ struct FillParams {
     // of both value spaces fit int8 (the v_perm weight table).
     const int32_t* alpha;
     int32_t lut_ok;
-    int32_t pad2_;
+    int32_t slack;                    // affine: blocks a band starts behind the structural minimum (>= 0)
 };
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).

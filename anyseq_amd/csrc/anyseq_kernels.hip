@@ -793,16 +793,19 @@ struct HandOff<int2> {
 template <int CH, bool SKEW, typename T = int32_t>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
                         uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
-                        uint32_t* cons0, uint32_t* err, bool reset_in = false) {
+                        uint32_t* cons0, uint32_t* err, bool reset_in = false, int ext = 0) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
     const int nchunks = (w + CH - 1) / CH;
+    // ext: skewed blocks staged past the last chunk (the affine asm epilogue's), whose
+    // columns >= w all hold code 0xFF
+    const int nskew = nchunks + ext;
     const bool need_in = g_in != nullptr;
     const GLOBAL_AS uint8_t* sg = gmem(s);
     int s_next = 0, sk_next = 0, in_next = 0;
     uint32_t idle = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    while (s_next < nchunks || (SKEW && sk_next < nchunks) || (need_in && in_next < nchunks)) {
+    while (s_next < nchunks || (SKEW && sk_next < nskew) || (need_in && in_next < nchunks)) {
         bool progress = false;
         if (s_next < nchunks) {
             const uint32_t tl = lds_ld(tail);
@@ -832,24 +835,28 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                 progress = true;
             }
         }
-        if (SKEW && sk_next < s_next) {
+        const int sk_avail = s_next >= nchunks ? nskew : s_next;
+        if (SKEW && sk_next < sk_avail) {
             // skewed copy of block b needs raw columns 32b-64 .. 32b+31 (staged: b < s_next)
             // and a free slot: the trailing wave has finished block b - kSkewBlocks
             const uint32_t tl = lds_ld(tail);
-            int lim = min(s_next, tl >= 0x7fffffffu ? nchunks : (int)tl + kSkewBlocks);
+            int lim = min(sk_avail, tl >= 0x7fffffffu ? nskew : (int)tl + kSkewBlocks);
             lim = min(lim, sk_next + 8);
             for (int b = sk_next; b < lim; ++b) {
                 uint32_t d[8];
                 load_sbytes<32>(s_ring, (32 * b - 1 - lane) & (kSRing - 1), d);
                 // columns left of 0 (virtual prologue lanes): code 0xFF, which matches no
-                // query code (the LUT weight of 0xFF is -1)
+                // query code (the LUT weight of 0xFF is -1); so are the
+                // columns >= w of the epilogue's blocks
                 const int cneg = 32 * b - 1 - lane;
-                if (cneg < 0) {
+                if (cneg < 0 || (ext && cneg + 31 >= w)) {
 #pragma unroll
                     for (int i = 0; i < 8; ++i)
 #pragma unroll
-                        for (int kb = 0; kb < 4; ++kb)
-                            if (cneg + 4 * i + kb < 0) d[i] |= 0xffu << (8 * kb);
+                        for (int kb = 0; kb < 4; ++kb) {
+                            const int c = cneg + 4 * i + kb;
+                            if (c < 0 || (ext && c >= w)) d[i] |= 0xffu << (8 * kb);
+                        }
                 }
                 uint32_t* dst = skew + (b % kSkewBlocks) * 8 * 64 + lane;
 #pragma unroll
@@ -1050,6 +1057,7 @@ struct AffK {
     int thr;      // FillParams::throttle
     bool codes;   // q / s hold alphabet codes (0xFF never a code): the virtual prologue may clamp
     bool lut;     // codes 0..7 and int8 weights: the v_perm weight table
+    int slack;    // FillParams::slack
 };
 
 // Borders of a problem in G space (H border values by border mode, see
@@ -1140,125 +1148,6 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
     }
 }
 
-// Steady-state blocks b .. be-1 of a band (tools/gen_block_asm.py, gen_loop_aff),
-// specialised by role like band_loop_asm.  Returns 0, or 1 on a spin timeout.
-struct AffLoopArgs {
-    uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs;
-    uint64_t gp;
-};
-#ifdef ANYSEQ_STAMPS   // diagnostic build: first steady block start / loop end times
-#define AFF_LOOP_NAME(NAME) NAME##_TS
-#define AFF_TS_OUT , [ts] "+s"(ts_v), [te] "+s"(te_v), [tsf] "+s"(ts_f)
-#else
-#define AFF_LOOP_NAME(NAME) NAME
-#define AFF_TS_OUT
-#endif
-#define AFF_ASM_TS(NAME)                                                                                        \
-    asm volatile(NAME                                                                                          \
-                 : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
-                   [hg] "+v"(hg), [best] "+v"(best), [z] "+s"(z), [zb] "+s"(zb), [b] "+s"(b), [sp] "+s"(sp),     \
-                   [sf] "+s"(sf), [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), \
-                   [x3] "=&s"(x3), [x4] "=&s"(x4) AFF_TS_OUT                                                   \
-                 : [be] "s"(be), [q] "v"(q), [wm] "v"(k.wm), [wx] "v"(k.wx), [go] "v"(k.go), [nge] "s"(nge),     \
-                   [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp),          \
-                   [anc] "v"(la.anc), [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo),  \
-                   [lid8] "v"(la.lid8), [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp),           \
-                   [thr] "s"(thr)                                                                              \
-                 : ANYSEQ_AFF_ASM_CLOBBERS, "memory")
-#define AFF_ASM(NAME)                                                                                           \
-    asm volatile(NAME                                                                                          \
-                 : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
-                   [hg] "+v"(hg), [best] "+v"(best), [z] "+s"(z), [zb] "+s"(zb), [b] "+s"(b), [sp] "+s"(sp),     \
-                   [sf] "+s"(sf), [sc] "+s"(sc), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), \
-                   [x3] "=&s"(x3), [x4] "=&s"(x4)                                                              \
-                 : [be] "s"(be), [q] "v"(q), [wm] "v"(k.wm), [wx] "v"(k.wx), [go] "v"(k.go), [nge] "s"(nge),     \
-                   [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(la.apr), [acn] "v"(la.acn), [anp] "v"(la.anp),          \
-                   [anc] "v"(la.anc), [asf] "v"(la.asf), [atl] "v"(la.atl), [skb] "v"(la.skb), [lo] "v"(la.lo),  \
-                   [lid8] "v"(la.lid8), [bvb] "v"(la.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp),           \
-                   [thr] "s"(thr)                                                                              \
-                 : ANYSEQ_AFF_ASM_CLOBBERS, "memory")
-// L: the clamp + best loop (any amode != 0), else the plain loop.
-template <bool L, bool BORDER, int PUB>
-__device__ __forceinline__ uint32_t aff_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
-                                                 const AffLoopArgs& la, int q, int& g, int& fdn, int& dg, int2& tf,
-                                                 int& e, int& hg, int& best, uint32_t& z, uint32_t& zb, const AffK& k,
-                                                 uint64_t& ts_v, uint64_t& te_v, uint32_t& ts_f) {
-    uint32_t st, x0, x1, x2, x3, x4;
-    const uint64_t hm = 0xffffffff00000000ull;
-#define RFL(x) __builtin_amdgcn_readfirstlane(x)
-    b = RFL(b);
-    sp = RFL(sp);
-    sf = RFL(sf);
-    sc = RFL(sc);
-    be = RFL(be);
-    z = RFL(z);
-    zb = RFL(zb);
-    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), nge = RFL(k.nge), thr = RFL((uint32_t)k.thr);
-    const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
-#undef RFL
-    int tfg = tf.x, tff = tf.y;
-#ifdef ANYSEQ_STAMPS
-    ts_f = __builtin_amdgcn_readfirstlane(ts_f);
-    ts_v = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ts_v >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ts_v);
-    te_v = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(te_v >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)te_v);
-#else
-    (void)ts_v, (void)te_v, (void)ts_f;
-#endif
-    if constexpr (L) {
-        if constexpr (BORDER && PUB == 0) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B1_NONE));
-        if constexpr (BORDER && PUB == 1) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B1_LDS));
-        if constexpr (BORDER && PUB == 2) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B1_GLOB));
-        if constexpr (!BORDER && PUB == 0) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B0_NONE));
-        if constexpr (!BORDER && PUB == 1) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B0_LDS));
-        if constexpr (!BORDER && PUB == 2) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_L_B0_GLOB));
-    } else {
-        if constexpr (BORDER && PUB == 0) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B1_NONE));
-        if constexpr (BORDER && PUB == 1) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B1_LDS));
-        if constexpr (BORDER && PUB == 2) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B1_GLOB));
-        if constexpr (!BORDER && PUB == 0) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B0_NONE));
-        if constexpr (!BORDER && PUB == 1) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B0_LDS));
-        if constexpr (!BORDER && PUB == 2) AFF_ASM_TS(AFF_LOOP_NAME(ANYSEQ_AFF_G_B0_GLOB));
-    }
-    tf = make_int2(tfg, tff);
-    return st;
-}
-
-// Blocks 0 and 1 of a band without virtual lanes (tools/gen_block_asm.py,
-// gen_prologue_aff): the steady-state steps under a growing exec mask.
-template <bool L, bool BORDER, bool TRAIL>
-__device__ __forceinline__ uint32_t aff_prologue_asm(uint32_t& sp, uint32_t& sf, uint32_t& sc,
-                                                     const AffLoopArgs& la, int q, int& g, int& fdn, int& dg,
-                                                     int2& tf, int& e, int& hg, int& best, uint32_t& z, uint32_t& zb,
-                                                     const AffK& k) {
-    uint32_t st, x0, x1, x2, x3, x4, b = 0, be = 2;
-    const uint64_t hm = 0xffffffff00000000ull;
-#define RFL(x) __builtin_amdgcn_readfirstlane(x)
-    sp = RFL(sp);
-    sf = RFL(sf);
-    sc = RFL(sc);
-    z = RFL(z);
-    zb = RFL(zb);
-    const uint32_t rb = RFL(la.rb), nb = RFL(la.nb), bvs = RFL(la.bvs), nge = RFL(k.nge), thr = 0;
-    const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(la.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)la.gp);
-#undef RFL
-    int tfg = tf.x, tff = tf.y;
-    if constexpr (L) {
-        if constexpr (BORDER && TRAIL) AFF_ASM(ANYSEQ_AFFP_L_B1_T1);
-        if constexpr (BORDER && !TRAIL) AFF_ASM(ANYSEQ_AFFP_L_B1_T0);
-        if constexpr (!BORDER && TRAIL) AFF_ASM(ANYSEQ_AFFP_L_B0_T1);
-        if constexpr (!BORDER && !TRAIL) AFF_ASM(ANYSEQ_AFFP_L_B0_T0);
-    } else {
-        if constexpr (BORDER && TRAIL) AFF_ASM(ANYSEQ_AFFP_G_B1_T1);
-        if constexpr (BORDER && !TRAIL) AFF_ASM(ANYSEQ_AFFP_G_B1_T0);
-        if constexpr (!BORDER && TRAIL) AFF_ASM(ANYSEQ_AFFP_G_B0_T1);
-        if constexpr (!BORDER && !TRAIL) AFF_ASM(ANYSEQ_AFFP_G_B0_T0);
-    }
-    tf = make_int2(tfg, tff);
-    return st;
-}
-#undef AFF_ASM
 
 // Round-3 steady state (tools/gen_block_asm.py gen_aff2): blocks b .. be-1, kind
 // L = X space (clamp / best) or G space, weights by LUT or compare.  pf: the first
@@ -1288,11 +1177,24 @@ struct Aff2Args {
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
                    [hm] "s"(hm), [gp] "s"(gp)                                                                  \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
-template <bool L, bool BORDER, int PUB, bool LUT>
+// the band's last blocks (gen_aff2 epi): + the column-(w-1) capture and the poll clamp
+#define AF2E_ASM(NAME)                                                                                          \
+    asm volatile(NAME                                                                                          \
+                 : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
+                   [hg] "+v"(hg), [best] "+v"(bx), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf), [sc] "+s"(sc),     \
+                   [pf] "+s"(pf), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3), \
+                   [x4] "=&s"(x4), [cnt] "+v"(cnt), [gc] "+v"(gc), [ec] "+v"(ec), [fc] "+v"(fc) AF2_TS_OUT     \
+                 : [be] "s"(be), [q] "v"(a.q), [wm] "v"(a.wm), [wx] "v"(a.wx), [ll] "v"(a.ll), [lh] "v"(a.lh),   \
+                   [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
+                   [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
+                   [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
+                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch)                                                  \
+                 : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
+template <bool L, bool BORDER, int PUB, bool LUT, bool EPI = false>
 __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                   const Aff2Args& a, int go, int nge, int& g, int& fdn, int& dg,
                                                   int2& tf, int& e, int& hg, int& bx, uint64_t& ts_v, uint64_t& te_v,
-                                                  uint32_t& ts_f, uint32_t& nmiss) {
+                                                  uint32_t& ts_f, uint32_t& nmiss, uint32_t nch = 0, int* cap = nullptr) {
     uint32_t st, x0, x1, x2, x3, x4, pf = 0;
     const uint64_t hm = 0xffffffff00000000ull;
 #define RFL(x) __builtin_amdgcn_readfirstlane(x)
@@ -1314,22 +1216,34 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
 #endif
 #undef RFL
     int tfg = tf.x, tff = tf.y;
-#define AF2_SEL(K, U)                                                                   \
-    if constexpr (BORDER && PUB == 0) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B1_NONE_U##U));          \
-    if constexpr (BORDER && PUB == 1) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B1_LDS_U##U));           \
-    if constexpr (BORDER && PUB == 2) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B1_GLOB_U##U));          \
-    if constexpr (!BORDER && PUB == 0) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B0_NONE_U##U));         \
-    if constexpr (!BORDER && PUB == 1) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B0_LDS_U##U));          \
-    if constexpr (!BORDER && PUB == 2) AF2_ASM(AF2_NAME(ANYSEQ_AF2_##K##_B0_GLOB_U##U));
-    if constexpr (L && LUT) { AF2_SEL(L, 1) }
-    if constexpr (L && !LUT) { AF2_SEL(L, 0) }
-    if constexpr (!L && LUT) { AF2_SEL(G, 1) }
-    if constexpr (!L && !LUT) { AF2_SEL(G, 0) }
+#define AF2_SEL(A, V, K, U)                                                                   \
+    if constexpr (BORDER && PUB == 0) A(AF2_NAME(ANYSEQ_##V##_##K##_B1_NONE_U##U));          \
+    if constexpr (BORDER && PUB == 1) A(AF2_NAME(ANYSEQ_##V##_##K##_B1_LDS_U##U));           \
+    if constexpr (BORDER && PUB == 2) A(AF2_NAME(ANYSEQ_##V##_##K##_B1_GLOB_U##U));          \
+    if constexpr (!BORDER && PUB == 0) A(AF2_NAME(ANYSEQ_##V##_##K##_B0_NONE_U##U));         \
+    if constexpr (!BORDER && PUB == 1) A(AF2_NAME(ANYSEQ_##V##_##K##_B0_LDS_U##U));          \
+    if constexpr (!BORDER && PUB == 2) A(AF2_NAME(ANYSEQ_##V##_##K##_B0_GLOB_U##U));
+    if constexpr (EPI) {
+        nch = __builtin_amdgcn_readfirstlane(nch);
+        int cnt = cap[0], gc = cap[1], ec = cap[2], fc = cap[3];
+        if constexpr (L && LUT) { AF2_SEL(AF2E_ASM, AF2E, L, 1) }
+        if constexpr (L && !LUT) { AF2_SEL(AF2E_ASM, AF2E, L, 0) }
+        if constexpr (!L && LUT) { AF2_SEL(AF2E_ASM, AF2E, G, 1) }
+        if constexpr (!L && !LUT) { AF2_SEL(AF2E_ASM, AF2E, G, 0) }
+        cap[0] = cnt, cap[1] = gc, cap[2] = ec, cap[3] = fc;
+    } else {
+        (void)nch, (void)cap;
+        if constexpr (L && LUT) { AF2_SEL(AF2_ASM, AF2, L, 1) }
+        if constexpr (L && !LUT) { AF2_SEL(AF2_ASM, AF2, L, 0) }
+        if constexpr (!L && LUT) { AF2_SEL(AF2_ASM, AF2, G, 1) }
+        if constexpr (!L && !LUT) { AF2_SEL(AF2_ASM, AF2, G, 0) }
+    }
 #undef AF2_SEL
     tf = make_int2(tfg, tff);
     return st;
 }
 #undef AF2_ASM
+#undef AF2E_ASM
 
 template <bool PARTIAL>
 __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k,
@@ -1415,6 +1329,13 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
 #endif
     // clamp bound far below any cell when the problem does not clamp
     const int zoff = clamp ? 0 : 2 * kAffNeg;
+    // asm epilogue (the blocks past column w-1): needs codes (0xFF beyond w), not a
+    // last-row best (the last row's cells are read per column), and -- for the
+    // all-cells best -- top values beyond w that are real cells of the row above
+    // (every ring slot written by this band pair: nchunks >= kSlots) and a
+    // non-positive mismatch, so no extended cell exceeds a real one
+    const bool epi = k.codes && !(k.flags & 3) && bestmode != 2 &&
+                     (bestmode != 1 || (nchunks >= kSlots && k.wx - 2 * nge <= 0));
     Aff2Args la;
     if constexpr (ASM_OK) {
         la.rb = lds_addr(io.my_ring);
@@ -1455,7 +1376,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 // steady state the loop's poll (step 16) already sees the next chunk and
                 // prefetches its top row -- no wait on the band chain's critical path
                 if (!io.in_border) {
-                    const uint32_t need = (uint32_t)min(b + 2, nchunks);
+                    const uint32_t need = (uint32_t)min(b + 1 + k.slack, nchunks);
                     if (seen_prod < need && !(seen_prod = spin_lds_ge(io.my_prod, need, err))) return;
                 }
                 // state into the loop's space: the lane's cell of step t0-1 is column t0-2-lane
@@ -1489,8 +1410,36 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 } else {
                     if (k.lut) { AF2_ROLES(false, true) } else { AF2_ROLES(false, false) }
                 }
-#undef AF2_ROLES
 #undef AF2_CALL
+                if (!st && epi) {
+                    // the band's last blocks in the loop too: every lane runs on past column
+                    // w-1 (subject code 0xFF there) and keeps its column-(w-1) state
+                    int cap[4] = {w + lane - (int)bb * CH, g, e, fdn};   // steps until column w-1
+#define AF2_CALL(LV, BD, PB, LU)                                                                                     \
+    st = aff2_loop_asm<LV, BD, PB, LU, true>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
+                                             fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)nchunks, cap)
+                    if (xs) {
+                        if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
+                    } else {
+                        if (k.lut) { AF2_ROLES(false, true) } else { AF2_ROLES(false, false) }
+                    }
+#undef AF2_CALL
+                    if (st) {
+                        atomicOr(err, ERR_SPIN_TIMEOUT);
+                        return;
+                    }
+                    g = cap[1];
+                    e = cap[2];
+                    fdn = cap[3];
+                    if (xs) {
+                        g = to_g(g, w - 1);
+                        e = to_g(e, w - 1);
+                        fdn = to_g(fdn, w - 1);
+                        best = max(best, bx - (row + 2) * nge);
+                    }
+                    break;   // band done
+                }
+#undef AF2_ROLES
                 if (st) {
                     atomicOr(err, ERR_SPIN_TIMEOUT);
                     return;
@@ -1656,6 +1605,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
     const int nsym = fp.alpha ? __builtin_amdgcn_readfirstlane(*fp.alpha) : 0;
     k.codes = nsym > 0 && nsym < 255;
     k.lut = nsym > 0 && nsym <= 8 && fp.lut_ok;
+    k.slack = fp.slack;
     if (fp.prio && wave < NW) __builtin_amdgcn_s_setprio(3);   // compute waves before the I/O wave
     for (;;) {
         if (threadIdx.x == 0) {
@@ -1689,7 +1639,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
             const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
             io_wave<32, true, int2>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0], &sh.s_filled,
                                     &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
-                                    P.nslots < P.ngroups - 1);
+                                    P.nslots < P.ngroups - 1, 2);
         } else {
             const int band = first + wave;
             if (band <= last) {

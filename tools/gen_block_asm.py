@@ -310,307 +310,6 @@ def gen_loop2(kind, border, pub, ts=False):
     return out
 
 
-# ---------------------------------------------------------------- affine --
-AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v191
-AW, AA, AH = 192, 193, 194  # weight, diag + weight, H - Z temp (local best)
-ASK0, ASK1 = 196, 204       # subject words, double buffered
-AVT, AVT2, AVA, AVB = 212, 213, 214, 215
-
-
-def gen_loop_aff(kind, border, pub, ts=False):
-    """Affine (Gotoh, G-space) steady-state loop over full blocks b .. be-1 of a
-    band; same LDS protocol as gen_loop2 with (G, F) pairs in the rings.
-    Per step (kind G: global / semiglobal; L: local adds the clamp and the best):
-        C  v_cmp_eq_u32_sdwa vcc, q, s.byte
-        D  v_cndmask_b32     W, wx, wm, vcc
-        F1 v_mov_b32_dpp     TF, Fprev wave_shr:1   F of this cell from the row above
-        G1 v_mov_b32_dpp     TG, Gprev wave_shr:1   G of the row above (next diagonal)
-        X  v_max_i32         e, e, hg               E_G = max(E_G, G_left + go)
-        E  v_add_u32         A, dg, W
-        M  v_max3_i32        OG, A, e, TF           cell
-       (L  v_max_i32         OG, Z, OG              clamp: H >= 0 <=> G >= Z_t (wave-uniform);
-                                                    Z far below Z_t when the problem does not clamp)
-        H  v_add_u32         hg, go, OG             G + go (next E, this F-down)
-        Fm v_max_i32         OF, TF, hg             F-down
-       (L  every 2nd step: best = max3(best, OG - Zb, OG' - Zb'), Zb = Z_t)
-        S  two wave_shl:1 shift-register steps (publishing roles)."""
-    L = kind == "L"
-    trailing = pub != "lds"
-    out = []
-    e = out.append
-    sets = (ASK0, ASK1)
-
-    def TG(u):
-        return v(AT0 + 2 * u)
-
-    def TF(u):
-        return v(AT0 + 2 * u + 1)
-
-    def OG(u):
-        return v(AO0 + 2 * u)
-
-    def OF(u):
-        return v(AO0 + 2 * u + 1)
-
-    def body(k):
-        cs, ns = sets[k], sets[1 - k]
-        e("s_add_u32 %[x1], %[b], 1")
-        if border:
-            # band 0: lanes write the top border (G, G + go) of column 32b + lane
-            e("s_lshl_b32 %[x0], %[b], 5")
-            e("s_mul_i32 %[x2], %[x0], %[bvs]")
-            e(f"v_add_u32_e32 v{AVT}, %[x2], %[bvb]")
-            e(f"v_add_u32_e32 v{AVT + 1}, %[go], v{AVT}")
-            e("s_lshl_b32 %[x2], %[x0], 3")
-            e(f"v_add_u32_e32 v{AVA}, %[x2], %[lid8]")
-            e(f"v_and_b32_e32 v{AVA}, 0xfff, v{AVA}")
-            e(f"v_add_u32_e32 v{AVA}, %[rb], v{AVA}")
-            e(f"ds_write_b64 v{AVA}, v[{AVT}:{AVT + 1}]")
-            e("s_waitcnt lgkmcnt(0)")
-            throttle(e, k)
-        else:
-            wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=AVT2)
-        if ts:
-            # diagnostic build: the time the band's first steady-state block starts
-            e("s_cmp_lg_u32 %[tsf], 0")
-            e(f"s_cbranch_scc1 L_nots{k}_%=")
-            e("s_memrealtime %[ts]")
-            e("s_waitcnt lgkmcnt(0)")
-            e("s_mov_b32 %[tsf], 1")
-            e(f"L_nots{k}_%=:")
-        if pub == "lds":
-            e("s_cmp_lt_u32 %[b], 17")
-            e(f"s_cbranch_scc1 L_nobp{k}_%=")
-            e("s_sub_u32 %[x4], %[b], 17")
-            wait(e, f"bp{k}", "%[sc]", "%[x4]", "%[anc]", tmp=AVT2)
-            e(f"L_nobp{k}_%=:")
-        # top row of block b: 32 (G, F) pairs
-        e("s_lshl_b32 %[x2], %[b], 8")
-        e("s_and_b32 %[x2], %[x2], 4095")
-        e("s_add_u32 %[x2], %[x2], %[rb]")
-        e(f"v_mov_b32_e32 v{AVB}, %[x2]")
-        for i in range(16):
-            e(f"ds_read_b128 v[{AT0 + 4 * i}:{AT0 + 4 * i + 3}], v{AVB} offset:{16 * i}")
-        g, f, dg = "%[cur]", "%[fd]", "%[dg]"
-        pf = 0   # prefetch reads issued (outstanding behind the ring reads)
-        for u in range(32):
-            if u == 16:
-                # prefetch the next block's subject words (behind the ring reads)
-                e("s_cmp_ge_u32 %[x1], %[be]")
-                e(f"s_cbranch_scc1 L_nopf{k}_%=")
-                e("s_add_u32 %[x4], %[b], 2")
-                wait(e, f"sf{k}", "%[sf]", "%[x4]", "%[asf]", tmp=AVT2)
-                e("s_and_b32 %[x2], %[x1], 31")
-                e("s_lshl_b32 %[x2], %[x2], 11")
-                e(f"v_add_u32_e32 v{AVA}, %[x2], %[skb]")
-                for i in range(4):
-                    e(f"ds_read2st64_b32 v[{ns + 2 * i}:{ns + 2 * i + 1}], v{AVA} offset0:{2 * i} offset1:{2 * i + 1}")
-                e(f"L_nopf{k}_%=:")
-                pf = 4
-            if u >= 1 and (u - 1) % 2 == 0:
-                i = (u - 1) // 2      # ring read holding column 32b + u - 1
-                e(f"s_waitcnt lgkmcnt({min(15, 15 - i + pf)})")
-            sw = v(cs + u // 4)
-            tg = "%[tfg]" if u == 0 else TG(u - 1)
-            tf = "%[tff]" if u == 0 else TF(u - 1)
-            e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
-            e(f"v_cndmask_b32_e32 v{AW}, %[wx], %[wm], vcc")
-            e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
-            e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
-            e("v_max_i32_e32 %[e], %[e], %[hg]")
-            e(f"v_add_u32_e32 v{AA}, {dg}, v{AW}")
-            e(f"v_max3_i32 {OG(u)}, v{AA}, %[e], {tf}")
-            if L:
-                e(f"v_max_i32_e32 {OG(u)}, %[z], {OG(u)}")
-            e(f"v_add_u32_e32 %[hg], %[go], {OG(u)}")
-            e(f"v_max_i32_e32 {OF(u)}, {tf}, %[hg]")
-            if L:
-                # best in H space: OG - Zb (Zb = the true (r+c+2)(-ge); z is the clamp
-                # bound, Zb or far below it when the problem does not clamp)
-                if u % 2 == 0:
-                    e(f"v_subrev_u32_e32 v{AH}, %[zb], {OG(u)}")
-                else:
-                    e(f"v_subrev_u32_e32 v{AVT2}, %[zb], {OG(u)}")
-                    e(f"v_max3_i32 %[best], %[best], v{AH}, v{AVT2}")
-                e("s_add_u32 %[z], %[z], %[nge]")
-                e("s_add_u32 %[zb], %[zb], %[nge]")
-            if u >= 2 and pub != "none":
-                e(f"v_mov_b32_dpp {OG(u - 1)}, {OG(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-                e(f"v_mov_b32_dpp {OF(u - 1)}, {OF(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-            g, f, dg = OG(u), OF(u), tg
-        e(f"v_mov_b32_e32 %[cur], {OG(31)}")
-        e(f"v_mov_b32_e32 %[fd], {OF(31)}")
-        e(f"v_mov_b32_e32 %[dg], {TG(30)}")
-        if pub != "none":
-            e(f"v_mov_b32_dpp {OG(31)}, {OG(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-            e(f"v_mov_b32_dpp {OF(31)}, {OF(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-        e(f"v_mov_b32_e32 %[tfg], {TG(31)}")
-        e(f"v_mov_b32_e32 %[tff], {TF(31)}")
-        if pub != "none":
-            e("s_cmp_lt_u32 %[b], 2")
-            e(f"s_cbranch_scc1 L_nopub{k}_%=")
-            e("s_sub_u32 %[x2], %[b], 2")
-            e("s_lshl_b32 %[x2], %[x2], 8")
-            if pub == "lds":
-                e("s_and_b32 %[x2], %[x2], 4095")
-                e("s_add_u32 %[x2], %[x2], %[nb]")
-            e(f"v_add_u32_e32 v{AVT}, %[x2], %[lo]")
-            e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
-            e("s_mov_b64 exec, %[hm]")
-            if pub == "lds":
-                e(f"ds_write_b64 v{AVT}, v[{AO0 + 62}:{AO0 + 63}]")
-            else:
-                e(f"global_store_dwordx2 v{AVT}, v[{AO0 + 62}:{AO0 + 63}], %[gp] sc1")
-            e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
-            if pub == "lds":
-                e("s_sub_u32 %[x2], %[b], 1")
-                e(f"v_mov_b32_e32 v{AVT2}, %[x2]")
-                e(f"ds_write_b32 %[anp], v{AVT2}")
-            e(f"L_nopub{k}_%=:")
-        e(f"v_mov_b32_e32 v{AVT2}, %[x1]")
-        if not border:
-            e(f"ds_write_b32 %[acn], v{AVT2}")
-        if trailing:
-            e(f"ds_write_b32 %[atl], v{AVT2}")
-        e("s_mov_b32 %[b], %[x1]")
-
-    # prologue: the first block's subject words into set 0
-    e("s_add_u32 %[x1], %[b], 1")
-    wait(e, "sfp", "%[sf]", "%[x1]", "%[asf]", tmp=AVT2)
-    e("s_and_b32 %[x2], %[b], 31")
-    e("s_lshl_b32 %[x2], %[x2], 11")
-    e(f"v_add_u32_e32 v{AVA}, %[x2], %[skb]")
-    for i in range(4):
-        e(f"ds_read2st64_b32 v[{ASK0 + 2 * i}:{ASK0 + 2 * i + 1}], v{AVA} offset0:{2 * i} offset1:{2 * i + 1}")
-    e("s_waitcnt lgkmcnt(0)")
-    e("L_top_%=:")
-    body(0)
-    e("s_cmp_lt_u32 %[b], %[be]")
-    e("s_cbranch_scc0 L_done_%=")
-    body(1)
-    e("s_cmp_lt_u32 %[b], %[be]")
-    e("s_cbranch_scc1 L_top_%=")
-    e("L_done_%=:")
-    if ts:
-        e("s_memrealtime %[te]")
-        e("s_waitcnt lgkmcnt(0)")
-    e("s_mov_b32 %[st], 0")
-    e("s_branch L_end_%=")
-    e("L_timeout_%=:")
-    e("s_mov_b32 %[st], 1")
-    e("L_end_%=:")
-    return out
-
-
-def gen_prologue_aff(kind, border, trailing):
-    """Affine prologue: blocks 0 and 1 of a band whose lanes left of column 0 are
-    NOT virtual (any border mode but the scheme's own): the steps of gen_loop_aff
-    under an exec mask that grows by one lane per step (lane l first runs at step
-    l + 1, column 0), so lanes keep their initial border state until they start.
-    The DPPs run on the full exec (5 wait states after the exec write: the step's
-    two leading VALU + s_nop 2) so that a lane's first diagonal is its upper
-    neighbour's initial state; s_bfm_b64 then masks the cell update.  No publishing (the first chunk leaves in
-    block 2); the consumed / tail counters are written with the full exec."""
-    L = kind == "L"
-    out = []
-    e = out.append
-
-    def TG(u):
-        return v(AT0 + 2 * u)
-
-    def TF(u):
-        return v(AT0 + 2 * u + 1)
-
-    def OG(u):
-        return v(AO0 + 2 * u)
-
-    def OF(u):
-        return v(AO0 + 2 * u + 1)
-
-    for k in (0, 1):
-        e(f"s_mov_b32 %[b], {k}")
-        e("s_mov_b32 %[x1], " + str(k + 1))
-        wait(e, f"psf{k}", "%[sf]", "%[x1]", "%[asf]", tmp=AVT2)
-        # this block's subject words (set 0)
-        e(f"s_mov_b32 %[x2], {k << 11}")
-        e(f"v_add_u32_e32 v{AVA}, %[x2], %[skb]")
-        for i in range(4):
-            e(f"ds_read2st64_b32 v[{ASK0 + 2 * i}:{ASK0 + 2 * i + 1}], v{AVA} offset0:{2 * i} offset1:{2 * i + 1}")
-        if border:
-            e(f"s_mov_b32 %[x0], {32 * k}")
-            e("s_mul_i32 %[x2], %[x0], %[bvs]")
-            e(f"v_add_u32_e32 v{AVT}, %[x2], %[bvb]")
-            e(f"v_add_u32_e32 v{AVT + 1}, %[go], v{AVT}")
-            e(f"s_mov_b32 %[x2], {(32 * k) << 3}")
-            e(f"v_add_u32_e32 v{AVA}, %[x2], %[lid8]")
-            e(f"v_and_b32_e32 v{AVA}, 0xfff, v{AVA}")
-            e(f"v_add_u32_e32 v{AVA}, %[rb], v{AVA}")
-            e(f"ds_write_b64 v{AVA}, v[{AVT}:{AVT + 1}]")
-        else:
-            wait(e, f"ppr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=AVT2)
-        e("s_waitcnt lgkmcnt(0)")
-        e(f"s_mov_b32 %[x2], {(k << 8) & 4095}")
-        e("s_add_u32 %[x2], %[x2], %[rb]")
-        e(f"v_mov_b32_e32 v{AVB}, %[x2]")
-        for i in range(16):
-            e(f"ds_read_b128 v[{AT0 + 4 * i}:{AT0 + 4 * i + 3}], v{AVB} offset:{16 * i}")
-        e("s_waitcnt lgkmcnt(0)")
-        # lanes that have not started hold their state in every step register, so
-        # the full-exec DPPs below hand them (and their lower neighbours) the
-        # values of the C++ masked path
-        for u in range(32):
-            e(f"v_mov_b32_e32 {OG(u)}, %[cur]")
-            e(f"v_mov_b32_e32 {OF(u)}, %[fd]")
-        g, f, dg = "%[cur]", "%[fd]", "%[dg]"
-        for u in range(32):
-            t = 32 * k + u
-            sw = v(ASK0 + u // 4)
-            tg = "%[tfg]" if u == 0 else TG(u - 1)
-            tf = "%[tff]" if u == 0 else TF(u - 1)
-            e("s_mov_b64 exec, -1")
-            e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
-            e(f"v_cndmask_b32_e32 v{AW}, %[wx], %[wm], vcc")
-            e("s_nop 2")
-            e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
-            e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
-            # the cell's own update only on the lanes at column >= 0 (lane l from step l + 1)
-            e(f"s_bfm_b64 exec, {t}, 0")
-            e("v_max_i32_e32 %[e], %[e], %[hg]")
-            e(f"v_add_u32_e32 v{AA}, {dg}, v{AW}")
-            e(f"v_max3_i32 {OG(u)}, v{AA}, %[e], {tf}")
-            if L:
-                e(f"v_max_i32_e32 {OG(u)}, %[z], {OG(u)}")
-            e(f"v_add_u32_e32 %[hg], %[go], {OG(u)}")
-            e(f"v_max_i32_e32 {OF(u)}, {tf}, %[hg]")
-            if L:
-                e(f"v_subrev_u32_e32 v{AH}, %[zb], {OG(u)}")
-                e(f"v_max_i32_e32 %[best], %[best], v{AH}")
-                e("s_add_u32 %[z], %[z], %[nge]")
-                e("s_add_u32 %[zb], %[zb], %[nge]")
-            g, f, dg = OG(u), OF(u), tg
-        # state moves under the last step's mask: lanes that have not started keep theirs
-        e(f"v_mov_b32_e32 %[cur], {OG(31)}")
-        e(f"v_mov_b32_e32 %[fd], {OF(31)}")
-        e(f"v_mov_b32_e32 %[dg], {TG(30)}")
-        e(f"v_mov_b32_e32 %[tfg], {TG(31)}")
-        e(f"v_mov_b32_e32 %[tff], {TF(31)}")
-        e("s_mov_b64 exec, -1")
-        e(f"v_mov_b32_e32 v{AVT2}, %[x1]")
-        if not border:
-            e(f"ds_write_b32 %[acn], v{AVT2}")
-        if trailing:
-            e(f"ds_write_b32 %[atl], v{AVT2}")
-    e("s_mov_b32 %[b], 2")
-    e("s_mov_b32 %[st], 0")
-    e("s_branch L_end_%=")
-    e("L_timeout_%=:")
-    e("s_mov_b64 exec, -1")
-    e("s_mov_b32 %[st], 1")
-    e("L_end_%=:")
-    return out
-
-
-
 # ------------------------------------------------------- affine, round 3 --
 # Registers of gen_aff2 (TOP pairs / cell pairs as gen_loop_aff).
 B_AW, B_AA, B_AT, B_AP = 192, 193, 194, 195   # cmp weight, diag + weight, temp, poll result
@@ -619,7 +318,10 @@ B_VT, B_VT2, B_VA, B_VB = 212, 213, 214, 215    # temps / LDS addresses
 B_WB = 216                                       # LUT weight bytes of 4 steps
 
 
-def gen_aff2(kind, border, pub, lut, ts=False):
+AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v191
+
+
+def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
     """Affine steady-state loop, round 3: full blocks b .. be-1.
     kind G: G space (X_G = X + (r+c+2)|ge|), no clamp, no best (amode 0).
     kind L: X space (X = H + (r+2)|ge|, a per-ROW shift): the local clamp H >= 0 is
@@ -634,7 +336,12 @@ def gen_aff2(kind, border, pub, lut, ts=False):
     half was prefetched in the previous block (when the producer's counter, polled
     at step 16, already covered the next chunk: bands start one block later than
     the structural minimum, so in the steady state no poll waits); subject codes of
-    the next block at step 8; publishing as gen_loop_aff (shift register)."""
+    the next block at step 8; publishing by a shift register (lane 63's cells leave
+    through DPP wave_shl:1, one ds_write / global_store per block).
+    epi: the band's last blocks (some lanes past the last column w-1): every lane keeps
+    computing (the subject code 0xFF beyond w matches nothing, so no extended cell
+    exceeds the real ones' best under the clamp), polls stop at chunk nch-1, and each
+    lane captures its state at column w-1 (per-lane countdown cnt) into gc / ec / fc."""
     L = kind == "L"
     trailing = pub != "lds"
     out = []
@@ -679,7 +386,11 @@ def gen_aff2(kind, border, pub, lut, ts=False):
             border_write("%[b]")
             e("s_waitcnt lgkmcnt(0)")
         else:
-            wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=B_VT2)
+            if epi:
+                e("s_min_u32 %[x4], %[x1], %[nch]")   # chunks >= nch are never published
+                wait(e, f"pr{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
+            else:
+                wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=B_VT2)
         ring_addr("%[b]")
         top_reads(0, "%[b]")
         e(f"L_pfd{k}_%=:")
@@ -733,6 +444,8 @@ def gen_aff2(kind, border, pub, lut, ts=False):
                     e(f"v_readfirstlane_b32 %[x2], v{B_AP}")
                     e("s_max_u32 %[sp], %[sp], %[x2]")
                     e("s_add_u32 %[x4], %[b], 2")
+                    if epi:
+                        e("s_min_u32 %[x4], %[x4], %[nch]")
                     e("s_cmp_ge_u32 %[sp], %[x4]")
                     e(f"s_cbranch_scc0 L_noq{k}_%=")
                 ring_addr("%[x1]")
@@ -770,6 +483,13 @@ def gen_aff2(kind, border, pub, lut, ts=False):
             e(f"v_max3_i32 {OG_(u)}, v{B_AA}, %[e], {tf}")
             e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
             e(f"v_max_i32_e32 {OF_(u)}, {tf}, %[hg]")
+            if epi:
+                # the lane whose cell is column w-1 at this step keeps its state
+                e("v_cmp_eq_u32_e32 vcc, 0, %[cnt]")
+                e(f"v_cndmask_b32_e32 %[gc], %[gc], {OG_(u)}, vcc")
+                e("v_cndmask_b32_e32 %[ec], %[ec], %[e], vcc")
+                e(f"v_cndmask_b32_e32 %[fc], %[fc], {OF_(u)}, vcc")
+                e("v_add_u32_e32 %[cnt], -1, %[cnt]")
             if L and u % 2 == 1:
                 e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
             if u >= 2 and pub != "none":
@@ -887,33 +607,16 @@ def main():
     for kind in ("G", "L"):
         for border in (0, 1):
             for pub in ("none", "lds", "glob"):
-                for ts in (False, True):
-                    name = f"ANYSEQ_AFF_{kind}_B{border}_{pub.upper()}" + ("_TS" if ts else "")
-                    lines.append(f"#define {name} \\")
-                    for ln in gen_loop_aff(kind, border, pub, ts):
-                        lines.append(f'    "{ln}\\n" \\')
-                    lines.append("")
-    for kind in ("G", "L"):
-        for border in (0, 1):
-            for pub in ("none", "lds", "glob"):
                 for lut in (0, 1):
                     for ts in (False, True):
-                        name = f"ANYSEQ_AF2_{kind}_B{border}_{pub.upper()}_U{lut}" + ("_TS" if ts else "")
-                        lines.append(f"#define {name} \\")
-                        for ln in gen_aff2(kind, border, pub, lut, ts):
-                            lines.append(f'    "{ln}\\n" \\')
-                        lines.append("")
-    for kind in ("G", "L"):
-        for border in (0, 1):
-            for trailing in (0, 1):
-                name = f"ANYSEQ_AFFP_{kind}_B{border}_T{trailing}"
-                lines.append(f"#define {name} \\")
-                for ln in gen_prologue_aff(kind, border, trailing):
-                    lines.append(f'    "{ln}\\n" \\')
-                lines.append("")
-    clob = ", ".join(f'"v{n}"' for n in range(AT0, AVB + 1))
+                        for epi in (False, True):
+                            name = (f"ANYSEQ_AF2{'E' if epi else ''}_{kind}_B{border}_{pub.upper()}_U{lut}"
+                                    + ("_TS" if ts else ""))
+                            lines.append(f"#define {name} \\")
+                            for ln in gen_aff2(kind, border, pub, lut, ts, epi):
+                                lines.append(f'    "{ln}\\n" \\')
+                            lines.append("")
     sclob = ", ".join(f'"s{n}"' for n in range(TA, TB + 2))
-    lines.append(f"#define ANYSEQ_AFF_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
     clob = ", ".join(f'"v{n}"' for n in range(AT0, B_WB + 1))
     lines.append(f"#define ANYSEQ_AF2_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, A + 1))
