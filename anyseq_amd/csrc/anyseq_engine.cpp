@@ -461,8 +461,8 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     unsigned long long* dbg = nullptr;
     static DevBuf stamp_buf;
     if (getenv("ANYSEQ_STAMPS")) {
-        dbg = (unsigned long long*)stamp_buf.get(8 * (16 + 4 * 4096));
-        HIPCHECK(hipMemsetAsync(dbg, 0, 8 * (16 + 4 * 4096), st));
+        dbg = (unsigned long long*)stamp_buf.get(8 * (16 + 20 * 4096));
+        HIPCHECK(hipMemsetAsync(dbg, 0, 8 * (16 + 20 * 4096), st));
         fpl.dbg = dbg;
     }
     C.stamps = dbg;
@@ -596,6 +596,19 @@ void fill_collect(FillCtx& C) {
                                                                  : (t[i + 3] < (1ull << 32) ? -2.0 - (double)t[i + 3] : -1.0));
                 fclose(f);
             }
+            // hand-off events of one block per band (affine asm, diagnostic build): 16 per band
+            std::vector<unsigned long long> ev(16 * 4096);
+            HIPCHECK(hipMemcpy(ev.data(), dbg + 16 + 4 * 4096, ev.size() * 8, hipMemcpyDeviceToHost));
+            if (FILE* g = fopen((std::string(tl) + ".ev").c_str(), "a")) {
+                fprintf(g, "# launch\n");
+                for (size_t i = 0; i < ev.size(); i += 16) {
+                    if (!ev[i + 3] && !ev[i]) continue;
+                    fprintf(g, "%zu", i / 16);
+                    for (int k = 0; k < 13; ++k) fprintf(g, " %llu", ev[i + k]);
+                    fprintf(g, "\n");
+                }
+                fclose(g);
+            }
         }
     }
     if (err & ERR_BAD_DESC) fail("fill kernel read a corrupt problem descriptor (error %u; %s)", err, fill_summary(C).c_str());
@@ -634,7 +647,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.affine = sc.gap_open != 0;
     fp.dbg = nullptr;
     // affine_asm bit 0: asm steady state, bit 1: scalar row stores (diagnostics)
-    fp.pad = ((g_tuning.affasm & 1) ? 0 : 1) | (g_tuning.affasm & 2);
+    fp.pad = ((g_tuning.affasm & 1) ? 0 : 1) | (g_tuning.affasm & 2) | (g_tuning.affasm & 12);
     // the LUT weights (G space sub - 2 ge, X space sub - ge) must fit int8
     const int nge = -sc.gap_extend;
     const int ws[4] = {sc.match + 2 * nge, sc.mismatch + 2 * nge, sc.match + nge, sc.mismatch + nge};

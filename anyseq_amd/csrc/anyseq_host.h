@@ -84,13 +84,13 @@ struct Tuning {
     int fronts = 2;
     int NWa = 4;     // affine fill: compute waves per workgroup (3 or 4)
     int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
-    int affasm = 1;  // affine fill: bit 0 asm steady state, bit 2 asm prologue (experimental, off)
+    int affasm = 1;  // affine fill: bit 0 asm steady state; bit 1 no asm epilogue; bits 2/3 none for best-all / other
     int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
     int afft = 1;        // affine construct: run Hirschberg halves taller than wide transposed
-    int prio = 0;        // compute waves at s_setprio 3 (the I/O wave stays at 0)
+    int prio = 0;        // 1: compute waves at s_setprio 3; 2: the I/O wave at 3; 3: its hand-off step at 3
     int thr = 0;         // band 0 of every problem sleeps thr s_sleep-1 units per block (chain pace)
     int afflut = 1;      // affine fill: v_perm weight table when the pair has <= 8 symbols
-    int slack = 1;       // affine fill: blocks a band starts behind the structural minimum
+    int slack = 0;       // affine fill: half chunks a band starts behind the structural minimum
 };
 extern Tuning g_tuning;
 

@@ -790,23 +790,52 @@ struct HandOff<int2> {
     __device__ static int2 sentinel() { return make_int2((int)0x80808080, (int)0x80808080); }
 };
 
+#ifndef ANYSEQ_IO_SKEW_POLLING
+#define ANYSEQ_IO_SKEW_POLLING 8
+#endif
+constexpr int kIoSkewPolling = ANYSEQ_IO_SKEW_POLLING;   // skewed blocks per I/O pass while a hand-off poll is out
+
 template <int CH, bool SKEW, typename T = int32_t>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
                         uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
-                        uint32_t* cons0, uint32_t* err, bool reset_in = false, int ext = 0) {
+                        uint32_t* cons0, uint32_t* err, bool reset_in = false, int ext = 0, int pscale = 1,
+                        bool hprio = false, unsigned long long* evp = nullptr) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
+    constexpr int GR = 16;             // hand-off poll granule (columns)
+    constexpr int GPC = CH / GR;       // granules per chunk
     const int nchunks = (w + CH - 1) / CH;
+    const int ngran = (w + GR - 1) / GR;
     // ext: skewed blocks staged past the last chunk (the affine asm epilogue's), whose
-    // columns >= w all hold code 0xFF
+    // columns >= w all hold code 0xFF; pscale: units of the ring counter per chunk (the
+    // affine fill counts half chunks = granules)
     const int nskew = nchunks + ext;
     const bool need_in = g_in != nullptr;
     const GLOBAL_AS uint8_t* sg = gmem(s);
-    int s_next = 0, sk_next = 0, in_next = 0;
+    int s_next = 0, sk_next = 0, in_gran = 0;
     uint32_t idle = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    while (s_next < nchunks || (SKEW && sk_next < nskew) || (need_in && in_next < nchunks)) {
+    while (s_next < nchunks || (SKEW && sk_next < nskew) || (need_in && in_gran < ngran)) {
         bool progress = false;
+        // The hand-off poll goes out first (the band chain waits on it): 128 columns from
+        // the first granule not yet in, consumed after this iteration's staging work, so
+        // the load's round trip overlaps it.  The previous group's last band stores its
+        // bottom row straight into g_in (sc1), which the host filled with the sentinel
+        // (never a kernel value): a granule is in when none of its columns < w holds it.
+        T pv[2];
+        int plim = 0;
+#ifdef ANYSEQ_STAMPS
+        const uint64_t t_poll = evp ? __builtin_amdgcn_s_memrealtime() : 0;   // diagnostic build
+#endif
+        if (need_in && in_gran < ngran) {
+            plim = min(((int)lds_ld(cons0) + kSlots) * GPC, ngran);   // ring space
+            plim = min(plim, in_gran + 8);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int col = in_gran * GR + i * 64 + lane;
+                pv[i] = col < plim * GR && col < w ? HandOff<T>::load(g_in + col) : HandOff<T>::zero();
+            }
+        }
         if (s_next < nchunks) {
             const uint32_t tl = lds_ld(tail);
             // the trailing wave in block `tl` still reads columns >= tl*CH - kMaxBack
@@ -841,7 +870,7 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             // and a free slot: the trailing wave has finished block b - kSkewBlocks
             const uint32_t tl = lds_ld(tail);
             int lim = min(sk_avail, tl >= 0x7fffffffu ? nskew : (int)tl + kSkewBlocks);
-            lim = min(lim, sk_next + 8);
+            lim = min(lim, sk_next + (plim > in_gran ? kIoSkewPolling : 8));
             for (int b = sk_next; b < lim; ++b) {
                 uint32_t d[8];
                 load_sbytes<32>(s_ring, (32 * b - 1 - lane) & (kSRing - 1), d);
@@ -868,60 +897,61 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                 progress = true;
             }
         }
-        if (need_in && in_next < nchunks) {
-            // The previous group's last band stores its bottom row straight into g_in
-            // (sc1), which the host filled with the sentinel -1 (never a kernel value:
-            // G >= 0 and local H >= 0).  Poll the data itself: a chunk is ready when
-            // none of its columns < w still holds -1.
-            const int lim = min((int)lds_ld(cons0) + kSlots, nchunks);
-            if (lim > in_next) {
-                constexpr int PER = kSlots * CH / 64;   // 2 chunks per load row
-                T v[PER];
-                const int c0 = in_next * CH, c1 = lim * CH;
+        if (plim > in_gran) {
+            // hprio: the hand-off step runs at top issue priority (this wave shares a SIMD
+            // with a compute wave, which otherwise wins every VALU slot); staging and skew
+            // stay at the bottom, in the compute wave's bubbles
+            if (hprio) __builtin_amdgcn_s_setprio(3);
+            // leading run of complete granules (16 lanes each)
+            int ready = 0;
+            bool stop = false;
 #pragma unroll
-                for (int i = 0; i < PER; ++i) {
-                    const int col = c0 + i * 64 + lane;
-                    v[i] = col < c1 && col < w ? HandOff<T>::load(g_in + col) : HandOff<T>::zero();
-                }
-                // leading run of complete chunks
-                int ready = 0;
-                bool stop = false;
+            for (int i = 0; i < 2; ++i) {
+                const uint64_t bad = __ballot(HandOff<T>::pending(pv[i]));
 #pragma unroll
-                for (int i = 0; i < PER; ++i) {
-                    const uint64_t bad = __ballot(HandOff<T>::pending(v[i]));
-                    if (!stop && in_next + 2 * i < lim && (uint32_t)bad == 0u) ++ready; else stop = true;
-                    if (!stop && in_next + 2 * i + 1 < lim && (uint32_t)(bad >> 32) == 0u) ++ready; else stop = true;
-                }
-                if (ready > 0) {
-                    const int c2 = (in_next + ready) * CH;
-#pragma unroll
-                    for (int i = 0; i < PER; ++i) {
-                        const int col = c0 + i * 64 + lane;
-                        if (col < c2) ring0[col & IRM] = v[i];
-                    }
-                    // ring of hand-off rows (DPProblem::nslots < ngroups - 1): put the sentinel
-                    // back, so the group that reuses this slot 2*grid+2 groups later is polled
-                    // against fresh data
-                    if (reset_in) {
-                        T* gw = const_cast<T*>(g_in);
-#pragma unroll
-                        for (int i = 0; i < PER; ++i) {
-                            const int col = c0 + i * 64 + lane;
-                            if (col < c2 && col < w) HandOff<T>::store(gw + col, HandOff<T>::sentinel());
-                        }
-                    }
-                    lds_st(prod0, (uint32_t)(in_next + ready));
-                    in_next += ready;
-                    progress = true;
+                for (int g = 0; g < 4; ++g) {
+                    if (!stop && in_gran + 4 * i + g < plim && ((bad >> (16 * g)) & 0xffffu) == 0u) ++ready;
+                    else stop = true;
                 }
             }
+            if (ready > 0) {
+#ifdef ANYSEQ_STAMPS
+                // diagnostic build: when the granule of column 32000 (chunk 1000) came in
+                if (evp && lane == 0 && in_gran <= 2000 && in_gran + ready > 2000) {
+                    evp[11] = __builtin_amdgcn_s_memrealtime();
+                    evp[12] = t_poll;
+                }
+#endif
+                const int c0 = in_gran * GR, c2 = (in_gran + ready) * GR;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int col = c0 + i * 64 + lane;
+                    if (col < c2) ring0[col & IRM] = pv[i];
+                }
+                // ring of hand-off rows (DPProblem::nslots < ngroups - 1): put the sentinel
+                // back, so the group that reuses this slot 2*grid+2 groups later is polled
+                // against fresh data
+                if (reset_in) {
+                    T* gw = const_cast<T*>(g_in);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const int col = c0 + i * 64 + lane;
+                        if (col < c2 && col < w) HandOff<T>::store(gw + col, HandOff<T>::sentinel());
+                    }
+                }
+                in_gran += ready;
+                // the counter: granules (pscale 2, CH 32), else whole chunks
+                lds_st(prod0, in_gran >= ngran ? (uint32_t)(nchunks * pscale) : (uint32_t)(in_gran * pscale / GPC));
+                progress = true;
+            }
+            if (hprio) __builtin_amdgcn_s_setprio(0);
         }
         if (!progress) {
             __builtin_amdgcn_s_sleep(1);
             if ((++idle & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t_start > SPIN_TICKS || err_set(err))) {
                 atomicOr(err, ERR_SPIN_TIMEOUT | 8u);
-                lds_st(prod0, (uint32_t)nchunks);
-                lds_st(s_filled, (uint32_t)nchunks);
+                lds_st(prod0, (uint32_t)(nchunks * pscale));
+                lds_st(s_filled, (uint32_t)nskew);
                 return;
             }
         }
@@ -946,7 +976,10 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
         ck.wm = fp.match - 2 * fp.gap;
         ck.wx = fp.mismatch - 2 * fp.gap;
     }
-    if (fp.prio && wave < NW) __builtin_amdgcn_s_setprio(3);   // compute waves before the I/O wave
+    // issue priority: 1 = compute waves before the I/O wave, 2 = the I/O wave first (it
+    // sleeps when idle; its hand-off polls sit on the band chain)
+    if (fp.prio == 1 && wave < NW) __builtin_amdgcn_s_setprio(3);
+    if (fp.prio == 2 && wave == NW) __builtin_amdgcn_s_setprio(3);
     for (;;) {
         if (threadIdx.x == 0) {
             sh.group = (int32_t)atomicAdd(dq, 1u);
@@ -1160,7 +1193,7 @@ struct Aff2Args {
 };
 #ifdef ANYSEQ_STAMPS
 #define AF2_NAME(NAME) NAME##_TS
-#define AF2_TS_OUT , [ts] "+s"(ts_v), [te] "+s"(te_v), [tsf] "+s"(ts_f), [nmiss] "+s"(nmiss)
+#define AF2_TS_OUT , [ts] "+s"(ts_v), [te] "+s"(te_v), [tsf] "+s"(ts_f), [nmiss] "+s"(nmiss), [dbp] "+s"(dbp)
 #else
 #define AF2_NAME(NAME) NAME
 #define AF2_TS_OUT
@@ -1194,9 +1227,10 @@ template <bool L, bool BORDER, int PUB, bool LUT, bool EPI = false>
 __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                   const Aff2Args& a, int go, int nge, int& g, int& fdn, int& dg,
                                                   int2& tf, int& e, int& hg, int& bx, uint64_t& ts_v, uint64_t& te_v,
-                                                  uint32_t& ts_f, uint32_t& nmiss, uint32_t nch = 0, int* cap = nullptr) {
+                                                  uint32_t& ts_f, uint32_t& nmiss, uint32_t nch = 0, int* cap = nullptr,
+                                                  uint64_t dbp = 0) {
     uint32_t st, x0, x1, x2, x3, x4, pf = 0;
-    const uint64_t hm = 0xffffffff00000000ull;
+    const uint64_t hm = 0xffff000000000000ull;   // lanes 48..63 (publishing)
 #define RFL(x) __builtin_amdgcn_readfirstlane(x)
     b = RFL(b);
     sp = RFL(sp);
@@ -1209,10 +1243,11 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
 #ifdef ANYSEQ_STAMPS
     ts_f = RFL(ts_f);
     nmiss = RFL(nmiss);
+    dbp = ((uint64_t)(uint32_t)RFL((uint32_t)(dbp >> 32)) << 32) | (uint32_t)RFL((uint32_t)dbp);
     ts_v = ((uint64_t)(uint32_t)RFL((uint32_t)(ts_v >> 32)) << 32) | (uint32_t)RFL((uint32_t)ts_v);
     te_v = ((uint64_t)(uint32_t)RFL((uint32_t)(te_v >> 32)) << 32) | (uint32_t)RFL((uint32_t)te_v);
 #else
-    (void)ts_v, (void)te_v, (void)ts_f, (void)nmiss;
+    (void)ts_v, (void)te_v, (void)ts_f, (void)nmiss, (void)dbp;
 #endif
 #undef RFL
     int tfg = tf.x, tff = tf.y;
@@ -1323,19 +1358,23 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     const int fe = w >= CH - 1 ? (w - (CH - 1)) / CH + 1 : 0;   // full blocks: 32b + 30 < w
     uint32_t seen_prod = 0, seen_sfill = 0, seen_cons = 0;
     uint64_t ts_v = 0, te_v = 0;   // diagnostic build: steady-state start / end (s_memrealtime)
-    uint32_t ts_f = 0, nmiss = 0;  // diagnostic build: + blocks without a prefetched top row
+    uint32_t ts_f = 0, nmiss = 0;  // diagnostic build: + hand-off waits
+    // diagnostic build: hand-off event record of the band (tools/probes/_aff_timeline.py)
+    const uint64_t dbp = dbg && band < 2048 ? (uint64_t)(size_t)(dbg + 16 + 4 * 4096 + 16 * (band + (P.q_step < 0 ? 2048 : 0))) : 0;
+#ifdef ANYSEQ_STAMPS
+    auto ev_store = [&](int slot, uint64_t v) {
+        if (dbp && lane == 0) reinterpret_cast<unsigned long long*>(dbp)[slot] = v;
+    };
+#endif
 #ifdef ANYSEQ_STAMPS
     uint64_t t_b0 = 0;             // diagnostic build: C++ block 0 start
 #endif
     // clamp bound far below any cell when the problem does not clamp
     const int zoff = clamp ? 0 : 2 * kAffNeg;
-    // asm epilogue (the blocks past column w-1): needs codes (0xFF beyond w), not a
-    // last-row best (the last row's cells are read per column), and -- for the
-    // all-cells best -- top values beyond w that are real cells of the row above
-    // (every ring slot written by this band pair: nchunks >= kSlots) and a
-    // non-positive mismatch, so no extended cell exceeds a real one
-    const bool epi = k.codes && !(k.flags & 3) && bestmode != 2 &&
-                     (bestmode != 1 || (nchunks >= kSlots && k.wx - 2 * nge <= 0));
+    // asm epilogue (the blocks past column w-1, whose cells feed no real cell): needs
+    // codes (0xFF beyond w) and not a last-row best (the last row's cells are read per
+    // column); the loop's best takes real cells only
+    const bool epi = k.codes && !(k.flags & 3) && bestmode != 2 && !(k.flags & (bestmode == 1 ? 4 : 8));
     Aff2Args la;
     if constexpr (ASM_OK) {
         la.rb = lds_addr(io.my_ring);
@@ -1347,7 +1386,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         la.asf = lds_addr(io.s_filled);
         la.atl = lds_addr(io.tail);
         la.skb = lds_addr(io.skew) + 4u * lane;
-        la.lo = 8u * (lane - 32);
+        la.lo = 8u * (lane - 48);   // publishing lanes 48..63: 16 columns each half block
         la.lid8 = 8u * lane;
         // band 0's top border (value, value + go) in the loop's space
         la.bvb = (uint32_t)(xs ? to_x(B.top(lane, nge), lane) : B.top(lane, nge));
@@ -1376,7 +1415,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 // steady state the loop's poll (step 16) already sees the next chunk and
                 // prefetches its top row -- no wait on the band chain's critical path
                 if (!io.in_border) {
-                    const uint32_t need = (uint32_t)min(b + 1 + k.slack, nchunks);
+                    const uint32_t need = (uint32_t)min(2 * b + 1 + k.slack, 2 * nchunks);
                     if (seen_prod < need && !(seen_prod = spin_lds_ge(io.my_prod, need, err))) return;
                 }
                 // state into the loop's space: the lane's cell of step t0-1 is column t0-2-lane
@@ -1395,7 +1434,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 uint32_t st = 0;
 #define AF2_CALL(LV, BD, PB, LU)                                                                               \
     st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, fdn, \
-                                       dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss)
+                                       dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, nullptr, dbp)
 #define AF2_ROLES(LV, LU)                          \
     switch (role) {                                \
         case 0: AF2_CALL(LV, false, 0, LU); break; \
@@ -1414,10 +1453,14 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 if (!st && epi) {
                     // the band's last blocks in the loop too: every lane runs on past column
                     // w-1 (subject code 0xFF there) and keeps its column-(w-1) state
+#ifdef ANYSEQ_STAMPS
+                    ev_store(7, te_v);                               // main loop end
+                    ev_store(8, __builtin_amdgcn_s_memrealtime());   // epilogue entry
+#endif
                     int cap[4] = {w + lane - (int)bb * CH, g, e, fdn};   // steps until column w-1
 #define AF2_CALL(LV, BD, PB, LU)                                                                                     \
     st = aff2_loop_asm<LV, BD, PB, LU, true>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
-                                             fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)nchunks, cap)
+                                             fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), cap, dbp)
                     if (xs) {
                         if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
                     } else {
@@ -1428,6 +1471,9 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                         atomicOr(err, ERR_SPIN_TIMEOUT);
                         return;
                     }
+#ifdef ANYSEQ_STAMPS
+                    ev_store(9, te_v);   // epilogue end
+#endif
                     g = cap[1];
                     e = cap[2];
                     fdn = cap[3];
@@ -1470,8 +1516,8 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 const int bv = B.top(t0 + lane, nge);
                 const int bvr = xs ? to_x(bv, t0 + lane) : bv;   // rings hold the loop's space
                 io.my_ring[(t0 + lane) & IRM] = make_int2(bvr, bvr + go);
-            } else if (seen_prod < (uint32_t)(b + 1)) {
-                if (!(seen_prod = spin_lds_ge(io.my_prod, (uint32_t)(b + 1), err))) return;
+            } else if (seen_prod < (uint32_t)(2 * b + 2)) {
+                if (!(seen_prod = spin_lds_ge(io.my_prod, (uint32_t)(2 * b + 2), err))) return;
             }
             const int4* src = reinterpret_cast<const int4*>(io.my_ring + (t0 & IRM));
 #pragma unroll
@@ -1554,7 +1600,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         }
         if (!io.in_border && b < nchunks) lds_st(io.my_cons, (uint32_t)(b + 1));
         if (io.trailing) lds_st(io.tail, (uint32_t)(b + 1));
-        if (pub) lds_st(io.next_prod, (uint32_t)(j + 1));
+        if (pub) lds_st(io.next_prod, (uint32_t)(2 * j + 2));
     }
     if (!io.in_border) lds_st(io.my_cons, (uint32_t)(nchunks + kSlots));
     if (io.trailing) lds_st(io.tail, 0x7fffffffu);
@@ -1567,6 +1613,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         dbg[slot + 2] = __builtin_amdgcn_s_memrealtime();
         dbg[slot + 3] = t_b0 ? t_b0 : (uint64_t)nmiss;   // (asm path: prefetch misses)
     }
+    ev_store(10, __builtin_amdgcn_s_memrealtime());   // band end
 #endif
     if (!dead) {
         if (P.out_col) gmem(P.out_col)[row] = aff_to_h(g, row, w - 1, nge);
@@ -1606,7 +1653,10 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
     k.codes = nsym > 0 && nsym < 255;
     k.lut = nsym > 0 && nsym <= 8 && fp.lut_ok;
     k.slack = fp.slack;
-    if (fp.prio && wave < NW) __builtin_amdgcn_s_setprio(3);   // compute waves before the I/O wave
+    // issue priority: 1 = compute waves before the I/O wave, 2 = the I/O wave first (it
+    // sleeps when idle; its hand-off polls sit on the band chain)
+    if (fp.prio == 1 && wave < NW) __builtin_amdgcn_s_setprio(3);
+    if (fp.prio == 2 && wave == NW) __builtin_amdgcn_s_setprio(3);
     for (;;) {
         if (threadIdx.x == 0) {
             sh.group = (int32_t)atomicAdd(dq, 1u);
@@ -1639,7 +1689,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
             const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
             io_wave<32, true, int2>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0], &sh.s_filled,
                                     &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
-                                    P.nslots < P.ngroups - 1, 2);
+                                    P.nslots < P.ngroups - 1, 2, 2, fp.prio == 3,
+                                    fp.dbg && first < 2048 ? fp.dbg + 16 + 4 * 4096 + 16 * (first + (P.q_step < 0 ? 2048 : 0))
+                                                           : nullptr);
         } else {
             const int band = first + wave;
             if (band <= last) {

@@ -312,13 +312,14 @@ def gen_loop2(kind, border, pub, ts=False):
 
 # ------------------------------------------------------- affine, round 3 --
 # Registers of gen_aff2 (TOP pairs / cell pairs as gen_loop_aff).
-B_AW, B_AA, B_AT, B_AP = 192, 193, 194, 195   # cmp weight, diag + weight, temp, poll result
-B_SK0, B_SK1 = 196, 204                          # subject words (codes), double buffered
-B_VT, B_VT2, B_VA, B_VB = 212, 213, 214, 215    # temps / LDS addresses
-B_WB = 216                                       # LUT weight bytes of 4 steps
+B_AW, B_AA, B_AT, B_AP = 136, 137, 138, 139   # cmp weight, diag + weight, temp, poll result
+B_SK0, B_SK1 = 140, 148                          # subject words (codes), double buffered
+B_VT, B_VT2, B_VA, B_VB = 156, 157, 158, 159    # temps / LDS addresses
+B_WB = 160                                       # LUT weight bytes of 4 steps
 
 
-AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v191
+NEG_INF = -(1 << 29)   # kAffNeg
+AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
 def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
@@ -332,28 +333,29 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
     lut: the diagonal weight of 4 steps from ONE v_perm_b32 of the lane's 8-entry
          weight table (query code against subject codes 0..7; code 0xFF -> -1)
          and a byte-select SDWA add; else v_cmp + v_cndmask (any codes).
-    Per block: the top row's second half is read at the block start, the first
-    half was prefetched in the previous block (when the producer's counter, polled
-    at step 16, already covered the next chunk: bands start one block later than
-    the structural minimum, so in the steady state no poll waits); subject codes of
-    the next block at step 8; publishing by a shift register (lane 63's cells leave
-    through DPP wave_shl:1, one ds_write / global_store per block).
+    Hand-off in HALF chunks (16 columns; the ring counters count halves): lane 63's
+    cells leave through a DPP wave_shl:1 shift register, whose lanes 48..63 hold the
+    chunk's first 16 columns after step 16 and its last 16 at the block end -- one
+    ds_write_b64 / global_store_dwordx2 per half.  The consumer reads the first half of
+    its top row at the block start (waiting for half 2b) and the second half at step 14
+    (half 2b+1, polled at step 10), so a band trails the one above by about 2.6 blocks
+    (64 steps of skew + 16 of granularity + latency) instead of whole chunks.
+    Subject codes of the next block at step 8.
     epi: the band's last blocks (some lanes past the last column w-1): every lane keeps
-    computing (the subject code 0xFF beyond w matches nothing, so no extended cell
-    exceeds the real ones' best under the clamp), polls stop at chunk nch-1, and each
-    lane captures its state at column w-1 (per-lane countdown cnt) into gc / ec / fc."""
+    computing past w (subject code 0xFF; those cells feed no real cell), polls stop at
+    the last half (nch = 2 x chunks), the best takes real cells only, and each lane
+    captures its state at column w-1 (per-lane countdown cnt) into gc / ec / fc."""
     L = kind == "L"
     trailing = pub != "lds"
     out = []
     e = out.append
     sets = (B_SK0, B_SK1)
 
-    def top_reads(first, dst_b):
-        """8 ds_read_b128 of top-row pairs [16*first, 16*first+16) of block dst_b
-        (register x2 = dst_b's ring byte offset already in VB)."""
+    def top_reads(half):
+        """8 ds_read_b128 of top-row pairs [16*half, 16*half+16) (chunk address in VB)."""
         for i in range(8):
-            reg = AT0 + 32 * first + 4 * i
-            e(f"ds_read_b128 v[{reg}:{reg + 3}], v{B_VB} offset:{128 * first + 16 * i}")
+            reg = AT0 + 32 * half + 4 * i
+            e(f"ds_read_b128 v[{reg}:{reg + 3}], v{B_VB} offset:{128 * half + 16 * i}")
 
     def ring_addr(breg):
         # ring byte address of chunk `breg` into VB: rb + ((breg << 8) & 4095)
@@ -374,29 +376,82 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
         e(f"v_add_u32_e32 v{B_VA}, %[rb], v{B_VA}")
         e(f"ds_write_b64 v{B_VA}, v[{B_VT}:{B_VT2}]")
 
+    def half_target(add):
+        # x4 = 2b + add (clamped to the last half in the epilogue)
+        e("s_lshl_b32 %[x4], %[b], 1")
+        e(f"s_add_u32 %[x4], %[x4], {add}")
+        if epi:
+            e("s_min_u32 %[x4], %[x4], %[nch]")
+
+    EVB = 1000   # diagnostic build: the block whose hand-off events are recorded
+
+    def event(k, slot, bval):
+        """Diagnostic build: at block `bval` (b + const), store s_memrealtime to
+        dbp[slot] (vector store from v138:139; the record pointer is 0 when off)."""
+        if not ts:
+            return
+        e(f"s_cmp_eq_u32 %[b], {bval}")
+        e(f"s_cbranch_scc0 L_ev{slot}{k}_%=")
+        e("s_cmp_lg_u64 %[dbp], 0")
+        e(f"s_cbranch_scc0 L_ev{slot}{k}_%=")
+        e(f"s_memrealtime s[{TB}:{TB + 1}]")
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"v_mov_b32_e32 v138, s{TB}")
+        e(f"v_mov_b32_e32 v139, s{TB + 1}")
+        e(f"v_mov_b32_e32 v{B_VT2}, 0")
+        e(f"global_store_dwordx2 v{B_VT2}, v[138:139], %[dbp] offset:{8 * slot}")
+        e(f"L_ev{slot}{k}_%=:")
+
+    def count_miss(k, tag):
+        if ts:   # diagnostic: hand-off waits (block start or step 14)
+            e("s_cmp_ge_u32 %[sp], %[x4]")
+            e(f"s_cbranch_scc1 L_nm{tag}{k}_%=")
+            e("s_add_u32 %[nmiss], %[nmiss], 1")
+            e(f"L_nm{tag}{k}_%=:")
+
+    def publish(k, half, reg):
+        """Lanes 48..63 of the (G, F) pair `reg` hold 16 columns of chunk b-2: half
+        `half` of the next band's top row (LDS: always written -- a dummy slot and
+        counter 0 while b < 2 -- so the counted lgkmcnt waits stay fixed)."""
+        if pub == "glob":
+            e("s_cmp_lt_u32 %[b], 2")
+            e(f"s_cbranch_scc1 L_nopub{half}{k}_%=")
+        e("s_sub_u32 %[x2], %[b], 2")
+        e("s_lshl_b32 %[x2], %[x2], 8")
+        if pub == "lds":
+            e("s_and_b32 %[x2], %[x2], 4095")
+            e("s_add_u32 %[x2], %[x2], %[nb]")
+        e(f"v_add_u32_e32 v{B_VT}, %[x2], %[lo]")
+        e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
+        e("s_mov_b64 exec, %[hm]")
+        if pub == "lds":
+            e(f"ds_write_b64 v{B_VT}, v[{reg}:{reg + 1}] offset:{128 * half}")
+        else:
+            e(f"global_store_dwordx2 v{B_VT}, v[{reg}:{reg + 1}], %[gp] offset:{128 * half} sc1")
+        e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
+        if pub == "lds":
+            # counter: 2(b-2) + half + 1 halves published (0 while b < 2)
+            e("s_lshl_b32 %[x2], %[b], 1")
+            e(f"s_sub_u32 %[x2], %[x2], {3 - half}")
+            e("s_max_i32 %[x2], %[x2], 0")
+            e(f"v_mov_b32_e32 v{B_VT2}, %[x2]")
+            e(f"ds_write_b32 %[anp], v{B_VT2}")
+        if pub == "glob":
+            e(f"L_nopub{half}{k}_%=:")
+
     def body(k):
         cs, ns = sets[k], sets[1 - k]
         e("s_add_u32 %[x1], %[b], 1")
-        # ---- this block's top row
-        e("s_cmp_eq_u32 %[pf], 0")
-        e(f"s_cbranch_scc0 L_pfd{k}_%=")
-        if ts:
-            e("s_add_u32 %[nmiss], %[nmiss], 1")   # diagnostic: blocks whose top row was not prefetched
-        if border:
-            border_write("%[b]")
-            e("s_waitcnt lgkmcnt(0)")
-        else:
-            if epi:
-                e("s_min_u32 %[x4], %[x1], %[nch]")   # chunks >= nch are never published
-                wait(e, f"pr{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
-            else:
-                wait(e, f"pr{k}", "%[sp]", "%[x1]", "%[apr]", tmp=B_VT2)
+        event(k, 0, EVB + 2)          # producer: block EVB+2 starts
+        event(k, 3, EVB)              # consumer: block EVB starts
+        # ---- first half of this block's top row (half 2b)
+        if not border:
+            half_target(1)
+            count_miss(k, "a")
+            wait(e, f"pa{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
+        event(k, 4, EVB)              # consumer: first half of chunk EVB seen
         ring_addr("%[b]")
-        top_reads(0, "%[b]")
-        e(f"L_pfd{k}_%=:")
-        ring_addr("%[b]")
-        top_reads(1, "%[b]")
-        e("s_mov_b32 %[pf], 0")
+        top_reads(0)
         if ts:
             e("s_cmp_lg_u32 %[tsf], 0")
             e(f"s_cbranch_scc1 L_nots{k}_%=")
@@ -412,13 +467,12 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
             wait(e, f"bp{k}", "%[sc]", "%[x4]", "%[anc]", tmp=B_VT2)
             e(f"L_nobp{k}_%=:")
         g, f, dg = "%[cur]", "%[fd]", "%[dg]"
-        issued_s = False
-        issued_p = False
+        nsub = 5 if border else 4   # subject reads (+ the border write) at step 8
         for u in range(32):
             if u == 8:
                 # next block's subject codes (other register set) and, band 0, its border.
-                # The reads are issued in every block (after the last one they read a stale
-                # slot, unused): the counted lgkmcnt waits below assume they are in flight.
+                # Issued in every block (after the last one they read a stale slot, unused):
+                # the counted lgkmcnt waits assume they are in flight.
                 e("s_cmp_ge_u32 %[x1], %[be]")
                 e(f"s_cbranch_scc1 L_nopf{k}_%=")
                 e("s_add_u32 %[x4], %[b], 2")
@@ -431,35 +485,26 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
                     e(f"ds_read2st64_b32 v[{ns + 2 * i}:{ns + 2 * i + 1}], v{B_VA} offset0:{2 * i} offset1:{2 * i + 1}")
                 if border:
                     border_write("%[x1]")
-                issued_s = True
-            if u == 16 and not border:
-                # poll the producer's counter for the next chunk (result used at step 24)
+            if u == 10 and not border:
+                # poll the producer's counter for the second half (used at step 14)
                 e(f"ds_read_b32 v{B_AP}, %[apr]")
-                issued_p = True
-            if u == 24:
+            if u == 14:
                 e("s_waitcnt lgkmcnt(0)")
-                e("s_cmp_ge_u32 %[x1], %[be]")
-                e(f"s_cbranch_scc1 L_noq{k}_%=")
                 if not border:
                     e(f"v_readfirstlane_b32 %[x2], v{B_AP}")
                     e("s_max_u32 %[sp], %[sp], %[x2]")
-                    e("s_add_u32 %[x4], %[b], 2")
-                    if epi:
-                        e("s_min_u32 %[x4], %[x4], %[nch]")
-                    e("s_cmp_ge_u32 %[sp], %[x4]")
-                    e(f"s_cbranch_scc0 L_noq{k}_%=")
-                ring_addr("%[x1]")
-                top_reads(0, "%[x1]")
-                e("s_mov_b32 %[pf], 1")
-                e(f"L_noq{k}_%=:")
-            if 1 <= u <= 23 and u % 2 == 1:
-                ns_ = (5 if border else 4) if issued_s else 0   # subject reads (+ border write)
-                if u <= 15:
-                    i = (u + 1) // 2                       # first-half read holding T(u-1)
-                    allowed = (8 - i) + 8 + ns_
-                else:
-                    i = (u - 15) // 2                      # second-half read holding T(u-1)
-                    allowed = (8 - i) + ns_ + (1 if issued_p else 0)
+                    half_target(2)
+                    count_miss(k, "b")
+                    wait(e, f"pb{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
+                    event(k, 5, EVB)      # consumer: second half seen
+                top_reads(1)
+            if u in (1, 3, 5, 7, 9, 11, 13):
+                i = (u - 1) // 2                   # first-half read holding T(u-1)
+                allowed = (7 - i) + (nsub if u > 8 else 0) + (1 if (u > 10 and not border) else 0)
+                e(f"s_waitcnt lgkmcnt({min(15, allowed)})")
+            if u >= 17 and u % 2 == 1:
+                i = (u - 17) // 2                  # second-half read holding T(u-1)
+                allowed = (7 - i) + (2 if pub == "lds" else 0)
                 e(f"s_waitcnt lgkmcnt({min(15, allowed)})")
             sw = v(cs + u // 4)
             tg = "%[tfg]" if u == 0 else TG_(u - 1)
@@ -484,17 +529,25 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
             e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
             e(f"v_max_i32_e32 {OF_(u)}, {tf}, %[hg]")
             if epi:
+                if L:
+                    # best over real cells only (cnt >= 0: column <= w-1)
+                    e(f"v_max_i32_e32 v{B_AT}, %[best], {OG_(u)}")
+                    e("v_cmp_le_i32_e32 vcc, 0, %[cnt]")
+                    e(f"v_cndmask_b32_e32 %[best], %[best], v{B_AT}, vcc")
                 # the lane whose cell is column w-1 at this step keeps its state
                 e("v_cmp_eq_u32_e32 vcc, 0, %[cnt]")
                 e(f"v_cndmask_b32_e32 %[gc], %[gc], {OG_(u)}, vcc")
                 e("v_cndmask_b32_e32 %[ec], %[ec], %[e], vcc")
                 e(f"v_cndmask_b32_e32 %[fc], %[fc], {OF_(u)}, vcc")
                 e("v_add_u32_e32 %[cnt], -1, %[cnt]")
-            if L and u % 2 == 1:
+            if L and u % 2 == 1 and not epi:
                 e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
             if u >= 2 and pub != "none":
                 e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            if u == 16 and pub != "none":
+                publish(k, 0, AO0 + 6)             # cell pair of step 15: steps 0..15 in lanes 48..63
+                event(k, 1, EVB + 2)               # producer: first half of chunk EVB published
             g, f, dg = OG_(u), OF_(u), tg
         e(f"v_mov_b32_e32 %[cur], {OG_(31)}")
         e(f"v_mov_b32_e32 %[fd], {OF_(31)}")
@@ -505,26 +558,9 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
         e(f"v_mov_b32_e32 %[tfg], {TG_(31)}")
         e(f"v_mov_b32_e32 %[tff], {TF_(31)}")
         if pub != "none":
-            e("s_cmp_lt_u32 %[b], 2")
-            e(f"s_cbranch_scc1 L_nopub{k}_%=")
-            e("s_sub_u32 %[x2], %[b], 2")
-            e("s_lshl_b32 %[x2], %[x2], 8")
-            if pub == "lds":
-                e("s_and_b32 %[x2], %[x2], 4095")
-                e("s_add_u32 %[x2], %[x2], %[nb]")
-            e(f"v_add_u32_e32 v{B_VT}, %[x2], %[lo]")
-            e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
-            e("s_mov_b64 exec, %[hm]")
-            if pub == "lds":
-                e(f"ds_write_b64 v{B_VT}, v[{AO0 + 62}:{AO0 + 63}]")
-            else:
-                e(f"global_store_dwordx2 v{B_VT}, v[{AO0 + 62}:{AO0 + 63}], %[gp] sc1")
-            e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
-            if pub == "lds":
-                e("s_sub_u32 %[x2], %[b], 1")
-                e(f"v_mov_b32_e32 v{B_VT2}, %[x2]")
-                e(f"ds_write_b32 %[anp], v{B_VT2}")
-            e(f"L_nopub{k}_%=:")
+            publish(k, 1, AO0 + 6)                 # pair of step 31: steps 16..31 in lanes 48..63
+            event(k, 2, EVB + 2)                   # producer: second half published
+        event(k, 6, EVB)                           # consumer: block EVB ends
         e(f"v_mov_b32_e32 v{B_VT2}, %[x1]")
         if not border:
             e(f"ds_write_b32 %[acn], v{B_VT2}")
@@ -532,7 +568,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
             e(f"ds_write_b32 %[atl], v{B_VT2}")
         e("s_mov_b32 %[b], %[x1]")
 
-    # the first block's subject codes into set 0
+    # the first block's subject codes into set 0 (band 0: and its border)
     e("s_add_u32 %[x1], %[b], 1")
     wait(e, "sfp", "%[sf]", "%[x1]", "%[asf]", tmp=B_VT2)
     e("s_and_b32 %[x2], %[b], 31")
@@ -540,6 +576,8 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
     e(f"v_add_u32_e32 v{B_VA}, %[x2], %[skb]")
     for i in range(4):
         e(f"ds_read2st64_b32 v[{B_SK0 + 2 * i}:{B_SK0 + 2 * i + 1}], v{B_VA} offset0:{2 * i} offset1:{2 * i + 1}")
+    if border:
+        border_write("%[b]")
     e("s_waitcnt lgkmcnt(0)")
     e("L_top_%=:")
     body(0)
@@ -571,11 +609,13 @@ def TF_(u):
 
 
 def OG_(u):
-    return v(AO0 + 2 * u)
+    # step u's cell pair: four pairs in rotation -- a cell is read by the next step
+    # (DPP source, best) and then holds the publishing shift register for one step
+    return v(AO0 + 2 * (u % 4))
 
 
 def OF_(u):
-    return v(AO0 + 2 * u + 1)
+    return v(AO0 + 2 * (u % 4) + 1)
 
 
 def main():

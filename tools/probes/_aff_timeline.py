@@ -20,8 +20,9 @@ q = q[:rows]
 path = out + ".txt"
 os.environ["ANYSEQ_TIMELINE"] = ""
 A.score(kind, q, s, gap_open=-2, gap_extend=-1)
-if os.path.exists(path):
-    os.remove(path)
+for f_ in (path, path + ".ev"):
+    if os.path.exists(f_):
+        os.remove(f_)
 os.environ["ANYSEQ_TIMELINE"] = path
 v = A.score(kind, q, s, gap_open=-2, gap_extend=-1)
 os.environ["ANYSEQ_TIMELINE"] = ""
@@ -60,3 +61,49 @@ for front, sel in (("fwd", a[:, 0] < 2048), ("rev", a[:, 0] >= 2048)):
         print(f"   into slot {k}: start lag {np.median(d[m]):.3f}, end lag {np.median(de[m]):.3f}")
     q4 = len(d) // 4
     print("  start lag by chain quarter:", " ".join(f"{np.mean(d[i*q4:(i+1)*q4]):.3f}" for i in range(4)))
+
+# hand-off events of block 1000 (producer: its block 1002) per band, 10 ns ticks
+if os.path.exists(path + ".ev"):
+    ev = {}
+    for ln in open(path + ".ev"):
+        if ln.startswith("#"):
+            continue
+        x = [int(t) for t in ln.split()]
+        ev[x[0]] = x[1:]
+    for front, off in (("fwd", 0), ("rev", 2048)):
+        lat1, lat2, wa, lagb, blk = [], [], [], [], []
+        kinds = []
+        for k in range(2047):
+            p, c = ev.get(off + k), ev.get(off + k + 1)
+            if not p or not c or not all(p[:3]) or not all(c[3:7]):
+                continue
+            kinds.append((k + 1) % NW == 0)
+            lat1.append((c[4] - p[1]) / 100.0)
+            lat2.append((c[5] - p[2]) / 100.0)
+            wa.append((c[4] - c[3]) / 100.0)
+            lagb.append((c[3] - p[0]) / 100.0)
+            blk.append((c[6] - c[3]) / 100.0)
+        if not lat1:
+            continue
+        tr = [(v[8] - v[7]) / 100.0 for v in (ev.get(off + k) for k in range(2048)) if v and len(v) > 10 and v[7] and v[8]]
+        ep = [(v[9] - v[8]) / 100.0 for v in (ev.get(off + k) for k in range(2048)) if v and len(v) > 10 and v[9] and v[8]]
+        tl = [(v[10] - v[9]) / 100.0 for v in (ev.get(off + k) for k in range(2048)) if v and len(v) > 10 and v[10] and v[9]]
+        io = [((v[11] - p[1]) / 100.0, (v[11] - v[12]) / 100.0, (v[4] - v[11]) / 100.0)
+              for k in range(1, 2048) for v, p in [(ev.get(off + k), ev.get(off + k - 1))]
+              if v and p and len(v) > 12 and v[11] and p[1] and v[4]]
+        if io:
+            a = np.array(io)
+            print(f"  {front} HBM hop via the I/O wave: producer publish -> I/O sees it {np.median(a[:, 0]):.3f} us "
+                  f"(that poll's round trip {np.median(a[:, 1]):.3f} us); I/O -> consumer sees it {np.median(a[:, 2]):.3f} us")
+        if tr:
+            print(f"  {front}: main loop end -> epilogue entry median {np.median(tr):.3f} us; epilogue "
+                  f"{np.median(ep):.3f} us; epilogue end -> band end {np.median(tl):.3f} us")
+        kinds = np.array(kinds)
+        for name, sel in (("LDS", ~kinds), ("HBM", kinds)):
+            if sel.sum() == 0:
+                continue
+            m = lambda a: np.median(np.array(a)[sel])
+            print(f"  {front} {name} hops ({sel.sum()}): publish->seen first half {m(lat1):.3f} us, "
+                  f"second half {m(lat2):.3f} us; consumer block-start wait {m(wa):.3f} us; "
+                  f"consumer block 1000 start - producer block 1002 start {m(lagb):.3f} us; "
+                  f"consumer block time {m(blk):.3f} us")
