@@ -65,6 +65,10 @@ hipError_t anyseq_launch_seq_codes(const uint8_t* q, int n, const uint8_t* s, in
 hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
                                       int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows,
                                       hipStream_t st);
+hipError_t anyseq_launch_aff_level_plan(const AffLevelPlan* plan, hipStream_t st);
+hipError_t anyseq_launch_fill_prep_planned(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
+                                           void* sent, size_t sent_max_bytes, uint32_t sent_value,
+                                           const uint32_t* sent_n16, hipStream_t st);
 }
 
 namespace anyseq {
@@ -291,6 +295,7 @@ void init_tuning_locked() {
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
+    g_tuning.devplan = env_int("ANYSEQ_AFF_DEVPLAN", g_tuning.devplan);
     g_tuning_init = true;
 }
 
@@ -1005,22 +1010,12 @@ DPProblem aff_problem(const uint8_t* dq, int q_off, int q_step, int h, const uin
 
 // Border mode of a free start / end (oracle free_bm): local clamps everywhere,
 // semiglobal opens the side border only at the matrix edge.
-int free_bm(int kind, bool at_edge) {
-    return kind == KIND_LOCAL ? BM_FREE_LOCAL : (at_edge ? BM_FREE_SEMI_OPEN : BM_FREE_SEMI);
-}
+int free_bm(int kind, bool at_edge) { return aff_free_bm(kind, at_edge); }
 
 // The same borders with query and subject swapped (a transposed half).
-int transposed_bm(int bm) {
-    return bm == BM_EFREE ? BM_FFREE : bm == BM_EPAID ? BM_FPAID : bm == BM_FREE_SEMI ? BM_FREE_SEMI_T : bm;
-}
+int transposed_bm(int bm) { return aff_transposed_bm(bm); }
 
-struct RowToColJob {   // anyseq_kernels.hip RowToCol
-    const void* row;
-    int32_t* H;
-    int32_t* E;
-    int32_t n, hlast;
-    int32_t xs, pad_;     // the row holds X-space values (amode != 0)
-};
+using RowToColJob = RowToCol;   // anyseq_internal.h
 
 // One Hirschberg half: rows qoff + qstep*r (r < h) of the query against columns
 // soff + sstep*c (c < w) of the subject, border mode bm, kind bits amode; its last
@@ -1138,6 +1133,183 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
     };
     double t_wake = now_us();
+    // the device plan sizes the hand-off rows for the worst split of every level; past a
+    // few GB (genome-length halves) the host-built levels keep the exact sizes
+    auto plan_rowbuf_bytes = [&]() {
+        const int NWa = g_tuning.NWa == 3 ? 3 : 4;
+        size_t mx = 0;
+        for (int p2 = pw; p2 > MIN_PART_WIDTH_HB; p2 /= 2) {
+            const int h2 = p2 / 2, parts = (m + h2 - 1) / p2;
+            const int maxh = g_tuning.afft ? h2 : std::max(h2, n);
+            const int bound = std::max(1, ((maxh + 63) / 64 + NWa - 1) / NWa);
+            const int grid = std::max(1, std::min(g_tuning.grida > 0 ? g_tuning.grida : E.num_cus, 2 * parts * bound));
+            const int want = std::max(g_tuning.ring_slots > 0 ? g_tuning.ring_slots : 4 * grid + 4, 2 * grid + 2);
+            const int64_t cols = std::min<int64_t>((int64_t)n + (int64_t)parts * h2, (int64_t)parts * std::max(n, h2)) +
+                                 64 * (int64_t)parts;
+            mx = std::max(mx, (size_t)std::min(bound - 1, want) * 2 * (size_t)cols * 2 * 4);
+        }
+        return mx;
+    };
+    if (!sharded && g_tuning.devplan && plan_rowbuf_bytes() <= ((size_t)8 << 30)) {
+        // Device-planned levels: every level is enqueued up front -- plan
+        // (aff_level_plan_kernel builds the level from the splits on the device), prep,
+        // fill, row-to-column, join -- and the splits come back in ONE download after the
+        // last level, instead of a download and a host rebuild per level.
+        const int NWa = g_tuning.NWa == 3 ? 3 : 4;
+        struct Lev {
+            int pw, half, parts, bpp, bound, nh, slots, grid, want;
+            size_t rowbuf_bytes;
+        };
+        std::vector<Lev> lv;
+        size_t max_meta = 0, max_rowbuf = 0, max_rowpool = 0, max_joinbuf = 0;
+        int max_parts = 1;
+        const int nsl = std::max(1, (n + 1 + 4095) / 4096);   // join slices of the longest possible part
+        for (int p2 = pw, b2 = sp.bpp; p2 > MIN_PART_WIDTH_HB; p2 /= 2, b2 /= 2) {
+            Lev L;
+            L.pw = p2;
+            L.half = p2 / 2;
+            L.parts = (m + L.half - 1) / p2;
+            L.bpp = b2;
+            // a half runs at most `half` rows (taller ones transposed), else up to n
+            const int maxh = g_tuning.afft ? L.half : std::max(L.half, n);
+            L.bound = std::max(1, ((maxh + 63) / 64 + NWa - 1) / NWa);
+            L.nh = 2 * L.parts;
+            L.slots = L.nh * L.bound;
+            const int grid0 = g_tuning.grida > 0 ? g_tuning.grida : E.num_cus;
+            L.grid = std::max(1, std::min(grid0, L.slots));
+            const int min_slots = 2 * L.grid + 2;
+            L.want = std::max(g_tuning.ring_slots > 0 ? g_tuning.ring_slots : 2 * min_slots, min_slots);
+            // hand-off rows: a half's pitch is max(len, width) rounded up, Sum max(len_p, half)
+            // <= min(n + parts*half, parts*max(n, half))
+            const int64_t cols = std::min<int64_t>((int64_t)n + (int64_t)L.parts * L.half,
+                                                   (int64_t)L.parts * std::max(n, L.half)) +
+                                 64 * (int64_t)L.parts;
+            L.rowbuf_bytes = (size_t)std::min(L.bound - 1, L.want) * 2 * (size_t)cols * 2 * 4;
+            const size_t meta = (((32 + (size_t)L.slots) * 4 + 255) & ~(size_t)255) +
+                                (size_t)L.nh * sizeof(DPProblem) + (size_t)L.slots * sizeof(GroupRef);
+            max_meta = std::max(max_meta, meta);
+            max_rowbuf = std::max(max_rowbuf, L.rowbuf_bytes);
+            max_rowpool = std::max(max_rowpool, (size_t)2 * ((size_t)n + 64 * (size_t)L.parts) * 2 * 4);
+            max_joinbuf = std::max(max_joinbuf, (size_t)L.parts * nsl * 8);
+            max_parts = std::max(max_parts, L.parts);
+            lv.push_back(L);
+        }
+        const int nlev = (int)lv.size();
+        // every allocation before the first enqueue (growth may synchronise the device)
+        char* meta = (char*)E.pl_meta.get(std::max<size_t>(max_meta, 256));
+        int32_t* rowbuf = (int32_t*)E.pl_rowbuf.get(std::max<size_t>(max_rowbuf, 16));
+        int32_t* rowpool = (int32_t*)E.outrow.get(std::max<size_t>(max_rowpool, 16));
+        PartInfo* d_parts = (PartInfo*)E.pl_parts.get((size_t)max_parts * sizeof(PartInfo));
+        RowToCol* d_jobs = (RowToCol*)E.pl_jobs.get((size_t)2 * max_parts * sizeof(RowToCol));
+        int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * max_parts * 4);
+        void* partial = E.joinbuf.get(std::max<size_t>(max_joinbuf, 16));
+        uint32_t* d_tail = (uint32_t*)E.pl_hdr.get((size_t)(std::max(nlev, 1) * 5) * 4 + 16);   // hdr (4) | err
+        uint32_t* d_hdr = d_tail;                       // 4 words per level
+        uint32_t* d_err = d_tail + 4 * nlev;            // 1 word per level
+        uint32_t* h_tail = (uint32_t*)E.pl_pin.get((size_t)(std::max(nlev, 1) * 5) * 4 + 16);
+        while ((int)E.pl_ev.size() < 2 * nlev) {
+            hipEvent_t ev;
+            HIPCHECK(hipEventCreate(&ev));
+            E.pl_ev.push_back(ev);
+        }
+        if (check_ptrs_enabled()) {
+            register_static_range(meta, max_meta);
+            register_static_range(rowbuf, max_rowbuf);
+            register_static_range(rowpool, max_rowpool);
+        }
+        HIPCHECK(hipMemsetAsync(d_err, 0, (size_t)nlev * 4, st));
+        static std::atomic<int32_t> g_plan_epoch{0x40000};
+        uint32_t* ctr = (uint32_t*)meta;
+        for (int li = 0; li < nlev; ++li) {
+            const Lev& L = lv[li];
+            g_stage_level = li + 1;
+            const size_t zb = ((32 + (size_t)L.slots) * 4 + 255) & ~(size_t)255;
+            DPProblem* d_probs = (DPProblem*)(meta + zb);
+            GroupRef* d_groups = (GroupRef*)(meta + zb + (size_t)L.nh * sizeof(DPProblem));
+            const int32_t epoch = (g_plan_epoch.fetch_add(1) + 1) & 0x7ffff;
+            AffLevelPlan A{};
+            A.parts = L.parts;
+            A.bpp = L.bpp;
+            A.nb = sp.nb;
+            A.half = L.half;
+            A.pw = L.pw;
+            A.m = m;
+            A.n = n;
+            A.kind = kind;
+            A.best_bits = local ? AM_BEST_ALL : AM_BEST_LAST;
+            A.afft = g_tuning.afft ? 1 : 0;
+            A.NW = NWa;
+            A.want_slots = L.want;
+            A.bound = L.bound;
+            A.epoch = epoch;
+            A.q = cq;
+            A.s = cs;
+            A.LH = LH0;
+            A.LE = LE0;
+            A.RH = RH0;
+            A.RE = RE0;
+            A.pbest = pbest;
+            A.rowpool = rowpool;
+            A.rowbuf = rowbuf;
+            A.flags = ctr + 32;
+            A.spl = d_spl;
+            A.typ = d_typ;
+            A.score = li == 0 ? nullptr : d_score;
+            A.parts_out = d_parts;
+            A.probs = d_probs;
+            A.groups = d_groups;
+            A.jobs = d_jobs;
+            A.hdr = d_hdr + 4 * li;
+            HIPCHECK(anyseq_launch_aff_level_plan(&A, st));
+            HIPCHECK(anyseq_launch_fill_prep_planned(ctr, 32 + L.slots, pbest, 2 * L.parts, kAffNegH, rowbuf,
+                                                     L.rowbuf_bytes, 0x80808080u, d_hdr + 4 * li, st));
+            FillParams fpl = fp;
+            fpl.epoch = epoch;
+            fpl.prio = g_tuning.prio;
+            fpl.throttle = g_tuning.thr;
+            fpl.slack = g_tuning.slack;
+            fpl.dbg = nullptr;
+            HIPCHECK(hipEventRecord(E.pl_ev[2 * li], st));
+            HIPCHECK(anyseq_launch_fill_affine(NWa, d_probs, d_groups, L.slots, ctr, d_err + li, &fpl, L.grid, st));
+            HIPCHECK(hipEventRecord(E.pl_ev[2 * li + 1], st));
+            HIPCHECK(anyseq_launch_aff_row_to_col(d_jobs, L.nh, n, -sc.gap_extend, st));
+            HIPCHECK(anyseq_launch_aff_hb_join2(d_parts, L.parts, n, L.half, LH0, LE0, RH0, RE0, pbest, sc.gap_open,
+                                                sc.gap_extend, partial, d_spl, d_typ, li == 0 ? d_score : nullptr, st));
+            stage_check(st, "affine level (device plan)");
+        }
+        HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + 1) * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(h_tail, d_tail, (size_t)nlev * 5 * 4, hipMemcpyDeviceToHost, st));
+        {
+            const hipError_t e = stream_wait_spin(st);
+            if (e != hipSuccess) fail("affine construct levels failed: %s", hipGetErrorString(e));
+        }
+        for (int li = 0; li < nlev; ++li) {
+            const uint32_t err = h_tail[4 * nlev + li];
+            g_stage_level = li + 1;
+            if (err & ERR_BAD_DESC) fail("fill kernel read a corrupt problem descriptor (error %u; planned level %d)", err, li + 1);
+            if (err) fail("fill kernel reported error %u (spin timeout; planned level %d)", err, li + 1);
+            if (h_tail[4 * li + 1]) fail("internal: planned level %d: a half exceeds its group slots", li + 1);
+            float ms = 0.f;
+            HIPCHECK(hipEventElapsedTime(&ms, E.pl_ev[2 * li], E.pl_ev[2 * li + 1]));
+            g_fill_ms += ms;
+            g_fill_launches += 1;
+            uint64_t cells;
+            memcpy(&cells, h_tail + 4 * li + 2, 8);
+            g_fill_cells += (int64_t)cells;
+        }
+        memcpy(sp.v.data(), h_status, nsv * 4);
+        memcpy(typ.data(), h_status + nsv, nsv * 4);
+        // the splits run from 0 to n, in order, each with a known type
+        for (size_t i = 1; i < nsv; ++i)
+            if (sp.v[i] < sp.v[i - 1] || sp.v[i] > n || typ[i] < T_H || typ[i] > T_AFTER)
+                fail("internal: planned levels left split %zu = %d (type %d)", i - 1, sp.v[i], typ[i]);
+        if (nlev > 0) {
+            const int32_t s32 = h_status[2 * nsv];
+            score = kind == KIND_SEMIGLOBAL ? std::max(s32, 0) : s32;
+            if (kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
+        }
+        pw = MIN_PART_WIDTH_HB;   // (the host loop below has nothing left)
+    }
     while (pw > MIN_PART_WIDTH_HB) {
         const int half = pw / 2;
         const int parts = (m + half - 1) / pw;
@@ -1650,6 +1822,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "throttle") g_tuning.thr = value;
     else if (n == "affine_lut") g_tuning.afflut = value;
     else if (n == "slack") g_tuning.slack = value;
+    else if (n == "affine_device_plan") g_tuning.devplan = value;
     else return -1;
     return 0;
 }

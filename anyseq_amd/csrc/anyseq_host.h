@@ -91,6 +91,7 @@ struct Tuning {
     int thr = 0;         // band 0 of every problem sleeps thr s_sleep-1 units per block (chain pace)
     int afflut = 1;      // affine fill: v_perm weight table when the pair has <= 8 symbols
     int slack = 0;       // affine fill: half chunks a band starts behind the structural minimum
+    int devplan = 1;     // affine construct: Hirschberg levels planned on the device (one download)
 };
 extern Tuning g_tuning;
 
@@ -141,6 +142,11 @@ struct Engine {
     DevBuf jobs;
     DevBuf codes, codemeta;    // alphabet codes of the current pair (prepare_codes)
     DevBuf vstr;               // sharded construct, emulated ranks: their ' '-filled strings
+    // affine construct, device-planned levels: launch block, hand-off rows, part table,
+    // row-to-column jobs, per-level header and error words (+ their pinned download)
+    DevBuf pl_meta, pl_rowbuf, pl_parts, pl_jobs, pl_hdr;
+    PinBuf pl_pin;
+    std::vector<hipEvent_t> pl_ev;
     explicit Engine(int dev);
 };
 

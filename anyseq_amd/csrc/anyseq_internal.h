@@ -159,6 +159,58 @@ struct BlockInfo {
     int32_t xi, xj;       // affine construct, free end: the exit cell (written by aff_pred_kernel)
 };
 
+// Border mode of a free start / end (oracle free_bm): local clamps everywhere.
+__host__ __device__ inline int32_t aff_free_bm(int kind, bool at_edge) {
+    return kind == KIND_LOCAL ? BM_FREE_LOCAL : (at_edge ? BM_FREE_SEMI_OPEN : BM_FREE_SEMI);
+}
+// The same borders with query and subject swapped (a transposed half).
+__host__ __device__ inline int32_t aff_transposed_bm(int bm) {
+    return bm == BM_EFREE ? BM_FFREE : bm == BM_EPAID ? BM_FPAID : bm == BM_FREE_SEMI ? BM_FREE_SEMI_T : bm;
+}
+
+// Transposed Hirschberg half: its bottom row (G, F-down pairs) is the
+// original's last column (H, E-right) -> H space (aff_row_to_col_kernel).
+struct RowToCol {
+    const void* row;
+    int32_t* H;
+    int32_t* E;
+    int32_t n;      // columns of the transposed problem (rows of the original)
+    int32_t hlast;  // last row of the transposed problem
+    int32_t xs;     // the row holds X-space values (DPProblem::amode != 0)
+    int32_t pad_;
+};
+
+// Device-planned Hirschberg level of the affine construct (DESIGN.md §3.6,
+// aff_level_plan_kernel): the level's part table, half descriptors, group table and
+// row-to-column jobs are built on the device from the previous level's splits, so the
+// host enqueues every level without reading anything back.  Slots are fixed by the
+// level's geometry: half 2p / 2p+1 of part p (h = 0 when the part has no halves) and
+// `bound` groups per half (a half spans at most `half` columns, so a transposed or
+// square half has at most ceil(half / 64) bands); a group past its half's ngroups is
+// skipped by the fill (DPProblem::pad_ = kPlannedDesc).
+constexpr int32_t kPlannedDesc = 1;
+struct AffLevelPlan {
+    int32_t parts, bpp, nb, half, pw, m, n, kind;
+    int32_t best_bits;     // AM_BEST_ALL (local) or AM_BEST_LAST (semiglobal / global)
+    int32_t afft;          // halves taller than wide run transposed
+    int32_t NW, want_slots, bound, epoch;
+    const uint8_t* q;      // alphabet codes of the pair
+    const uint8_t* s;
+    int32_t *LH, *LE, *RH, *RE;   // the level's columns
+    int32_t* pbest;               // 2 per part
+    int32_t* rowpool;             // transposed halves' bottom rows
+    int32_t* rowbuf;              // group -> group hand-off rows (sentinel-filled by the prep)
+    uint32_t* flags;              // group flags: `bound` per half
+    const int32_t* spl;           // the splits / types so far (storage index = logical + 1)
+    const int32_t* typ;
+    const int32_t* score;         // level-1 join value (levels >= 2; null at level 1)
+    PartInfo* parts_out;
+    DPProblem* probs;             // 2 * parts
+    GroupRef* groups;             // 2 * parts * bound, k-major
+    RowToCol* jobs;               // per half (n = 0: not transposed)
+    uint32_t* hdr;                // [0] sentinel uint4s of rowbuf, [2..3] cells (u64)
+};
+
 // Affine final level (aff_predwalk_kernel): blocks of at most `lds_rows` rows (the
 // launch's tallest block, at most kPredLdsMaxRows) keep their predecessor bytes and
 // query rows and subject columns in LDS ((rows + 127) x 128 + rows + 128 bytes,

@@ -1673,9 +1673,14 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
         const GroupRef gr = groups[gi];
         const DPProblem P = probs[gr.prob];
         if (gr.epoch != fp.epoch || gr.check != group_check(gr.prob, gr.group, gr.epoch) ||
-            P.magic != prob_magic(&probs[gr.prob], gr.prob, fp.epoch) || gr.group >= P.ngroups) {
+            P.magic != prob_magic(&probs[gr.prob], gr.prob, fp.epoch) ||
+            (gr.group >= P.ngroups && P.pad_ != kPlannedDesc)) {
             if (threadIdx.x == 0) atomicOr(err, ERR_BAD_DESC);
             break;
+        }
+        if (gr.group >= P.ngroups) {   // a device-planned level's unused group slot
+            __syncthreads();
+            continue;
         }
         const int first = gr.group * NW;
         const int last = min(P.nbands, first + NW) - 1;
@@ -2351,22 +2356,200 @@ __global__ void aff_hb_join_final_kernel(const PartInfo* __restrict__ parts, int
 // E-right = max(E, H + go) instead of E changes no join decision: an E candidate
 // that only its H + go term lifts never exceeds the H candidate of its row, which
 // is tried first.
-struct RowToCol {
-    const int2* row;
-    int32_t* H;
-    int32_t* E;
-    int32_t n;      // columns of the transposed problem (rows of the original)
-    int32_t hlast;  // last row of the transposed problem
-    int32_t xs;     // the row holds X-space values (DPProblem::amode != 0)
-    int32_t pad_;
-};
 __global__ void aff_row_to_col_kernel(const RowToCol* __restrict__ jobs, int nge) {
     const RowToCol J = jobs[blockIdx.y];
     for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < J.n; c += blockDim.x * gridDim.x) {
-        const int2 v = J.row[c];
+        const int2 v = reinterpret_cast<const int2*>(J.row)[c];
         const int z = (J.hlast + (J.xs ? 0 : c) + 2) * nge;
         J.H[c] = v.x - z;
         J.E[c] = v.y - z;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Device-planned Hirschberg level (AffLevelPlan): the host-side
+// level builder of the affine construct (anyseq_engine.cpp add_half / fill_prepare)
+// restated on the device, one workgroup: part table, the two half descriptors of
+// every part (transposed when taller than wide), their hand-off ring and flag slots,
+// the k-major group table and the row-to-column jobs.  Hand-off rows and transposed
+// bottom rows are packed by block-wide exclusive scans over the parts in order.
+struct AffHalfGeo {
+    int32_t h, w;          // the problem as run (transposed: subject columns as rows)
+    int32_t tr, ngroups, nslots, wpad;
+    int64_t rowbuf;        // hand-off ring ints
+    int64_t rowpool;       // transposed bottom row ints
+};
+__device__ AffHalfGeo aff_half_geo(const AffLevelPlan& a, int len, int width) {
+    AffHalfGeo g{};
+    if (len <= 0) return g;
+    g.tr = a.afft && len > width;
+    g.h = g.tr ? width : len;
+    g.w = g.tr ? len : width;
+    const int nbands = (g.h + 63) / 64;
+    g.ngroups = (nbands + a.NW - 1) / a.NW;
+    g.wpad = (g.w + 63) & ~63;
+    g.nslots = max(1, min(g.ngroups - 1, a.want_slots));
+    g.rowbuf = g.ngroups > 1 ? (int64_t)g.nslots * g.wpad * 2 : 0;
+    g.rowpool = g.tr ? (int64_t)((len + 63) & ~63) * 2 : 0;
+    return g;
+}
+
+// block-wide exclusive scan (1024 threads) of one 64-bit value; returns the prefix,
+// *total the tile's sum
+__device__ int64_t block_scan_excl(int64_t v, int64_t* sh, int64_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wv] = x;
+    __syncthreads();
+    if (tid == 0) {
+        int64_t acc = 0;
+        for (int i = 0; i < 16; ++i) {
+            const int64_t t = sh[i];
+            sh[i] = acc;
+            acc += t;
+        }
+        sh[16] = acc;
+    }
+    __syncthreads();
+    const int64_t r = sh[wv] + x - v;
+    *total = sh[16];
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(1024) void aff_level_plan_kernel(const AffLevelPlan a) {
+    __shared__ int64_t sh[17];
+    __shared__ unsigned long long cells;
+    __shared__ int32_t bad;
+    if (threadIdx.x == 0) {
+        cells = 0;
+        bad = 0;
+    }
+    __syncthreads();
+    // kind != global with a level-1 value <= 0: the empty alignment, no halves
+    const bool stop = a.score && a.kind != KIND_GLOBAL && *a.score <= 0;
+    RowToCol* jobs = a.jobs;
+    int64_t rb_base = 0, rp_base = 0;
+    for (int t0 = 0; t0 < a.parts; t0 += 1024) {
+        const int p = t0 + (int)threadIdx.x;
+        PartInfo pi{};
+        AffHalfGeo gl{}, gr{};
+        int off = 0, len = 0, hoj_l = 0, hoj_r = 0, hw = 0;
+        bool sfree = false, efree = false;
+        if (p < a.parts) {
+            const int sb = p * a.bpp - 1, eb = min((p + 1) * a.bpp - 1, a.nb - 1);
+            const int ts = a.typ[sb + 1], te = a.typ[eb + 1];
+            pi.split_index = p * a.bpp + a.bpp / 2 - 1;
+            off = a.spl[sb + 1];
+            if (stop || ts == T_BEFORE || te == T_AFTER) {   // empty part: so are both halves
+                pi.flags = 4;
+                pi.empty_type = ts == T_BEFORE ? T_BEFORE : T_AFTER;
+                pi.off = off;
+            } else {
+                len = a.spl[eb + 1] - off;
+                hoj_l = p * a.pw;
+                hoj_r = p * a.pw + a.half;
+                hw = min(a.half, a.m - hoj_r);
+                sfree = ts == T_AFTER;
+                efree = te == T_BEFORE;
+                pi.off = off;
+                pi.len = len;
+                pi.rhw = hw;
+                pi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : aff_free_bm(a.kind, hoj_l == 0);
+                pi.emode = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : aff_free_bm(a.kind, hoj_r + hw == a.m);
+                pi.flags = (sfree ? 1 : 0) | (efree ? 2 : 0);
+                gl = aff_half_geo(a, len, a.half);
+                gr = aff_half_geo(a, len, hw);
+            }
+            a.parts_out[p] = pi;
+            if (gl.ngroups > a.bound || gr.ngroups > a.bound) atomicOr(&bad, 1);
+        }
+        int64_t tot_rb, tot_rp;
+        const int64_t rb = rb_base + block_scan_excl(gl.rowbuf + gr.rowbuf, sh, &tot_rb);
+        const int64_t rp = rp_base + block_scan_excl(gl.rowpool + gr.rowpool, sh, &tot_rp);
+        rb_base += tot_rb;
+        rp_base += tot_rp;
+        if (p < a.parts) {
+            for (int side = 0; side < 2; ++side) {
+                const AffHalfGeo& g = side ? gr : gl;
+                const int idx = 2 * p + side;
+                DPProblem P{};
+                RowToCol J{};
+                if (g.h > 0) {
+                    // the half as add_half builds it (original orientation first)
+                    const int qoff = side ? off + len - 1 : off, qstep = side ? -1 : 1;
+                    const int soff = side ? hoj_r + hw - 1 : hoj_l, sstep = side ? -1 : 1;
+                    const int bm = side ? pi.emode : pi.smode;
+                    const bool fr = side ? sfree : efree;
+                    const int amode = (bm == BM_FREE_LOCAL ? AM_CLAMP : 0) | (fr ? a.best_bits : 0);
+                    int32_t* H = (side ? a.RH : a.LH) + off;
+                    int32_t* E = (side ? a.RE : a.LE) + off;
+                    P.best = fr ? a.pbest + 2 * p + side : nullptr;
+                    if (g.tr) {
+                        P.q = a.s;
+                        P.q_off = soff;
+                        P.q_step = sstep;
+                        P.s = a.q;
+                        P.s_off = qoff;
+                        P.s_step = qstep;
+                        P.bmode = aff_transposed_bm(bm);
+                        P.amode = (amode & AM_CLAMP) |
+                                  ((amode & AM_BEST_LASTCOL) == AM_BEST_LAST ? AM_BEST_LASTCOL : (amode & AM_BEST_LASTCOL));
+                        const int64_t ro = rp + (side ? gl.rowpool : 0);
+                        P.out_row = a.rowpool + ro;
+                        J.row = P.out_row;
+                        J.H = H;
+                        J.E = E;
+                        J.n = len;
+                        J.hlast = g.h - 1;
+                        J.xs = P.amode != 0 ? 1 : 0;
+                    } else {
+                        P.q = a.q;
+                        P.q_off = qoff;
+                        P.q_step = qstep;
+                        P.s = a.s;
+                        P.s_off = soff;
+                        P.s_step = sstep;
+                        P.bmode = bm;
+                        P.amode = amode;
+                        P.out_col = H;
+                        P.out_col_e = E;
+                    }
+                    P.h = g.h;
+                    P.w = g.w;
+                    P.nbands = (g.h + 63) / 64;
+                    P.ngroups = g.ngroups;
+                    P.wpad = g.wpad;
+                    P.nslots = g.nslots;
+                    P.rowbuf = a.rowbuf + rb + (side ? gl.rowbuf : 0);
+                    atomicAdd(&cells, (unsigned long long)((int64_t)g.h * g.w));
+                } else {
+                    P.nslots = 1;
+                }
+                P.flags = a.flags + (size_t)idx * a.bound;
+                P.magic = prob_magic(&P, idx, a.epoch);
+                P.pad_ = kPlannedDesc;
+                a.probs[idx] = P;
+                jobs[idx] = J;
+            }
+        }
+    }
+    // the group table, k-major over the half slots (a half's groups in increasing k)
+    const int nh = 2 * a.parts;
+    for (int i = (int)threadIdx.x; i < nh * a.bound; i += blockDim.x) {
+        const int k = i / nh, pr = i % nh;
+        a.groups[i] = GroupRef{pr, k, a.epoch, group_check(pr, k, a.epoch)};
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.hdr[0] = (uint32_t)(rb_base / 4);   // sentinel uint4s (every ring is a multiple of 128 ints)
+        a.hdr[1] = (uint32_t)bad;
+        reinterpret_cast<unsigned long long*>(a.hdr)[1] = cells;
     }
 }
 
@@ -2683,8 +2866,11 @@ hipError_t anyseq_launch_fill(int R, int CH, int NW, const anyseq::DPProblem* pr
 namespace anyseq {
 __global__ __launch_bounds__(256) void fill_prep_kernel(uint32_t* zero, int nzero, int32_t* init, int ninit,
                                                         int32_t init_value, uint4* sent, size_t nsent, uint32_t sv,
-                                                        const uint4* up_src, uint4* up_dst, int nup) {
+                                                        const uint4* up_src, uint4* up_dst, int nup,
+                                                        const uint32_t* nsent_dev) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    // a device-planned level: the plan kernel sized the hand-off rows (at most nsent)
+    if (nsent_dev) nsent = min(nsent, (size_t)*nsent_dev);
     // the launch's descriptors, read straight from the host's pinned staging area (no
     // separate copy operation in front of this kernel)
     for (size_t i = tid; i < (size_t)nup; i += nth) up_dst[i] = up_src[i];
@@ -2825,7 +3011,20 @@ hipError_t anyseq_launch_fill_prep(uint32_t* zero, int nzero, int32_t* init, int
     const size_t work = std::max<size_t>(std::max<size_t>((size_t)nzero, (size_t)ninit), std::max<size_t>(n16, nup));
     const int blocks = (int)std::max<size_t>(1, std::min<size_t>(2048, (work + 255) / 256));
     hipLaunchKernelGGL(anyseq::fill_prep_kernel, dim3(blocks), dim3(256), 0, st, zero, nzero, init, ninit, init_value,
-                       (uint4*)sent, n16, sent_value, (const uint4*)up_src, (uint4*)up_dst, nup);
+                       (uint4*)sent, n16, sent_value, (const uint4*)up_src, (uint4*)up_dst, nup, (const uint32_t*)nullptr);
+    return hipGetLastError();
+}
+
+// The prep of a device-planned level: the hand-off rows' size is read from the plan
+// header (*sent_n16 uint4s, at most sent_max_bytes).
+hipError_t anyseq_launch_fill_prep_planned(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
+                                           void* sent, size_t sent_max_bytes, uint32_t sent_value,
+                                           const uint32_t* sent_n16, hipStream_t st) {
+    const size_t n16 = sent_max_bytes / 16;
+    const size_t work = std::max<size_t>(std::max<size_t>((size_t)nzero, (size_t)ninit), n16);
+    const int blocks = (int)std::max<size_t>(1, std::min<size_t>(2048, (work + 255) / 256));
+    hipLaunchKernelGGL(anyseq::fill_prep_kernel, dim3(blocks), dim3(256), 0, st, zero, nzero, init, ninit, init_value,
+                       (uint4*)sent, n16, sent_value, (const uint4*)nullptr, (uint4*)nullptr, 0, sent_n16);
     return hipGetLastError();
 }
 
@@ -2891,6 +3090,11 @@ hipError_t anyseq_launch_aff_hb_join2(const void* parts, int nparts, int maxlen,
         hipLaunchKernelGGL(aff_hb_join_final_kernel, dim3((nparts + 63) / 64), dim3(64), 0, st,
                            (const PartInfo*)parts, nparts, nslices, (const int2*)partial, splits, types, score);
     }
+    return hipGetLastError();
+}
+
+hipError_t anyseq_launch_aff_level_plan(const anyseq::AffLevelPlan* plan, hipStream_t st) {
+    hipLaunchKernelGGL(anyseq::aff_level_plan_kernel, dim3(1), dim3(1024), 0, st, *plan);
     return hipGetLastError();
 }
 
