@@ -66,6 +66,7 @@ hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* 
                                       int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows,
                                       hipStream_t st);
 hipError_t anyseq_launch_aff_level_plan(const AffLevelPlan* plan, hipStream_t st);
+hipError_t anyseq_launch_aff_level_tail(const void* tail, int fill_groups, hipStream_t st);
 hipError_t anyseq_launch_fill_prep_planned(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
                                            void* sent, size_t sent_max_bytes, uint32_t sent_value,
                                            const uint32_t* sent_n16, hipStream_t st);
@@ -1150,7 +1151,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         }
         return mx;
     };
-    if (!sharded && g_tuning.devplan && plan_rowbuf_bytes() <= ((size_t)8 << 30)) {
+    if (!sharded && g_tuning.devplan && plan_rowbuf_bytes() <= ((size_t)8 << 30) && n < 8192 * 4096 - 1) {
         // Device-planned levels: every level is enqueued up front -- plan
         // (aff_level_plan_kernel builds the level from the splits on the device), prep,
         // fill, row-to-column, join -- and the splits come back in ONE download after the
@@ -1197,16 +1198,26 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         const int nlev = (int)lv.size();
         // every allocation before the first enqueue (growth may synchronise the device)
         char* meta = (char*)E.pl_meta.get(std::max<size_t>(max_meta, 256));
+        // hand-off rows: every planned fill puts the sentinel back after each read, so the
+        // buffer stays all sentinel between launches; it is filled once per allocation
+        // (and again after a failed call)
+        void* const rb_prev = E.pl_rowbuf.p;
         int32_t* rowbuf = (int32_t*)E.pl_rowbuf.get(std::max<size_t>(max_rowbuf, 16));
+        if (rowbuf != rb_prev || E.pl_dirty)
+            HIPCHECK(hipMemsetD32Async(rowbuf, 0x80808080, E.pl_rowbuf.cap / 4, st));
+        E.pl_dirty = true;   // until this call has checked its error words
         int32_t* rowpool = (int32_t*)E.outrow.get(std::max<size_t>(max_rowpool, 16));
         PartInfo* d_parts = (PartInfo*)E.pl_parts.get((size_t)max_parts * sizeof(PartInfo));
         RowToCol* d_jobs = (RowToCol*)E.pl_jobs.get((size_t)2 * max_parts * sizeof(RowToCol));
         int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * max_parts * 4);
         void* partial = E.joinbuf.get(std::max<size_t>(max_joinbuf, 16));
-        uint32_t* d_tail = (uint32_t*)E.pl_hdr.get((size_t)(std::max(nlev, 1) * 5) * 4 + 16);   // hdr (4) | err
-        uint32_t* d_hdr = d_tail;                       // 4 words per level
-        uint32_t* d_err = d_tail + 4 * nlev;            // 1 word per level
-        uint32_t* h_tail = (uint32_t*)E.pl_pin.get((size_t)(std::max(nlev, 1) * 5) * 4 + 16);
+        // per level: header (8 words: sentinel uint4s, bound check, cells (u64), tail counter)
+        // then one error word per level
+        const size_t tail_words = (size_t)std::max(nlev, 1) * 9;
+        uint32_t* d_tail = (uint32_t*)E.pl_hdr.get(tail_words * 4 + 16);
+        uint32_t* d_hdr = d_tail;
+        uint32_t* d_err = d_tail + 8 * nlev;
+        uint32_t* h_tail = (uint32_t*)E.pl_pin.get(tail_words * 4 + 16);
         while ((int)E.pl_ev.size() < 2 * nlev) {
             hipEvent_t ev;
             HIPCHECK(hipEventCreate(&ev));
@@ -1217,17 +1228,20 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             register_static_range(rowbuf, max_rowbuf);
             register_static_range(rowpool, max_rowpool);
         }
-        HIPCHECK(hipMemsetAsync(d_err, 0, (size_t)nlev * 4, st));
+        HIPCHECK(hipMemsetAsync(d_tail, 0, tail_words * 4, st));
         static std::atomic<int32_t> g_plan_epoch{0x40000};
         uint32_t* ctr = (uint32_t*)meta;
+        std::vector<AffLevelPlan> plans((size_t)nlev);
+        std::vector<int32_t> epochs((size_t)nlev);
         for (int li = 0; li < nlev; ++li) {
             const Lev& L = lv[li];
-            g_stage_level = li + 1;
             const size_t zb = ((32 + (size_t)L.slots) * 4 + 255) & ~(size_t)255;
             DPProblem* d_probs = (DPProblem*)(meta + zb);
             GroupRef* d_groups = (GroupRef*)(meta + zb + (size_t)L.nh * sizeof(DPProblem));
             const int32_t epoch = (g_plan_epoch.fetch_add(1) + 1) & 0x7ffff;
-            AffLevelPlan A{};
+            epochs[li] = epoch;
+            AffLevelPlan& A = plans[li];
+            A = AffLevelPlan{};
             A.parts = L.parts;
             A.bpp = L.bpp;
             A.nb = sp.nb;
@@ -1259,12 +1273,23 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             A.probs = d_probs;
             A.groups = d_groups;
             A.jobs = d_jobs;
-            A.hdr = d_hdr + 4 * li;
-            HIPCHECK(anyseq_launch_aff_level_plan(&A, st));
-            HIPCHECK(anyseq_launch_fill_prep_planned(ctr, 32 + L.slots, pbest, 2 * L.parts, kAffNegH, rowbuf,
-                                                     L.rowbuf_bytes, 0x80808080u, d_hdr + 4 * li, st));
+            A.hdr = d_hdr + 8 * li;
+        }
+        // level 1: plan + prep; every level: fill, then one tail launch (join, next level's
+        // sentinel rows, counters, best cells and plan)
+        if (nlev > 0) {
+            HIPCHECK(anyseq_launch_aff_level_plan(&plans[0], st));
+            HIPCHECK(anyseq_launch_fill_prep_planned(ctr, 32 + lv[0].slots, pbest, 2 * lv[0].parts, kAffNegH, rowbuf,
+                                                     0, 0x80808080u, d_hdr, st));
+        }
+        for (int li = 0; li < nlev; ++li) {
+            const Lev& L = lv[li];
+            const AffLevelPlan& A = plans[li];
+            g_stage_level = li + 1;
+            DPProblem* d_probs = A.probs;
+            GroupRef* d_groups = A.groups;
             FillParams fpl = fp;
-            fpl.epoch = epoch;
+            fpl.epoch = epochs[li];
             fpl.prio = g_tuning.prio;
             fpl.throttle = g_tuning.thr;
             fpl.slack = g_tuning.slack;
@@ -1272,29 +1297,61 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li], st));
             HIPCHECK(anyseq_launch_fill_affine(NWa, d_probs, d_groups, L.slots, ctr, d_err + li, &fpl, L.grid, st));
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li + 1], st));
-            HIPCHECK(anyseq_launch_aff_row_to_col(d_jobs, L.nh, n, -sc.gap_extend, st));
-            HIPCHECK(anyseq_launch_aff_hb_join2(d_parts, L.parts, n, L.half, LH0, LE0, RH0, RE0, pbest, sc.gap_open,
-                                                sc.gap_extend, partial, d_spl, d_typ, li == 0 ? d_score : nullptr, st));
+            AffLevelTail T{};
+            T.parts = d_parts;
+            T.jobs = d_jobs;
+            T.LH = LH0;
+            T.LE = LE0;
+            T.RH = RH0;
+            T.RE = RE0;
+            T.pbest = pbest;
+            T.nparts = L.parts;
+            T.half = L.half;
+            // ~256 join workgroups: few long parts split into slices, many short ones whole
+            T.nslices = std::max(1, std::min(nsl, (256 + L.parts - 1) / L.parts));
+            T.slice_len = (n + 1 + T.nslices - 1) / T.nslices;
+            T.go = sc.gap_open;
+            T.ge = sc.gap_extend;
+            T.partial = partial;
+            T.splits = d_spl;
+            T.types = d_typ;
+            T.score = li == 0 ? d_score : nullptr;
+            T.done = d_hdr + 8 * li + 4;
+            T.has_next = li + 1 < nlev;
+            if (T.has_next) {
+                const Lev& N = lv[li + 1];
+                T.sent = rowbuf;
+                T.nsent16 = 0;   // (the rows are sentinel already)
+                T.zero = ctr;
+                T.nzero = 32 + N.slots;
+                T.init = pbest;
+                T.ninit = 2 * N.parts;
+                T.next = plans[li + 1];
+            }
+            HIPCHECK(anyseq_launch_aff_level_tail(&T, T.has_next && T.nsent16 ? 1024 : 1, st));
             stage_check(st, "affine level (device plan)");
         }
         HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + 1) * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(h_tail, d_tail, (size_t)nlev * 5 * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(h_tail, d_tail, (size_t)nlev * 9 * 4, hipMemcpyDeviceToHost, st));
         {
             const hipError_t e = stream_wait_spin(st);
             if (e != hipSuccess) fail("affine construct levels failed: %s", hipGetErrorString(e));
         }
+        bool any_err = false;
+        for (int li = 0; li < nlev; ++li) any_err |= h_tail[8 * nlev + li] != 0;
+        E.pl_dirty = any_err;
         for (int li = 0; li < nlev; ++li) {
-            const uint32_t err = h_tail[4 * nlev + li];
+            const uint32_t err = h_tail[8 * nlev + li];
             g_stage_level = li + 1;
             if (err & ERR_BAD_DESC) fail("fill kernel read a corrupt problem descriptor (error %u; planned level %d)", err, li + 1);
             if (err) fail("fill kernel reported error %u (spin timeout; planned level %d)", err, li + 1);
-            if (h_tail[4 * li + 1]) fail("internal: planned level %d: a half exceeds its group slots", li + 1);
+            if (h_tail[8 * li + 1]) fail("internal: planned level %d: a half exceeds its group slots", li + 1);
             float ms = 0.f;
             HIPCHECK(hipEventElapsedTime(&ms, E.pl_ev[2 * li], E.pl_ev[2 * li + 1]));
             g_fill_ms += ms;
             g_fill_launches += 1;
             uint64_t cells;
-            memcpy(&cells, h_tail + 4 * li + 2, 8);
+            memcpy(&cells, h_tail + 8 * li + 2, 8);
             g_fill_cells += (int64_t)cells;
         }
         memcpy(sp.v.data(), h_status, nsv * 4);

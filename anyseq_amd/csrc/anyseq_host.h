@@ -147,6 +147,7 @@ struct Engine {
     DevBuf pl_meta, pl_rowbuf, pl_parts, pl_jobs, pl_hdr;
     PinBuf pl_pin;
     std::vector<hipEvent_t> pl_ev;
+    bool pl_dirty = true;      // pl_rowbuf may hold non-sentinel words (fresh, or a failed call)
     explicit Engine(int dev);
 };
 

@@ -211,6 +211,35 @@ struct AffLevelPlan {
     uint32_t* hdr;                // [0] sentinel uint4s of rowbuf, [2..3] cells (u64)
 };
 
+// The tail of a device-planned level, one launch: the join of level L
+// (one workgroup per slice of kJoinSlice candidates per part; a transposed half's
+// last column is read straight from its bottom row, which replaces the
+// row-to-column pass), the sentinel fill of level L+1's hand-off rows (every
+// workgroup, grid-stride over the host's bound), and -- in the last workgroup to
+// finish -- the join's final pass (splits, types), then level L+1's counters, best
+// cells and plan.
+struct AffLevelTail {
+    const PartInfo* parts;
+    const RowToCol* jobs;
+    const int32_t *LH, *LE, *RH, *RE;
+    const int32_t* pbest;
+    int32_t nparts, half, nslices, go, ge;
+    int32_t slice_len;    // candidates per slice (nslices * slice_len > the longest possible part)
+    void* partial;        // int2 per (part, slice)
+    int32_t* splits;
+    int32_t* types;
+    int32_t* score;        // level 1: the join value
+    uint32_t* done;        // zeroed before the launch
+    void* sent;            // next level's hand-off rows (uint4 units)
+    size_t nsent16;
+    int32_t has_next;
+    uint32_t* zero;        // next level's counters + group flags
+    int32_t nzero;
+    int32_t* init;         // next level's best cells
+    int32_t ninit;
+    AffLevelPlan next;
+};
+
 // Affine final level (aff_predwalk_kernel): blocks of at most `lds_rows` rows (the
 // launch's tallest block, at most kPredLdsMaxRows) keep their predecessor bytes and
 // query rows and subject columns in LDS ((rows + 127) x 128 + rows + 128 bytes,

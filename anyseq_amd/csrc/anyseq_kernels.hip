@@ -956,6 +956,13 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             }
         }
     }
+    // the producer's last chunk may extend past w (whole-chunk stores of the asm
+    // epilogue): those columns get the sentinel back too, so a ring that is reset
+    // after every read is all sentinel again once the launch is over
+    if (need_in && reset_in) {
+        T* gw = const_cast<T*>(g_in);
+        for (int c = ngran * GR + lane; c < nchunks * CH; c += 64) HandOff<T>::store(gw + c, HandOff<T>::sentinel());
+    }
 }
 
 template <int KIND, int R, int X, int NW, int CH>
@@ -1694,7 +1701,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
             const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
             io_wave<32, true, int2>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0], &sh.s_filled,
                                     &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
-                                    P.nslots < P.ngroups - 1, 2, 2, fp.prio == 3,
+                                    P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc, 2, 2, fp.prio == 3,
                                     fp.dbg && first < 2048 ? fp.dbg + 16 + 4 * 4096 + 16 * (first + (P.q_step < 0 ? 2048 : 0))
                                                            : nullptr);
         } else {
@@ -2422,7 +2429,7 @@ __device__ int64_t block_scan_excl(int64_t v, int64_t* sh, int64_t* total) {
     return r;
 }
 
-__global__ __launch_bounds__(1024) void aff_level_plan_kernel(const AffLevelPlan a) {
+__device__ void aff_level_plan_body(const AffLevelPlan& a) {
     __shared__ int64_t sh[17];
     __shared__ unsigned long long cells;
     __shared__ int32_t bad;
@@ -2551,6 +2558,158 @@ __global__ __launch_bounds__(1024) void aff_level_plan_kernel(const AffLevelPlan
         a.hdr[1] = (uint32_t)bad;
         reinterpret_cast<unsigned long long*>(a.hdr)[1] = cells;
     }
+}
+
+__global__ __launch_bounds__(1024) void aff_level_plan_kernel(const AffLevelPlan a) { aff_level_plan_body(a); }
+
+constexpr int kTailStage = 8192;   // partials staged in LDS per chunk of parts (64 KiB)
+__global__ __launch_bounds__(1024) void aff_level_tail_kernel(const AffLevelTail t) {
+    __shared__ int sv[1024], sk[1024];
+    __shared__ int last;
+    const int nj = t.nslices * t.nparts;
+    const int b = blockIdx.x;
+    if (t.has_next) {
+        const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+        for (size_t i = (size_t)b * blockDim.x + threadIdx.x; i < t.nsent16; i += (size_t)gridDim.x * blockDim.x)
+            reinterpret_cast<uint4*>(t.sent)[i] = v;
+    }
+    const int part = b / max(t.nslices, 1), slice = b % max(t.nslices, 1);
+    const PartInfo pi = b < nj ? t.parts[part] : PartInfo{};
+    // slices past the part's candidates (the slice count covers the longest possible part)
+    const bool idle = b < nj && (pi.flags & 4 || (slice > 0 && slice * t.slice_len - 1 >= pi.len));
+    // partials: write-through (sc1) stores, drained before the counter, read back with sc1
+    // loads -- no L2 write-back fence, which would also flush the sentinel rows
+    int2* partial = reinterpret_cast<int2*>(t.partial);
+    if (idle && threadIdx.x == 0)
+        HandOff<int2>::store(partial + (size_t)part * t.nslices + slice, make_int2(-2147483647, 0x7fffffff));
+    if (b < nj && !idle) {
+        const int off = pi.off, len = pi.len, nge = -t.ge;
+        int best = -2147483647, key = 0x7fffffff;
+        if (!(pi.flags & 4)) {
+            const bool sfree = pi.flags & 1, efree = pi.flags & 2;
+            const int bLH = aff_top_h(pi.smode, t.half - 1, t.go, t.ge), bLE = sfree ? kAffNeg : bLH;
+            const int bRH = aff_top_h(pi.emode, pi.rhw - 1, t.go, t.ge), bRE = efree ? kAffNeg : bRH;
+            const RowToCol JL = t.jobs[2 * part], JR = t.jobs[2 * part + 1];
+            if (slice == 0 && threadIdx.x == 0) {
+                if (efree && t.pbest[2 * part] > best) {
+                    best = t.pbest[2 * part];
+                    key = 0;
+                }
+                if (sfree && t.pbest[2 * part + 1] > best) {
+                    best = t.pbest[2 * part + 1];
+                    key = 1;
+                }
+            }
+            const int i0 = slice * t.slice_len - 1, i1 = min(len, i0 + t.slice_len);
+            for (int i = i0 + (int)threadIdx.x; i < i1; i += blockDim.x) {
+                const int k = len - i - 2;
+                int hl, el, hr, er;
+                if (i < 0) {
+                    hl = bLH;
+                    el = bLE;
+                } else if (JL.n > 0) {   // transposed left half: its bottom row, H space
+                    const int2 v = reinterpret_cast<const int2*>(JL.row)[i];
+                    const int z = (JL.hlast + (JL.xs ? 0 : i) + 2) * nge;
+                    hl = v.x - z;
+                    el = v.y - z;
+                } else {
+                    hl = t.LH[off + i];
+                    el = t.LE[off + i];
+                }
+                if (k < 0) {
+                    hr = bRH;
+                    er = bRE;
+                } else if (JR.n > 0) {
+                    const int2 v = reinterpret_cast<const int2*>(JR.row)[k];
+                    const int z = (JR.hlast + (JR.xs ? 0 : k) + 2) * nge;
+                    hr = v.x - z;
+                    er = v.y - z;
+                } else {
+                    hr = t.RH[off + k];
+                    er = t.RE[off + k];
+                }
+                const int vh = hl + hr, ve = el + er - t.go;
+                if (vh > best) {
+                    best = vh;
+                    key = 2 + 2 * (i + 1);
+                }
+                if (ve > best) {
+                    best = ve;
+                    key = 3 + 2 * (i + 1);
+                }
+            }
+        }
+        sv[threadIdx.x] = best;
+        sk[threadIdx.x] = key;
+        __syncthreads();
+        for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) {
+                const int v2 = sv[threadIdx.x + o], k2 = sk[threadIdx.x + o];
+                if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && k2 < sk[threadIdx.x])) {
+                    sv[threadIdx.x] = v2;
+                    sk[threadIdx.x] = k2;
+                }
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) HandOff<int2>::store(partial + (size_t)part * t.nslices + slice, make_int2(sv[0], sk[0]));
+    }
+    // the last workgroup to finish
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicAdd(t.done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    // the final pass over chunks of parts: every partial of the chunk is loaded at once
+    // (independent write-through loads, one round trip) into LDS, then reduced per part
+    __shared__ int2 stage[kTailStage];
+    const int pc = min((int)blockDim.x, max(1, kTailStage / max(t.nslices, 1)));   // (host: nslices <= kTailStage)
+    for (int p0 = 0; p0 < t.nparts; p0 += pc) {
+        const int np = min(pc, t.nparts - p0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < np * t.nslices; i += blockDim.x)
+            stage[i] = HandOff<int2>::load(partial + (size_t)p0 * t.nslices + i);
+        __syncthreads();
+        const int part = p0 + (int)threadIdx.x;
+        if ((int)threadIdx.x >= np) continue;
+        const PartInfo pi = t.parts[part];
+        if (pi.flags & 4) {
+            t.splits[pi.split_index + 1] = pi.off;
+            t.types[pi.split_index + 1] = pi.empty_type;
+            continue;
+        }
+        int best = -2147483647, kk = 0x7fffffff;
+        for (int sl = 0; sl < t.nslices; ++sl) {
+            const int2 v = stage[threadIdx.x * t.nslices + sl];
+            if (v.x > best || (v.x == best && v.y < kk)) {
+                best = v.x;
+                kk = v.y;
+            }
+        }
+        int type, spl;
+        if (kk == 0) {
+            type = T_BEFORE;
+            spl = pi.off + pi.len;
+        } else if (kk == 1) {
+            type = T_AFTER;
+            spl = pi.off;
+        } else {
+            type = (kk & 1) ? T_E : T_H;
+            spl = pi.off + (kk - 2) / 2;
+        }
+        t.splits[pi.split_index + 1] = spl;
+        t.types[pi.split_index + 1] = type;
+        if (t.score && part == 0) *t.score = best;
+    }
+    if (!t.has_next) return;
+    __syncthreads();
+    __threadfence_block();
+    for (int i = threadIdx.x; i < t.nzero; i += blockDim.x) t.zero[i] = 0u;
+    for (int i = threadIdx.x; i < t.ninit; i += blockDim.x) t.init[i] = kAffNeg;
+    __syncthreads();
+    aff_level_plan_body(t.next);
 }
 
 // Final level: Gotoh with predecessor bytes for one 128-column block per wave,
@@ -3095,6 +3254,15 @@ hipError_t anyseq_launch_aff_hb_join2(const void* parts, int nparts, int maxlen,
 
 hipError_t anyseq_launch_aff_level_plan(const anyseq::AffLevelPlan* plan, hipStream_t st) {
     hipLaunchKernelGGL(anyseq::aff_level_plan_kernel, dim3(1), dim3(1024), 0, st, *plan);
+    return hipGetLastError();
+}
+
+// One launch per level boundary of the device-planned construct (aff_level_tail_kernel):
+// `fill_groups` workgroups at least, so the next level's sentinel fill spreads over the chip.
+hipError_t anyseq_launch_aff_level_tail(const void* tail, int fill_groups, hipStream_t st) {
+    const anyseq::AffLevelTail& t = *(const anyseq::AffLevelTail*)tail;
+    const int grid = std::max(std::max(1, t.nslices * t.nparts), t.has_next ? fill_groups : 1);
+    hipLaunchKernelGGL(anyseq::aff_level_tail_kernel, dim3(grid), dim3(1024), 0, st, t);
     return hipGetLastError();
 }
 
