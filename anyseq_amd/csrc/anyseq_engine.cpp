@@ -1152,7 +1152,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         return mx;
     };
     if (!sharded && g_tuning.devplan && plan_rowbuf_bytes() <= ((size_t)8 << 30) && n < 8192 * 4096 - 1) {
-        // Device-planned levels (DESIGN.md §3.6): every level is enqueued up front -- plan
+        // Device-planned levels (DESIGN.md §3.7): every level is enqueued up front -- plan
         // (aff_level_plan_kernel builds the level from the splits on the device), prep,
         // fill, row-to-column, join -- and the splits come back in ONE download after the
         // last level, instead of a download and a host rebuild per level.

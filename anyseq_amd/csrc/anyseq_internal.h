@@ -180,7 +180,7 @@ struct RowToCol {
     int32_t pad_;
 };
 
-// Device-planned Hirschberg level of the affine construct (DESIGN.md §3.6,
+// Device-planned Hirschberg level of the affine construct (DESIGN.md §3.7,
 // aff_level_plan_kernel): the level's part table, half descriptors, group table and
 // row-to-column jobs are built on the device from the previous level's splits, so the
 // host enqueues every level without reading anything back.  Slots are fixed by the
@@ -211,7 +211,7 @@ struct AffLevelPlan {
     uint32_t* hdr;                // [0] sentinel uint4s of rowbuf, [2..3] cells (u64)
 };
 
-// The tail of a device-planned level, one launch (DESIGN.md §3.6): the join of level L
+// The tail of a device-planned level, one launch (DESIGN.md §3.7): the join of level L
 // (one workgroup per slice of kJoinSlice candidates per part; a transposed half's
 // last column is read straight from its bottom row, which replaces the
 // row-to-column pass), the sentinel fill of level L+1's hand-off rows (every

@@ -2374,7 +2374,7 @@ __global__ void aff_row_to_col_kernel(const RowToCol* __restrict__ jobs, int nge
 }
 
 // ---------------------------------------------------------------------------
-// Device-planned Hirschberg level (AffLevelPlan, DESIGN.md §3.6): the host-side
+// Device-planned Hirschberg level (AffLevelPlan, DESIGN.md §3.7): the host-side
 // level builder of the affine construct (anyseq_engine.cpp add_half / fill_prepare)
 // restated on the device, one workgroup: part table, the two half descriptors of
 // every part (transposed when taller than wide), their hand-off ring and flag slots,

@@ -54,9 +54,12 @@ BYTES_PER_CELL = 4           # one int32 H store per cell
 VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2
 VALU_DESIGN_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
 # VALU instructions per wave step (64 cells) of the steady-state asm loops
-# (tools/gen_block_asm.py): linear 5 (+1 publishing shift), affine 9
-# (+2 publishing shifts) plain, +2.5 with the local clamp and best tracking.
-VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.0, "affine_local": 13.5}
+# (tools/gen_block_asm.py): linear 5 (+1 publishing shift); affine
+# round 3: 9.25 counted in G space, 10.75 in X space (clamp + best), and the PMC
+# measurement of the X-space fill with its block overheads, 12.9 per wave step
+# (profiles/r03a_pmc.json: SQ_INSTS_VALU / (cells / 64)); G space = 9.25 + the same
+# 2.15 of block overhead.
+VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.4, "affine_local": 12.9}
 
 AFFINE = dict(match=2, mismatch=-1, gap_open=-2, gap_extend=-1)
 METRIC = "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; % of HBM roofline"
@@ -350,8 +353,8 @@ def construct_bench_sharded(args, world, rank, local_rank):
                                    f"dealt round-robin over {world} GPUs", "baseline_config": args.config,
                        "query_len": n, "subject_len": m, "parallelism": f"Hirschberg halves x{world} (RCCL "
                                                                          "all-reduce of level columns)",
-                       "score": int(score), "transport": "RCCL all-reduce, unverified on >1 GPU until a SCALE "
-                                                         "run exists"},
+                       "score": int(score), "transport": "RCCL all-reduce, unmeasured on hardware (no "
+                                                         "multi-GPU run before this one)"},
         }
         print(json.dumps(out), flush=True)
     dist.barrier()
@@ -466,8 +469,8 @@ def score_bench(args, world, rank, local_rank):
                                       else f", {n}x{m} cells per GPU"),
                        "baseline_config": args.config, "query_len": n, "subject_len": m,
                        "parallelism": parallelism, "score": int(score),
-                       "transport": ("RCCL send/recv, unverified on >1 GPU until a SCALE run exists"
-                                     if world > 1 else None)},
+                       "transport": ("RCCL send/recv (host-polled chunk trigger), unmeasured on hardware "
+                                     "(no multi-GPU run before this one)" if world > 1 else None)},
             "roofline": roofline("fill_affine_kernel" if aff else "fill_kernel", cells_per_launch, kernel_ms,
                                  valu_key, tag),
         }

@@ -11,7 +11,7 @@ out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/aff_timeline"
 kind = sys.argv[2] if len(sys.argv) > 2 else "local"
 rows = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
 os.environ["ANYSEQ_STAMPS"] = "1"
-os.environ["ANYSEQ_LIB"] = os.path.abspath("anyseq_amd/libanyseq_stamps.so")
+os.environ["ANYSEQ_LIB"] = os.path.abspath(os.environ.get("ANYSEQ_TL_LIB", "anyseq_amd/libanyseq_stamps.so"))
 sys.path.insert(0, ".")
 import anyseq_amd as A  # noqa: E402
 
