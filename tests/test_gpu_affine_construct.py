@@ -84,3 +84,17 @@ def test_affine_construct_transposed_halves(anyseq, oracle, kind, transpose):
             same(anyseq, oracle, kind, q, s, SCHEMES[i % len(SCHEMES)])
     finally:
         anyseq.set_option("affine_transpose", 1)
+
+
+def test_affine_construct_planned_rows_stay_clean(anyseq, oracle):
+    """Device-planned levels reuse one hand-off row buffer without a
+    sentinel fill: every column a producer stores must get the sentinel back from its
+    reader, including the band epilogue's columns past w.  Alternating shapes (odd and
+    even widths, partial last chunks, several groups per half) move the per-launch row
+    layout around, so a stale word left by one launch lands inside another's row."""
+    rng = random.Random(58)
+    for it in range(16):
+        n = rng.randint(900, 2600) | (it & 1)
+        m = rng.randint(900, 2600) | ((it >> 1) & 1)
+        kind = KINDS[it % 3]
+        same(anyseq, oracle, kind, rnd(rng, n), rnd(rng, m), SCHEMES[it % len(SCHEMES)])
