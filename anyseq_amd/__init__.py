@@ -242,7 +242,8 @@ def shard_score_local(kind, query, subject, nshards: int, match=2, mismatch=-1, 
 
 def construct_local_sharded(kind, query, subject, nshards: int, match=2, mismatch=-1, gap_open=-2, gap_extend=-1):
     """Sharded affine construct with `nshards` virtual ranks in this process on one GPU:
-    the level-by-level round-robin plan of the RCCL path, one fill
+    the plan of the RCCL path: level 1 column-blocked over the ranks
+    when its halves run transposed, later levels' halves dealt round-robin, one fill
     launch per rank per level.  Returns (optimal_score, alQuery, alSubject)."""
     q, s = _b(query), _b(subject)
     L = len(q) + len(s)

@@ -1378,6 +1378,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         pinfo.assign((size_t)parts, PartInfo{});
         std::vector<RowToColJob> jobs;
         int half_index = 0;   // the level's half fills in part order: left 2k, right 2k+1
+        ShardLevel1 l1;
+        bool l1_blocked = false;
         if (sharded) {   // rows a rank does not fill are zero in the SUM reduction
             for (int32_t* b : {LH0, LE0, RH0, RE0}) HIPCHECK(hipMemsetAsync(b, 0, nviews * nn * 4, st));
         }
@@ -1409,6 +1411,37 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             const int best_bits = local ? AM_BEST_ALL : AM_BEST_LAST;
             // (half_index advances on every rank, so all ranks agree on the owners)
             const int ol = owner(half_index++), orr = owner(half_index++);
+            if (level1 && sharded && shards->level1 && parts == 1 && g_tuning.afft && len > half && len >= world &&
+                env_int("ANYSEQ_SHARD_L1", 1) != 0) {
+                // column-blocked level 1: both halves transposed, every
+                // rank fills a block of query columns of both
+                auto tam = [](int am) {
+                    return (am & AM_CLAMP) |
+                           ((am & AM_BEST_LASTCOL) == AM_BEST_LAST ? AM_BEST_LASTCOL : (am & AM_BEST_LASTCOL));
+                };
+                l1.kind = kind;
+                l1.sc = sc;
+                l1.fp = fp;
+                l1.cq = cq;
+                l1.cs = cs;
+                l1.n = n;
+                l1.m = m;
+                l1.half = half;
+                l1.bm_l = transposed_bm(pi.smode);
+                l1.am_l = tam((pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0));
+                l1.bm_r = transposed_bm(pi.emode);
+                l1.am_r = tam((pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0));
+                l1.LH = LH0;
+                l1.LE = LE0;
+                l1.RH = RH0;
+                l1.RE = RE0;
+                l1.nn = nn;
+                l1.pbest = pbest0;
+                l1.pstride = (size_t)2 * parts;
+                l1.st = st;
+                l1_blocked = true;
+                continue;
+            }
             for (int v = 0; v < nviews; ++v) {
                 const size_t vo = (size_t)v * nn;
                 int32_t* pb = pbest0 + (size_t)v * 2 * parts;
@@ -1451,6 +1484,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                 fill_async(E, E.fc, probs, fp, st, 0, nullptr, 0, pbv, 2 * parts, kAffNegH);
             }
             pending_fill = true;
+        }
+        if (l1_blocked) {   // (every view's best cells were reset above: no view has probs)
+            shards->level1(l1);
+            stage_check(st, "sharded level 1");
         }
         if (!d_up) {
             char* d = (char*)E.parts.get(pb + jb + 16);

@@ -177,7 +177,7 @@ struct RowToCol {
     int32_t n;      // columns of the transposed problem (rows of the original)
     int32_t hlast;  // last row of the transposed problem
     int32_t xs;     // the row holds X-space values (DPProblem::amode != 0)
-    int32_t pad_;
+    int32_t c0;     // G space: the row's first column in the half (a column block of a sharded level, §6.2)
 };
 
 // Device-planned Hirschberg level of the affine construct (DESIGN.md §3.7,

@@ -2385,7 +2385,7 @@ __global__ void aff_row_to_col_kernel(const RowToCol* __restrict__ jobs, int nge
     const RowToCol J = jobs[blockIdx.y];
     for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < J.n; c += blockDim.x * gridDim.x) {
         const int2 v = reinterpret_cast<const int2*>(J.row)[c];
-        const int z = (J.hlast + (J.xs ? 0 : c) + 2) * nge;
+        const int z = (J.hlast + (J.xs ? 0 : c + J.c0) + 2) * nge;
         J.H[c] = v.x - z;
         J.E[c] = v.y - z;
     }
@@ -2627,7 +2627,7 @@ __global__ __launch_bounds__(1024) void aff_level_tail_kernel(const AffLevelTail
                     el = bLE;
                 } else if (JL.n > 0) {   // transposed left half: its bottom row, H space
                     const int2 v = reinterpret_cast<const int2*>(JL.row)[i];
-                    const int z = (JL.hlast + (JL.xs ? 0 : i) + 2) * nge;
+                    const int z = (JL.hlast + (JL.xs ? 0 : i + JL.c0) + 2) * nge;
                     hl = v.x - z;
                     el = v.y - z;
                 } else {
@@ -2639,7 +2639,7 @@ __global__ __launch_bounds__(1024) void aff_level_tail_kernel(const AffLevelTail
                     er = bRE;
                 } else if (JR.n > 0) {
                     const int2 v = reinterpret_cast<const int2*>(JR.row)[k];
-                    const int z = (JR.hlast + (JR.xs ? 0 : k) + 2) * nge;
+                    const int z = (JR.hlast + (JR.xs ? 0 : k + JR.c0) + 2) * nge;
                     hr = v.x - z;
                     er = v.y - z;
                 } else {

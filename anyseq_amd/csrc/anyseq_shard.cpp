@@ -44,6 +44,7 @@ extern "C" hipError_t anyseq_launch_shard_aff_combine(int kind, const void* rowT
                                                       int sT, const int32_t* lB, const int32_t* lBf, int sB, int last,
                                                       const int32_t* colT, const int32_t* colB, int adj, int32_t* out,
                                                       hipStream_t st);
+extern "C" hipError_t anyseq_launch_aff_row_to_col(const void* jobs, int njobs, int maxn, int nge, hipStream_t st);
 extern "C" hipError_t anyseq_launch_shard_combine(int kind, const int32_t* rowT, int h1, const int32_t* rowB, int h2,
                                                   int w, int gap, const int32_t* lT, int sT, const int32_t* lB,
                                                   int sB, int last, const int32_t* colT, const int32_t* colB, int adj,
@@ -98,6 +99,9 @@ struct Shard {
     const int32_t* lB = nullptr;
     const int32_t* lTe = nullptr;  // affine: received E columns (+ [h] = F of the last row)
     const int32_t* lBe = nullptr;
+    // column-blocked construct level: the two bottom rows -> the level's column segments
+    DevBuf jobs;
+    RowToCol h_jobs[2] = {};
     void init() {
         if (st) return;
         for (Front* f : {&top, &bot})
@@ -178,9 +182,10 @@ void wait_stream(hipStream_t s, double seconds, const char* what) {
 }
 
 // Per-step setup of one shard: problems, sentinel buffers, counters.
+// h1_req >= 0: the top front's rows (a construct level splits at `half`, not n/2).
 void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds_block,
-                 int m, std::vector<DPProblem>& probs, int& h1, int& h2, bool direct = false) {
-    h1 = n / 2;
+                 int m, std::vector<DPProblem>& probs, int& h1, int& h2, bool direct = false, int h1_req = -1) {
+    h1 = h1_req >= 0 ? h1_req : n / 2;
     h2 = n - h1;
     const int g = S.g, w = S.w;
     const int wpad = (w + 63) & ~63;
@@ -514,18 +519,25 @@ int grid_per_shard(const Engine& E, int nshards) {
     return std::max(8, xcds * std::max(1, (per_xcd - 8) / nshards));
 }
 
+// The in-process shards (kept: streams, counters, buffers are reused; they never move,
+// their buffers are registered by address).
+std::vector<Shard>& local_shards() {
+    static std::vector<Shard> shards;
+    if (shards.capacity() < 64) shards.reserve(64);
+    return shards;
+}
+
 int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int n, const char* s, int m, int N) {
     check_shard_shape(kind, sc, n, m, N);
     Engine& E = engine();
     std::lock_guard<std::mutex> lk(E.mu);
-    static std::vector<Shard> shards;   // kept: streams, counters, buffers are reused
+    std::vector<Shard>& shards = local_shards();
     // every local shard's persistent fill must be co-resident with the others (they
     // wait for each other): grid_per_shard gives each at least one workgroup per XCD
     // and keeps 8 CUs per XCD free, so at most CUs/8 - 8 shards fit (24 on MI355X)
     const int max_local = std::max(1, E.num_cus / 8 - 8);
     if (N > max_local) fail("sharded fill: at most %d local shards on this device (got %d)", max_local, N);
     if (N > 64) fail("sharded fill: at most 64 local shards");
-    if (shards.capacity() < 64) shards.reserve(64);   // shards never move (buffers are registered by address)
     if ((int)shards.size() < N) shards.resize(N);
     uint8_t* dq = (uint8_t*)E.q.get((size_t)n);
     uint8_t* ds = (uint8_t*)E.s.get((size_t)m);
@@ -719,6 +731,165 @@ int64_t shard_score_rccl(int kind, const anyseq_scoring& sc) {
     return v;
 }
 
+
+// ---------------------------------------------------------------------------
+// Column-blocked level 1 of the sharded affine construct (DESIGN.md §6.2,
+// align.impala:254-259).  Level 1's halves, both transposed (subject codes as rows),
+// are the two fronts of ONE problem split at row `half`: the forward half is the top
+// front, the reversed one the bottom front.  Shard g fills query columns
+// [c0, c0 + w) of both with the score sharding's boundary-column transport, and its
+// two bottom rows become its segment of the level's columns (zero elsewhere, so the
+// construct's SUM reduction assembles them).  The halves' border modes and kind bits
+// replace the score's; a last-column best cell belongs to the shard that holds the
+// half's last column (the reversed half's: the first).
+void level1_setup(Shard& S, int N, const ShardLevel1& J, int view, std::vector<DPProblem>& probs) {
+    int h1 = 0, h2 = 0;
+    probs.clear();
+    setup_shard(S, N, J.kind, J.sc, J.cs, J.m, J.cq + S.c0, J.n, probs, h1, h2, false, J.half);
+    const bool holds_last[2] = {S.g == N - 1, S.g == 0};
+    const int bm[2] = {J.bm_l, J.bm_r}, am[2] = {J.am_l, J.am_r};
+    int32_t* pb = J.pbest + (size_t)view * J.pstride;
+    for (int f = 0; f < 2; ++f) {
+        DPProblem& P = probs[f];
+        int a = am[f];
+        if ((a & AM_BEST_LASTCOL) == AM_BEST_LASTCOL && !holds_last[f]) a &= ~AM_BEST_LASTCOL;
+        P.bmode = bm[f];
+        P.amode = a;
+        P.best = (a & AM_BEST_LASTCOL) ? pb + f : nullptr;
+    }
+    // bottom row (kernel value space, G or X) -> H / E of the level's columns; a global
+    // (G space) block's frame is shifted by its first column in the half (as the score
+    // combine's), which the job's column offset takes out
+    const size_t vo = (size_t)view * J.nn;
+    const int cr = J.n - S.c0 - S.w;   // the block's first column in the reversed half
+    const bool glob = J.kind == KIND_GLOBAL;
+    S.h_jobs[0] = RowToCol{S.top.out_row.p, J.LH + vo + S.c0, J.LE + vo + S.c0, S.w, h1 - 1,
+                           probs[0].amode != 0 ? 1 : 0, glob ? S.c0 : 0};
+    S.h_jobs[1] = RowToCol{S.bot.out_row.p, J.RH + vo + cr, J.RE + vo + cr, S.w, h2 - 1,
+                           probs[1].amode != 0 ? 1 : 0, glob ? cr : 0};
+    // (synchronous: every shard is set up before any fill is launched)
+    HIPCHECK(hipMemcpy(S.jobs.get(sizeof S.h_jobs), S.h_jobs, sizeof S.h_jobs, hipMemcpyHostToDevice));
+}
+
+// After a shard's fill: its column segments, then the construct's stream waits for it.
+void level1_finish(Shard& S, const ShardLevel1& J) {
+    HIPCHECK(anyseq_launch_aff_row_to_col(S.jobs.p, 2, S.w, -J.sc.gap_extend, S.st));
+    HIPCHECK(hipEventRecord(S.ready, S.st));
+    HIPCHECK(hipStreamWaitEvent(J.st, S.ready, 0));
+}
+
+hipEvent_t level1_event() {
+    static hipEvent_t ev = nullptr;
+    if (!ev) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    return ev;
+}
+
+void check_level1(const ShardLevel1& J, int N) {
+    if (J.n < N) fail("sharded construct level 1: %d query columns cannot be split over %d ranks", J.n, N);
+    if (J.half < 1 || J.half >= J.m) fail("internal: sharded level 1 split %d of %d rows", J.half, J.m);
+    if (g_tuning.R != 1) fail("sharded construct: rows_per_lane must be 1");
+}
+
+// Emulated ranks (anyseq_construct_local_sharded): N in-process shards, view g = rank g.
+void level1_local(const ShardLevel1& J, int N) {
+    check_level1(J, N);
+    Engine& E = engine();   // (the construct holds E.mu)
+    std::vector<Shard>& shards = local_shards();
+    const int max_local = std::max(1, E.num_cus / 8 - 8);
+    if (N > max_local) fail("sharded construct: at most %d emulated ranks on this device (got %d)", max_local, N);
+    if ((int)shards.size() < N) shards.resize(N);
+    check_hw_queues(3 * N - 2);
+    for (int g = 0; g < N; ++g) {
+        shards[g].init();
+        if (g + 1 < N) lazy_stream(shards[g].top.s_send);
+        if (g > 0) lazy_stream(shards[g].bot.s_send);
+    }
+    // behind the construct's stream: the level's zeroed columns and reset best cells
+    HIPCHECK(hipEventRecord(level1_event(), J.st));
+    std::vector<std::vector<DPProblem>> probs(N);
+    for (int g = 0; g < N; ++g) {
+        Shard& S = shards[g];
+        HIPCHECK(hipStreamWaitEvent(S.st, level1_event(), 0));
+        S.g = g;
+        S.c0 = block_c0(g, N, J.n);
+        S.w = block_c0(g + 1, N, J.n) - S.c0;
+        level1_setup(S, N, J, g, probs[g]);
+    }
+    for (int g = 0; g < N; ++g)   // a copy lands in a neighbour's left_in after its sentinel fill
+        for (int k = 0; k < N; ++k)
+            if (k != g) {
+                if (shards[g].top.s_send) HIPCHECK(hipStreamWaitEvent(shards[g].top.s_send, shards[k].ready, 0));
+                if (shards[g].bot.s_send) HIPCHECK(hipStreamWaitEvent(shards[g].bot.s_send, shards[k].ready, 0));
+            }
+    const int grid = grid_per_shard(E, N);
+    for (int g = 0; g < N; ++g) fill_prepare(E, shards[g].fc, probs[g], J.fp, shards[g].st, grid);
+    for (int g = 0; g < N; ++g) fill_launch(shards[g].fc);
+    std::vector<Xfer> xs = local_xfers(shards, N, E.device);
+    std::vector<std::thread> th = start_xfers(xs);
+    std::vector<Shard*> sp;
+    for (int g = 0; g < N; ++g) sp.push_back(&shards[g]);
+    bool ok = true;
+    std::string err;
+    for (int g = 0; g < N; ++g) {
+        try {
+            wait_stream(shards[g].st, 120.0, "sharded construct level 1");
+            fill_finish(shards[g].fc);
+        } catch (const Failure& f) {
+            ok = false;
+            if (err.empty()) err = f.msg;
+        }
+    }
+    finish_xfers(th, xs, sp, ok);
+    for (int g = 0; g < N; ++g)
+        for (Front* f : {&shards[g].top, &shards[g].bot})
+            if (f->s_send) wait_stream(f->s_send, 30.0, "shard transport");
+    if (!ok) fail("%s", err.c_str());
+    for (int g = 0; g < N; ++g) level1_finish(shards[g], J);
+}
+
+// One rank per GPU (anyseq_shard_construct): this rank's block over RCCL.
+void level1_rccl(const ShardLevel1& J) {
+    if (!g_rccl || g_rccl->rank < 0) fail("anyseq_shard_init has not been called");
+    RcclState& R = *g_rccl;
+    check_level1(J, R.world);
+    Engine& E = engine();   // (the construct holds E.mu)
+    Shard& S = R.shard;
+    S.init();
+    check_hw_queues(1 + 2 * ((R.rank > 0) + (R.rank < R.world - 1)));
+    if (R.rank > 0) {
+        lazy_stream(S.top.s_recv);
+        lazy_stream(S.bot.s_send);
+    }
+    if (R.rank < R.world - 1) {
+        lazy_stream(S.top.s_send);
+        lazy_stream(S.bot.s_recv);
+    }
+    HIPCHECK(hipEventRecord(level1_event(), J.st));
+    HIPCHECK(hipStreamWaitEvent(S.st, level1_event(), 0));
+    S.g = R.rank;
+    S.c0 = block_c0(R.rank, R.world, J.n);
+    S.w = block_c0(R.rank + 1, R.world, J.n) - S.c0;
+    std::vector<DPProblem> probs;
+    level1_setup(S, R.world, J, 0, probs);
+    fill_async(E, S.fc, probs, J.fp, S.st, grid_per_shard(E, 1));
+    std::vector<Xfer> xs = rccl_xfers(R, E.device);
+    std::vector<std::thread> th = start_xfers(xs);
+    bool ok = true;
+    std::string err;
+    try {
+        wait_stream(S.st, 300.0, "sharded construct level 1");
+        fill_finish(S.fc);
+    } catch (const Failure& f) {
+        ok = false;
+        err = f.msg;
+    }
+    finish_xfers(th, xs, {&S}, ok);
+    if (!ok) fail("%s", err.c_str());
+    for (hipStream_t t : {S.top.s_send, S.top.s_recv, S.bot.s_send, S.bot.s_recv})
+        if (t) wait_stream(t, 60.0, "shard transport");
+    level1_finish(S, J);
+}
+
 }  // namespace
 }  // namespace host
 }  // namespace anyseq
@@ -852,6 +1023,7 @@ int anyseq_construct_local_sharded(int kind, const anyseq_scoring* sc, const cha
         ConstructShards cs;
         cs.world = nshards;
         cs.local = true;
+        cs.level1 = [nshards](const ShardLevel1& J) { level1_local(J, nshards); };
         const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
                                             lens, alQuery, alSubject, cs);
         if (score) *score = v;
@@ -879,6 +1051,7 @@ int anyseq_shard_construct(int kind, const anyseq_scoring* sc, const char* query
         cs.max_u8 = [comm](uint8_t* p, size_t n, hipStream_t st) {
             NCCLCHECK(ncclAllReduce(p, p, n, ncclUint8, ncclMax, comm, st));
         };
+        cs.level1 = [](const ShardLevel1& J) { level1_rccl(J); };
         const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
                                             lens, alQuery, alSubject, cs);
         if (score) *score = v;

@@ -96,3 +96,27 @@ def level_halves(parts):
         out.append((k + 1, p, "right", off, ln))
         k += 2
     return out
+
+
+# Column-blocked level 1 (anyseq_shard.cpp level1_setup).  Level 1's two
+# halves, transposed (subject as rows), are the two fronts of one problem split at row
+# `half`; rank g fills query columns [c0, c0 + w) of both with the boundary-column
+# transport above.  Its bottom rows are its segments of the level's columns.
+
+def level1_segments(g: int, world: int, n: int):
+    """((first, w) of LH, (first, w) of RH) written by rank g: LH is indexed by query
+    position, RH (the reversed half) by distance from the query's end."""
+    c0, w = block(g, world, n)
+    return (c0, w), (n - c0 - w, w)
+
+
+def level1_frame(kind: int, first: int, gap: int) -> int:
+    """H_true = H_block + this: a global block's top border is the scheme's from its own
+    column 0 (the score's frames, `combine_adjust`); free borders are 0 everywhere."""
+    return first * gap if kind == GLOBAL else 0
+
+
+def level1_best_ranks(world: int):
+    """Ranks holding the last column of (forward, reversed) half: a last-column best
+    cell (semiglobal free end) is theirs alone; every rank's cells count for local."""
+    return world - 1, 0

@@ -306,7 +306,8 @@ def construct_bench(args):
 
 def construct_bench_sharded(args, world, rank, local_rank):
     """configs[2] / [3] over N GPUs (strong scaling, one construct): every rank holds the
-    pair; each Hirschberg level's half fills and the final blocks are dealt round-robin,
+    pair; level 1 is column-blocked over all ranks (boundary columns over RCCL
+    send/recv), later levels' half fills and the final blocks are dealt round-robin,
     the level columns all-reduced over RCCL.  Host strings in and out."""
     import torch
     import torch.distributed as dist
@@ -349,12 +350,13 @@ def construct_bench_sharded(args, world, rank, local_rank):
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "int32",
             "data": "synthetic (main.cpp generator)" if args.config == 2 else "synthetic related-genome pair",
-            "config": {"workload": f"{kind} affine alignment, score + Hirschberg traceback, {n}x{m}, levels "
-                                   f"dealt round-robin over {world} GPUs", "baseline_config": args.config,
-                       "query_len": n, "subject_len": m, "parallelism": f"Hirschberg halves x{world} (RCCL "
-                                                                         "all-reduce of level columns)",
-                       "score": int(score), "transport": "RCCL all-reduce, unmeasured on hardware (no "
-                                                         "multi-GPU run before this one)"},
+            "config": {"workload": f"{kind} affine alignment, score + Hirschberg traceback, {n}x{m}, level 1 "
+                                   f"column-blocked, later levels dealt round-robin over {world} GPUs", "baseline_config": args.config,
+                       "query_len": n, "subject_len": m, "parallelism": f"level-1 column blocks + Hirschberg "
+                                                                         f"halves x{world} (RCCL all-reduce of "
+                                                                         "level columns)",
+                       "score": int(score), "transport": "RCCL send/recv (level 1) + all-reduce, unmeasured "
+                                                         "on hardware (no multi-GPU run before this one)"},
         }
         print(json.dumps(out), flush=True)
     dist.barrier()

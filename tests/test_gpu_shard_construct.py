@@ -1,7 +1,8 @@
 """GPU parity of the sharded affine construct (align.impala:237-311
 distributed by Hirschberg level): `nshards` virtual ranks in one process, one fill
-launch per rank per level, the half fills and final blocks dealt round-robin.  It
-must return exactly the single-GPU construct (which the oracle pins) -- score and
+launch per rank per level, the half fills and final blocks dealt round-robin --
+level 1 column-blocked over all ranks when its halves run transposed (DESIGN.md
+§6.2).  It must return exactly the single-GPU construct (which the oracle pins) -- score and
 both sparse strings -- for every shard count."""
 import hashlib
 import json
@@ -53,3 +54,56 @@ def test_sharded_construct_config2(anyseq):
                                                 sc["gap_extend"])
     assert v == g["score"]
     assert (hashlib.sha256(aq).hexdigest(), hashlib.sha256(as_).hexdigest()) == (g["sha_alq"], g["sha_als"])
+
+
+def related(rng, q, m):
+    """A subject of length m sharing q's prefix with point mutations and indels."""
+    out = bytearray()
+    i = 0
+    while len(out) < m:
+        r = rng.random()
+        if i < len(q) and r < 0.85:
+            out.append(q[i])
+            i += 1
+        elif r < 0.92:
+            out.append(rng.choice(b"ACGT"))
+            i += 1
+        elif r < 0.96:
+            out.append(rng.choice(b"ACGT"))
+        else:
+            i += rng.randint(1, 6)
+    return bytes(out)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_sharded_construct_level1_column_blocks(anyseq, kind):
+    """Column-blocked level 1: rank g fills query columns
+    [g n/N, (g+1) n/N) of both transposed level-1 halves with the boundary-column
+    transport; its bottom rows are its segment of the level's columns.  Shapes: the
+    reversed half one row tall (m one above a power of two), narrow blocks, uneven
+    splits, m a power of two; schemes with and without a free gap open."""
+    rng = random.Random(93)
+    shapes = [(700, 513), (200, 129), (1500, 1025), (3000, 2100), (5000, 4096), (2500, 3000)]
+    for i, (n, m) in enumerate(shapes):
+        sc = SCHEMES[i % len(SCHEMES)]
+        q = rnd(rng, n)
+        s = related(rng, q, m) if i % 2 == 0 else rnd(rng, m)
+        want = anyseq.construct(kind, q, s, *sc)
+        for ns in (2, 3, 5, 8):
+            assert anyseq.construct_local_sharded(kind, q, s, ns, *sc) == want, (kind, n, m, sc, ns)
+
+
+def test_sharded_construct_level1_path_taken(anyseq, monkeypatch):
+    """The column-blocked level 1 runs one fill per rank (round-robin: the two halves'
+    owners only), and both plans give the single-GPU result."""
+    rng = random.Random(94)
+    q = rnd(rng, 3000)
+    s = related(rng, q, 2600)
+    want = anyseq.construct("local", q, s, 2, -1, -2, -1)
+    launches = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("ANYSEQ_SHARD_L1", flag)
+        anyseq.last_fill_stats()
+        assert anyseq.construct_local_sharded("local", q, s, 8, 2, -1, -2, -1) == want, flag
+        launches[flag] = anyseq.last_fill_stats()[1]
+    assert launches["1"] - launches["0"] == 8 - 2, launches

@@ -215,3 +215,83 @@ def test_sharded_construct_plan(world):
                 want[pos + i] = ord("ACGT_"[(b + i) % 5])
             pos += h + 128
         assert al == bytes(want)
+
+
+
+# ------------------------------------ column-blocked construct level 1 (§6.2) --
+def _level1_worker(rank, world, port, cases, results):
+    """Rank g fills its block of query columns of both transposed level-1 halves
+    (pure-Python stand-in fill, linear scores), ships the boundary columns like the
+    score plan, writes its bottom rows into zeroed LH / RH at level1_segments, shifted by
+    level1_frame; a SUM all-reduce must give the columns of the whole halves."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    gap = -1
+    for kind_name, q, s, half in cases:
+        kind = KINDS[kind_name]
+        n = len(q)
+        (c0, w), (r0, _) = SP.level1_segments(rank, world, n)
+        blk = q[c0:c0 + w]
+        rows_f, rows_r = s[:half], s[half:][::-1]
+        lt = None
+        if rank > 0:
+            t = torch.zeros(len(rows_f), dtype=torch.int64)
+            dist.recv(t, src=rank - 1)
+            lt = [int(x) + SP.left_shift_top(kind, rank, world, n, gap) for x in t]
+        Ht = _fill(kind, rows_f, blk, lt)
+        if rank < world - 1:
+            dist.send(torch.tensor([row[w - 1] for row in Ht], dtype=torch.int64), dst=rank + 1)
+        lb = None
+        if rank < world - 1:
+            t = torch.zeros(len(rows_r), dtype=torch.int64)
+            dist.recv(t, src=rank + 1)
+            lb = [int(x) + SP.left_shift_bottom(kind, rank, world, n, gap) for x in t]
+        Hb = _fill(kind, rows_r, blk[::-1], lb)
+        if rank > 0:
+            dist.send(torch.tensor([row[w - 1] for row in Hb], dtype=torch.int64), dst=rank - 1)
+        LH = torch.zeros(n, dtype=torch.int64)
+        RH = torch.zeros(n, dtype=torch.int64)
+        for k in range(w):
+            LH[c0 + k] = Ht[-1][k] + SP.level1_frame(kind, c0, gap)
+            RH[r0 + k] = Hb[-1][k] + SP.level1_frame(kind, r0, gap)
+        dist.all_reduce(LH, op=dist.ReduceOp.SUM)
+        dist.all_reduce(RH, op=dist.ReduceOp.SUM)
+        out.append((LH.tolist(), RH.tolist()))
+    if rank == 0:
+        results.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_level1_column_blocks(world):
+    import torch.multiprocessing as mp
+    rng = random.Random(55 + world)
+    cases = []
+    for kind in KINDS:
+        for n, m in [(9, 7), (40, 33), (57, 64), (31, 17)]:
+            q = bytes(rng.choice(b"ACGT") for _ in range(n))
+            s = bytes(rng.choice(b"ACGT") for _ in range(m))
+            half = 1 << ((m - 1).bit_length() - 1)   # next_pow_2(m) / 2
+            cases.append((kind, q, s, half))
+    ctx = mp.get_context("spawn")
+    results = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_level1_worker, args=(r, world, port, cases, results)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = results.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for (kind, q, s, half), (LH, RH) in zip(cases, got):
+        k = KINDS[kind]
+        want_l = _fill(k, s[:half], q, None)[-1]              # the whole forward half's bottom row
+        want_r = _fill(k, s[half:][::-1], q[::-1], None)[-1]  # the whole reversed half's
+        assert LH == want_l, (kind, len(q), len(s))
+        assert RH == want_r, (kind, len(q), len(s))
+    assert SP.level1_best_ranks(world) == (world - 1, 0)
