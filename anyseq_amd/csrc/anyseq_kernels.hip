@@ -806,10 +806,6 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
     constexpr int GPC = CH / GR;       // granules per chunk
     const int nchunks = (w + CH - 1) / CH;
     const int ngran = (w + GR - 1) / GR;
-    // producers store whole 16-byte column pairs (the asm loop) up to w rounded up to 2:
-    // every column they write gets the sentinel back, so a ring reset after every read
-    // is all sentinel again once the launch is over
-    const int w2 = (w + 1) & ~1;
     // ext: skewed blocks staged past the last chunk (the affine asm epilogue's), whose
     // columns >= w all hold code 0xFF; pscale: units of the ring counter per chunk (the
     // affine fill counts half chunks = granules)
@@ -934,13 +930,17 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                 }
                 // ring of hand-off rows (DPProblem::nslots < ngroups - 1): put the sentinel
                 // back, so the group that reuses this slot 2*grid+2 groups later is polled
-                // against fresh data
+                // against fresh data.  Whole granules, also their columns past w: the
+                // producer stores whole 16-column halves, and a word it left past w would
+                // sit inside the row of a later launch with another layout (device-planned
+                // levels reuse the rows without a sentinel fill) and be read
+                // there as data before that launch's producer wrote it
                 if (reset_in) {
                     T* gw = const_cast<T*>(g_in);
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
                         const int col = c0 + i * 64 + lane;
-                        if (col < c2 && col < w2) HandOff<T>::store(gw + col, HandOff<T>::sentinel());
+                        if (col < c2) HandOff<T>::store(gw + col, HandOff<T>::sentinel());
                     }
                 }
                 in_gran += ready;
@@ -959,6 +959,13 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                 return;
             }
         }
+    }
+    // the producer's last chunk may extend past w (whole-chunk stores of the asm
+    // epilogue): those columns get the sentinel back too, so a ring that is reset
+    // after every read is all sentinel again once the launch is over
+    if (need_in && reset_in) {
+        T* gw = const_cast<T*>(g_in);
+        for (int c = ngran * GR + lane; c < nchunks * CH; c += 64) HandOff<T>::store(gw + c, HandOff<T>::sentinel());
     }
 }
 
@@ -1123,8 +1130,6 @@ struct AffShared {
     uint32_t prod[NW + 1];
     uint32_t cons[NW + 1];
     uint32_t skew[kSkewBlocks][8][64];   // pre-skewed subject, as FillShared::skew
-    // per compute wave: 63 lanes x 16 B + 15 offsets of 16 B (16-byte aligned: b128 stores)
-    __attribute__((aligned(16))) uint32_t pub_dummy[NW][80 * 4];
     uint32_t s_filled;
     uint32_t tail;
     int32_t group;
@@ -1143,7 +1148,6 @@ struct AffIO {
     uint32_t* s_filled;
     uint32_t* tail;
     int2* gout;   // last band of a group: HBM destination of the bottom row (G, F)
-    uint32_t* pub_dummy;   // this wave's dummy store area (the asm loop's non-publishing lanes)
 };
 
 // 32 steps in C++ (prologue / epilogue / partial bands; the steady state is the asm
@@ -1197,10 +1201,7 @@ struct Aff2Args {
     uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs;
     uint64_t gp;
     int q, wm, wx, ll, lh, zlp;
-    uint32_t dw;                  // publishing: this lane's dummy address (lane 63: set per block)
-    uint32_t rs[4];               // publishing to HBM: raw buffer resource of the hand-off row
 };
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifdef ANYSEQ_STAMPS
 #define AF2_NAME(NAME) NAME##_TS
 #define AF2_TS_OUT , [ts] "+s"(ts_v), [te] "+s"(te_v), [tsf] "+s"(ts_f), [nmiss] "+s"(nmiss), [dbp] "+s"(dbp)
@@ -1218,7 +1219,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
                    [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
                    [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
-                   [hm] "s"(hm), [gp] "s"(gp), [dw] "v"(a.dw), [rs] "s"(rs)                                    \
+                   [hm] "s"(hm), [gp] "s"(gp)                                                                  \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
 // the band's last blocks (gen_aff2 epi): + the column-(w-1) capture and the poll clamp
 #define AF2E_ASM(NAME)                                                                                          \
@@ -1231,7 +1232,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
                    [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
                    [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
-                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [dw] "v"(a.dw), [rs] "s"(rs)                    \
+                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch)                                                  \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
 template <bool L, bool BORDER, int PUB, bool LUT, bool EPI = false>
 __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
@@ -1250,7 +1251,6 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
     const uint32_t rb = RFL(a.rb), nb = RFL(a.nb), bvs = RFL(a.bvs);
     const int ge = RFL(-nge);
     const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(a.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)a.gp);
-    const u32x4 rs = {(uint32_t)RFL(a.rs[0]), (uint32_t)RFL(a.rs[1]), (uint32_t)RFL(a.rs[2]), (uint32_t)RFL(a.rs[3])};
 #ifdef ANYSEQ_STAMPS
     ts_f = RFL(ts_f);
     nmiss = RFL(nmiss);
@@ -1325,8 +1325,13 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     constexpr bool ASM_OK = !PARTIAL;
     const bool zero_open = bm == BM_FREE_SEMI_OPEN || bm == BM_FREE_SEMI_T;
     const bool finite_left = bm == BM_NORMAL || bm == BM_FFREE || bm == BM_FPAID;
-    const bool virt = ASM_OK && !shard_left && !zero_open && !(bestmode == 2 && finite_left) &&
-                      !(bestmode == 1 && !clamp) && (!clamp || k.codes) && !(k.flags & 1);
+    // A best of every cell without the clamp takes the virtual cells too: those left of
+    // column -1 are "minus infinity", column -1 is the border.  It cannot win where the
+    // left border is -inf, nor under NORMAL when min(match, mismatch) >= go + ge (flags
+    // bit 4, set by the host): then cell (0,0) >= the largest border cell go + ge.
+    const bool best_border_ok = !(bestmode == 1 && !clamp) || !finite_left || (bm == BM_NORMAL && (k.flags & 16));
+    const bool virt = ASM_OK && !shard_left && !zero_open && !(bestmode == 2 && finite_left) && best_border_ok &&
+                      (!clamp || k.codes) && !(k.flags & 1);
     const int rb = band * 64;
     const int row = rb + lane;
     const bool dead = row >= h;
@@ -1397,20 +1402,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         la.asf = lds_addr(io.s_filled);
         la.atl = lds_addr(io.tail);
         la.skb = lds_addr(io.skew) + 4u * lane;
-        la.lo = 8u * (lane - 48);
-        // publishing: lane 63 stores to the next ring / the hand-off row (address set per
-        // block), the other lanes to a dummy area (LDS) or out of the buffer's range (HBM)
-        la.dw = io.out_lds ? lds_addr(io.pub_dummy) + 16u * (uint32_t)lane : 0x80000000u;
-        {
-            const uint64_t base = (uint64_t)(size_t)io.gout;
-            la.rs[0] = (uint32_t)base;
-            la.rs[1] = (uint32_t)(base >> 32) & 0xffffu;   // stride 0
-            // bytes: stores past column w (rounded up to a 16-byte pair) are dropped, so the
-            // epilogue's extended cells never reach the hand-off row (a reader puts the
-            // sentinel back on the columns it reads)
-            la.rs[2] = io.gout ? (uint32_t)((w + 1) & ~1) * 8u : 0u;
-            la.rs[3] = 0x00020000u;                          // gfx9 raw buffer
-        }
+        la.lo = 8u * (lane - 48);   // publishing lanes 48..63: 16 columns each half block
         la.lid8 = 8u * lane;
         // band 0's top border (value, value + go) in the loop's space
         la.bvb = (uint32_t)(xs ? to_x(B.top(lane, nge), lane) : B.top(lane, nge));
@@ -1739,7 +1731,6 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                 io.next_prod = band < last ? &sh.prod[wave + 1] : nullptr;
                 io.next_cons = band < last ? &sh.cons[wave + 1] : nullptr;
                 io.gout = band < last ? nullptr : g_out;
-                io.pub_dummy = sh.pub_dummy[wave];
                 if ((band + 1) * 64 > P.h) run_band_aff<true>(P, band, lane, io, err, k, fp.dbg);
                 else run_band_aff<false>(P, band, lane, io, err, k, fp.dbg);
             }

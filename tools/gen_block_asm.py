@@ -316,7 +316,6 @@ B_AW, B_AA, B_AT, B_AP = 136, 137, 138, 139   # cmp weight, diag + weight, temp,
 B_SK0, B_SK1 = 140, 148                          # subject words (codes), double buffered
 B_VT, B_VT2, B_VA, B_VB = 156, 157, 158, 159    # temps / LDS addresses
 B_WB = 160                                       # LUT weight bytes of 4 steps
-B_VW = 161                                       # per-lane publishing address
 
 
 NEG_INF = -(1 << 29)   # kAffNeg
@@ -324,7 +323,7 @@ AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..
 
 
 def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
-    """Affine steady-state loop, round 3 (DESIGN.md §3.2): full blocks b .. be-1.
+    """Affine steady-state loop, round 3 (DESIGN.md §3.5): full blocks b .. be-1.
     kind G: G space (X_G = X + (r+c+2)|ge|), no clamp, no best (amode 0).
     kind L: X space (X = H + (r+2)|ge|, a per-ROW shift): the local clamp H >= 0 is
             X >= zl, a per-lane constant, folded into the E update
@@ -334,18 +333,14 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
     lut: the diagonal weight of 4 steps from ONE v_perm_b32 of the lane's 8-entry
          weight table (query code against subject codes 0..7; code 0xFF -> -1)
          and a byte-select SDWA add; else v_cmp + v_cndmask (any codes).
-    Hand-off in HALF chunks (16 columns; the ring counters count halves).  Lane 63's
-    cells of steps 2i, 2i+1 (columns 2i, 2i+1 of chunk b-2) leave at the start of step
-    2i+2 in ONE 16-byte store from every lane: lane 63's address is its slot in the
-    next band's LDS ring (pub lds) or in the HBM hand-off row (pub glob: a raw buffer
-    store whose other lanes are out of range, so dropped), the other lanes' a private
-    dummy area (lds) -- half a store per step, no shift register, no exec switching.
-    The counter of a half follows its last store (step 16, block end).  The consumer
-    reads the first half of its top row at the block start and the second half at
-    step 14 (half 2b+1, polled at step 10): a band trails the one above by about 2.6
-    blocks (64 steps of skew + 16 of granularity + latency).
-    Subject codes of the next block at step 8.  LDS waits are counted (lgkmcnt) over
-    the block's unconditional LDS operations in program order.
+    Hand-off in HALF chunks (16 columns; the ring counters count halves): lane 63's
+    cells leave through a DPP wave_shl:1 shift register, whose lanes 48..63 hold the
+    chunk's first 16 columns after step 16 and its last 16 at the block end -- one
+    ds_write_b64 / global_store_dwordx2 per half.  The consumer reads the first half of
+    its top row at the block start (waiting for half 2b) and the second half at step 14
+    (half 2b+1, polled at step 10), so a band trails the one above by about 2.6 blocks
+    (64 steps of skew + 16 of granularity + latency) instead of whole chunks.
+    Subject codes of the next block at step 8.
     epi: the band's last blocks (some lanes past the last column w-1): every lane keeps
     computing past w (subject code 0xFF; those cells feed no real cell), polls stop at
     the last half (nch = 2 x chunks), the best takes real cells only, and each lane
@@ -355,22 +350,12 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
     out = []
     e = out.append
     sets = (B_SK0, B_SK1)
-    ops = []   # unconditional LDS operations of the current block, in program order
-
-    def lds(tag):
-        ops.append(tag)
-
-    def wait_for(tag):
-        # s_waitcnt until the LDS operation `tag` (and everything before it) is done
-        after = len(ops) - 1 - ops.index(tag)
-        e(f"s_waitcnt lgkmcnt({min(15, after)})")
 
     def top_reads(half):
         """8 ds_read_b128 of top-row pairs [16*half, 16*half+16) (chunk address in VB)."""
         for i in range(8):
             reg = AT0 + 32 * half + 4 * i
             e(f"ds_read_b128 v[{reg}:{reg + 3}], v{B_VB} offset:{128 * half + 16 * i}")
-            lds(f"t{half}{i}")
 
     def ring_addr(breg):
         # ring byte address of chunk `breg` into VB: rb + ((breg << 8) & 4095)
@@ -424,40 +409,37 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
             e("s_add_u32 %[nmiss], %[nmiss], 1")
             e(f"L_nm{tag}{k}_%=:")
 
-    def pub_addr():
-        # this block's stores go to chunk b-2: lane 63's address, the others' dummy
+    def publish(k, half, reg):
+        """Lanes 48..63 of the (G, F) pair `reg` hold 16 columns of chunk b-2: half
+        `half` of the next band's top row (LDS: always written -- a dummy slot and
+        counter 0 while b < 2 -- so the counted lgkmcnt waits stay fixed)."""
+        if pub == "glob":
+            e("s_cmp_lt_u32 %[b], 2")
+            e(f"s_cbranch_scc1 L_nopub{half}{k}_%=")
         e("s_sub_u32 %[x2], %[b], 2")
         e("s_lshl_b32 %[x2], %[x2], 8")
         if pub == "lds":
-            # (b < 2: a slot of chunks 14/15, written again before anyone reads it)
             e("s_and_b32 %[x2], %[x2], 4095")
             e("s_add_u32 %[x2], %[x2], %[nb]")
-        # (glob, b < 2: a huge offset, out of range for lane 63 too)
-        e(f"v_mov_b32_e32 v{B_VW}, %[dw]")
-        e(f"v_writelane_b32 v{B_VW}, %[x2], 63")
-
-    def pub_store(i):
-        # lane 63's cells of steps 2i, 2i+1: one 16-byte store
-        reg = AO0 + 4 * (i % 2)
+        e(f"v_add_u32_e32 v{B_VT}, %[x2], %[lo]")
+        e("s_mov_b64 s[%d:%d], exec" % (TA, TA + 1))
+        e("s_mov_b64 exec, %[hm]")
         if pub == "lds":
-            e(f"ds_write_b128 v{B_VW}, v[{reg}:{reg + 3}] offset:{16 * i}")
-            lds(f"w{i}")
+            e(f"ds_write_b64 v{B_VT}, v[{reg}:{reg + 1}] offset:{128 * half}")
         else:
-            e(f"buffer_store_dwordx4 v[{reg}:{reg + 3}], v{B_VW}, %[rs], 0 offen offset:{16 * i} sc1")
-
-    def pub_counter(half):
-        if pub != "lds":
-            return
-        # 2(b-2) + half + 1 halves published (0 while b < 2)
-        e("s_lshl_b32 %[x2], %[b], 1")
-        e(f"s_sub_u32 %[x2], %[x2], {3 - half}")
-        e("s_max_i32 %[x2], %[x2], 0")
-        e(f"v_mov_b32_e32 v{B_VT2}, %[x2]")
-        e(f"ds_write_b32 %[anp], v{B_VT2}")
-        lds(f"c{half}")
+            e(f"global_store_dwordx2 v{B_VT}, v[{reg}:{reg + 1}], %[gp] offset:{128 * half} sc1")
+        e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
+        if pub == "lds":
+            # counter: 2(b-2) + half + 1 halves published (0 while b < 2)
+            e("s_lshl_b32 %[x2], %[b], 1")
+            e(f"s_sub_u32 %[x2], %[x2], {3 - half}")
+            e("s_max_i32 %[x2], %[x2], 0")
+            e(f"v_mov_b32_e32 v{B_VT2}, %[x2]")
+            e(f"ds_write_b32 %[anp], v{B_VT2}")
+        if pub == "glob":
+            e(f"L_nopub{half}{k}_%=:")
 
     def body(k):
-        ops.clear()
         cs, ns = sets[k], sets[1 - k]
         e("s_add_u32 %[x1], %[b], 1")
         event(k, 0, EVB + 2)          # producer: block EVB+2 starts
@@ -470,8 +452,6 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
         event(k, 4, EVB)              # consumer: first half of chunk EVB seen
         ring_addr("%[b]")
         top_reads(0)
-        if pub != "none":
-            pub_addr()
         if ts:
             e("s_cmp_lg_u32 %[tsf], 0")
             e(f"s_cbranch_scc1 L_nots{k}_%=")
@@ -487,12 +467,8 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
             wait(e, f"bp{k}", "%[sc]", "%[x4]", "%[anc]", tmp=B_VT2)
             e(f"L_nobp{k}_%=:")
         g, f, dg = "%[cur]", "%[fd]", "%[dg]"
+        nsub = 5 if border else 4   # subject reads (+ the border write) at step 8
         for u in range(32):
-            if pub != "none" and u >= 2 and u % 2 == 0:
-                pub_store(u // 2 - 1)
-                if u == 16:
-                    pub_counter(0)
-                    event(k, 1, EVB + 2)   # producer: first half of chunk EVB published
             if u == 8:
                 # next block's subject codes (other register set) and, band 0, its border.
                 # Issued in every block (after the last one they read a stale slot, unused):
@@ -507,17 +483,13 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
                 e(f"v_add_u32_e32 v{B_VA}, %[x2], %[skb]")
                 for i in range(4):
                     e(f"ds_read2st64_b32 v[{ns + 2 * i}:{ns + 2 * i + 1}], v{B_VA} offset0:{2 * i} offset1:{2 * i + 1}")
-                    lds(f"s{i}")
                 if border:
                     border_write("%[x1]")
-                    lds("bw")
             if u == 10 and not border:
                 # poll the producer's counter for the second half (used at step 14)
                 e(f"ds_read_b32 v{B_AP}, %[apr]")
-                lds("poll")
             if u == 14:
                 e("s_waitcnt lgkmcnt(0)")
-                ops.clear()   # everything before is done
                 if not border:
                     e(f"v_readfirstlane_b32 %[x2], v{B_AP}")
                     e("s_max_u32 %[sp], %[sp], %[x2]")
@@ -526,10 +498,14 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
                     wait(e, f"pb{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
                     event(k, 5, EVB)      # consumer: second half seen
                 top_reads(1)
-            if 1 <= u <= 13 and u % 2 == 1:
-                wait_for(f"t0{(u - 1) // 2}")      # first-half read holding T(u-1)
+            if u in (1, 3, 5, 7, 9, 11, 13):
+                i = (u - 1) // 2                   # first-half read holding T(u-1)
+                allowed = (7 - i) + (nsub if u > 8 else 0) + (1 if (u > 10 and not border) else 0)
+                e(f"s_waitcnt lgkmcnt({min(15, allowed)})")
             if u >= 17 and u % 2 == 1:
-                wait_for(f"t1{(u - 17) // 2}")     # second-half read holding T(u-1)
+                i = (u - 17) // 2                  # second-half read holding T(u-1)
+                allowed = (7 - i) + (2 if pub == "lds" else 0)
+                e(f"s_waitcnt lgkmcnt({min(15, allowed)})")
             sw = v(cs + u // 4)
             tg = "%[tfg]" if u == 0 else TG_(u - 1)
             tf = "%[tff]" if u == 0 else TF_(u - 1)
@@ -566,16 +542,24 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
                 e("v_add_u32_e32 %[cnt], -1, %[cnt]")
             if L and u % 2 == 1 and not epi:
                 e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
+            if u >= 2 and pub != "none":
+                e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            if u == 16 and pub != "none":
+                publish(k, 0, AO0 + 6)             # cell pair of step 15: steps 0..15 in lanes 48..63
+                event(k, 1, EVB + 2)               # producer: first half of chunk EVB published
             g, f, dg = OG_(u), OF_(u), tg
-        if pub != "none":
-            pub_store(15)
-            pub_counter(1)
-            event(k, 2, EVB + 2)                   # producer: second half published
         e(f"v_mov_b32_e32 %[cur], {OG_(31)}")
         e(f"v_mov_b32_e32 %[fd], {OF_(31)}")
         e(f"v_mov_b32_e32 %[dg], {TG_(30)}")
+        if pub != "none":
+            e(f"v_mov_b32_dpp {OG_(31)}, {OG_(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_mov_b32_dpp {OF_(31)}, {OF_(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
         e(f"v_mov_b32_e32 %[tfg], {TG_(31)}")
         e(f"v_mov_b32_e32 %[tff], {TF_(31)}")
+        if pub != "none":
+            publish(k, 1, AO0 + 6)                 # pair of step 31: steps 16..31 in lanes 48..63
+            event(k, 2, EVB + 2)                   # producer: second half published
         event(k, 6, EVB)                           # consumer: block EVB ends
         e(f"v_mov_b32_e32 v{B_VT2}, %[x1]")
         if not border:
@@ -673,7 +657,7 @@ def main():
                                 lines.append(f'    "{ln}\\n" \\')
                             lines.append("")
     sclob = ", ".join(f'"s{n}"' for n in range(TA, TB + 2))
-    clob = ", ".join(f'"v{n}"' for n in range(AT0, B_VW + 1))
+    clob = ", ".join(f'"v{n}"' for n in range(AT0, B_WB + 1))
     lines.append(f"#define ANYSEQ_AF2_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, A + 1))
     lines.append(f"#define ANYSEQ_BLOCK_ASM_CLOBBERS {clob}, \"vcc\"")
