@@ -92,6 +92,7 @@ struct Tuning {
     int afflut = 1;      // affine fill: v_perm weight table when the pair has <= 8 symbols
     int slack = 0;       // affine fill: half chunks a band starts behind the structural minimum
     int devplan = 1;     // affine construct: Hirschberg levels planned on the device (one download)
+    int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe
 };
 extern Tuning g_tuning;
 

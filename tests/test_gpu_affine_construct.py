@@ -98,3 +98,25 @@ def test_affine_construct_planned_rows_stay_clean(anyseq, oracle):
         m = rng.randint(900, 2600) | ((it >> 1) & 1)
         kind = KINDS[it % 3]
         same(anyseq, oracle, kind, rnd(rng, n), rnd(rng, m), SCHEMES[it % len(SCHEMES)])
+
+
+@pytest.mark.parametrize("virtual_best", [1, 0])
+def test_affine_construct_virtual_best_border(anyseq, oracle, virtual_best):
+    """Local construct halves with a free end and a NORMAL border take the best of every
+    cell without the clamp; with min(match, mismatch) >= go + ge they run the virtual
+    prologue, whose column -1 border cells cannot exceed cell (0,0).
+    Schemes on both sides of that bound -- (2,-9,-1,-1) and (1,-6,-2,-2) keep the C++
+    prologue -- and mostly-mismatching pairs, where a border cell would win if counted;
+    the option off must give the same."""
+    rng = random.Random(59)
+    anyseq.set_option("virtual_best", virtual_best)
+    try:
+        for it in range(12):
+            sc = [(2, -1, -2, -1), (2, -9, -1, -1), (1, -6, -2, -2), (3, -2, -1, -3)][it % 4]
+            n, m = rng.randint(300, 1500), rng.randint(300, 1500)
+            alph = (b"ACGT", b"AC", b"ACGTNRYK")[it % 3]
+            q = rnd(rng, n, alph)
+            s = rnd(rng, m, alph[::-1] if it % 2 else alph)
+            same(anyseq, oracle, "local", q, s, sc)
+    finally:
+        anyseq.set_option("virtual_best", 1)
