@@ -969,6 +969,132 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
     }
 }
 
+// The linear fill's I/O wave (round 2): whole-chunk hand-off polls.  The affine
+// fill's io_wave above polls 16-column granules ahead of its staging work; on the
+// linear kernel (configs[1], 65536^2) that variant measured 3.44 ms per launch against
+// 3.11 ms with this one (profiles/r03e_c1_kernel_stats.csv, r03f_bench_c1_c3_c4.json),
+// so the linear fill keeps it.
+template <int CH, bool SKEW, typename T = int32_t>
+__device__ void io_wave_lin(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
+                        uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
+                        uint32_t* cons0, uint32_t* err, bool reset_in = false) {
+    constexpr int IRM = kSlots * CH - 1;
+    constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
+    const int nchunks = (w + CH - 1) / CH;
+    const bool need_in = g_in != nullptr;
+    const GLOBAL_AS uint8_t* sg = gmem(s);
+    int s_next = 0, sk_next = 0, in_next = 0;
+    uint32_t idle = 0;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    while (s_next < nchunks || (SKEW && sk_next < nchunks) || (need_in && in_next < nchunks)) {
+        bool progress = false;
+        if (s_next < nchunks) {
+            const uint32_t tl = lds_ld(tail);
+            // the trailing wave in block `tl` still reads columns >= tl*CH - kMaxBack
+            int lim = (int)min((uint32_t)nchunks, tl >= 0x7fffffffu ? (uint32_t)nchunks
+                                                                     : tl + SCH - kMaxBack / CH - 1);
+            lim = min(lim, s_next + 1024 / CH);   // one batch: 16 loads in flight per lane
+            if (lim > s_next) {
+                const int c0 = s_next * CH;
+                uint8_t v[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int c = c0 + i * 64 + lane;
+                    v[i] = (c < w && c < lim * CH) ? sg[s_off + s_step * c] : (uint8_t)0;
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int c = c0 + i * 64 + lane;
+                    if (c < lim * CH) {
+                        const int p = c & (kSRing - 1);
+                        s_ring[p] = v[i];
+                        if (p < 64) s_ring[p + kSRing] = v[i];
+                    }
+                }
+                if (!SKEW) lds_st(s_filled, (uint32_t)lim);
+                s_next = lim;
+                progress = true;
+            }
+        }
+        if (SKEW && sk_next < s_next) {
+            // skewed copy of block b needs raw columns 32b-64 .. 32b+31 (staged: b < s_next)
+            // and a free slot: the trailing wave has finished block b - kSkewBlocks
+            const uint32_t tl = lds_ld(tail);
+            int lim = min(s_next, tl >= 0x7fffffffu ? nchunks : (int)tl + kSkewBlocks);
+            lim = min(lim, sk_next + 8);
+            for (int b = sk_next; b < lim; ++b) {
+                uint32_t d[8];
+                load_sbytes<32>(s_ring, (32 * b - 1 - lane) & (kSRing - 1), d);
+                uint32_t* dst = skew + (b % kSkewBlocks) * 8 * 64 + lane;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) dst[64 * i] = d[i];
+            }
+            if (lim > sk_next) {
+                lds_st(s_filled, (uint32_t)lim);
+                sk_next = lim;
+                progress = true;
+            }
+        }
+        if (need_in && in_next < nchunks) {
+            // The previous group's last band stores its bottom row straight into g_in
+            // (sc1), which the host filled with the sentinel -1 (never a kernel value:
+            // G >= 0 and local H >= 0).  Poll the data itself: a chunk is ready when
+            // none of its columns < w still holds -1.
+            const int lim = min((int)lds_ld(cons0) + kSlots, nchunks);
+            if (lim > in_next) {
+                constexpr int PER = kSlots * CH / 64;   // 2 chunks per load row
+                T v[PER];
+                const int c0 = in_next * CH, c1 = lim * CH;
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int col = c0 + i * 64 + lane;
+                    v[i] = col < c1 && col < w ? HandOff<T>::load(g_in + col) : HandOff<T>::zero();
+                }
+                // leading run of complete chunks
+                int ready = 0;
+                bool stop = false;
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const uint64_t bad = __ballot(HandOff<T>::pending(v[i]));
+                    if (!stop && in_next + 2 * i < lim && (uint32_t)bad == 0u) ++ready; else stop = true;
+                    if (!stop && in_next + 2 * i + 1 < lim && (uint32_t)(bad >> 32) == 0u) ++ready; else stop = true;
+                }
+                if (ready > 0) {
+                    const int c2 = (in_next + ready) * CH;
+#pragma unroll
+                    for (int i = 0; i < PER; ++i) {
+                        const int col = c0 + i * 64 + lane;
+                        if (col < c2) ring0[col & IRM] = v[i];
+                    }
+                    // ring of hand-off rows (DPProblem::nslots < ngroups - 1): put the sentinel
+                    // back, so the group that reuses this slot 2*grid+2 groups later is polled
+                    // against fresh data
+                    if (reset_in) {
+                        T* gw = const_cast<T*>(g_in);
+#pragma unroll
+                        for (int i = 0; i < PER; ++i) {
+                            const int col = c0 + i * 64 + lane;
+                            if (col < c2 && col < w) HandOff<T>::store(gw + col, HandOff<T>::sentinel());
+                        }
+                    }
+                    lds_st(prod0, (uint32_t)(in_next + ready));
+                    in_next += ready;
+                    progress = true;
+                }
+            }
+        }
+        if (!progress) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((++idle & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t_start > SPIN_TICKS || err_set(err))) {
+                atomicOr(err, ERR_SPIN_TIMEOUT | 8u);
+                lds_st(prod0, (uint32_t)nchunks);
+                lds_st(s_filled, (uint32_t)nchunks);
+                return;
+            }
+        }
+    }
+}
+
 template <int KIND, int R, int X, int NW, int CH>
 __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __restrict__ probs,
                                                               const GroupRef* __restrict__ groups, int ngroups_total,
@@ -1023,7 +1149,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
             g_out = P.out_row;
         if (wave == NW) {
             const int32_t* g_in = g.group > 0 ? P.rowbuf + (size_t)((g.group - 1) % P.nslots) * P.wpad : nullptr;
-            io_wave<CH, R == 1 && X == 0 && CH == 32>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0],
+            io_wave_lin<CH, R == 1 && X == 0 && CH == 32>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0],
                                                       &sh.s_filled, &sh.tail, g_in, sh.in_ring[0], &sh.prod[0],
                                                       &sh.cons[0], err, P.nslots < P.ngroups - 1);
         } else {
