@@ -553,7 +553,17 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
     }
     int32_t* res = (int32_t*)E.fc.ctr.get(128) + 4;
     HIPCHECK(hipMemset(res, kind == KIND_LOCAL ? 0 : 0x80, 4));
-    const FillParams fp = make_params(kind, sc);
+    FillParams fp = make_params(kind, sc);
+    // affine: the fills compare alphabet codes (the v_perm weight table);
+    // the transported columns are values, so any consistent recoding is exact
+    const uint8_t *fq = dq, *fs = ds;
+    if (sc.gap_open != 0) {
+        const SeqCodes cd = prepare_codes(E, dq, n, ds, m, E.stream);
+        HIPCHECK(hipStreamSynchronize(E.stream));
+        fq = cd.q;
+        fs = cd.s;
+        fp.alpha = cd.alpha;
+    }
     std::vector<std::vector<DPProblem>> probs(N);
     int h1 = 0, h2 = 0;
     for (int g = 0; g < N; ++g) {
@@ -562,7 +572,7 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
         S.g = g;
         S.c0 = block_c0(g, N, m);
         S.w = block_c0(g + 1, N, m) - S.c0;
-        setup_shard(S, N, kind, sc, dq, n, ds + S.c0, m, probs[g], h1, h2, direct);
+        setup_shard(S, N, kind, sc, fq, n, fs + S.c0, m, probs[g], h1, h2, direct);
         if (kind == KIND_LOCAL) {
             probs[g][0].best = res;
             probs[g][1].best = res;
@@ -699,10 +709,21 @@ int64_t shard_score_rccl(int kind, const anyseq_scoring& sc) {
     S.w = R.w;
     int32_t* res = (int32_t*)S.res.get(64);
     HIPCHECK(hipMemsetAsync(res, kind == KIND_LOCAL ? 0 : 0x80, 4, S.st));
-    const FillParams fp = make_params(kind, sc);
+    FillParams fp = make_params(kind, sc);
+    // affine: alphabet codes of this rank's query and subject block (each rank recodes
+    // its own pair: only the equality of symbols enters the DP, and the ranks exchange
+    // values, never symbols)
+    const uint8_t* fq = (const uint8_t*)R.q.p;
+    const uint8_t* fs = (const uint8_t*)R.s.p;
+    if (sc.gap_open != 0) {
+        const SeqCodes cd = prepare_codes(E, fq, R.n, fs, R.w, S.st);
+        fq = cd.q;
+        fs = cd.s;
+        fp.alpha = cd.alpha;
+    }
     std::vector<DPProblem> probs;
     int h1 = 0, h2 = 0;
-    setup_shard(S, R.world, kind, sc, (const uint8_t*)R.q.p, R.n, (const uint8_t*)R.s.p, R.m, probs, h1, h2);
+    setup_shard(S, R.world, kind, sc, fq, R.n, fs, R.m, probs, h1, h2);
     if (kind == KIND_LOCAL) {
         probs[0].best = res;
         probs[1].best = res;

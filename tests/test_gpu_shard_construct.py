@@ -45,13 +45,15 @@ def test_sharded_construct_multi_level(anyseq):
             assert anyseq.construct_local_sharded(kind, base, bytes(mut[200:5800]), ns, 2, -1, -2, -1) == want, (kind, ns)
 
 
-def test_sharded_construct_config2(anyseq):
-    """configs[2] (SW affine 65536^2) over 4 virtual ranks against the committed fixture."""
+@pytest.mark.parametrize("ranks", [4, 8])
+def test_sharded_construct_config2(anyseq, ranks):
+    """configs[2] (SW affine 65536^2) over 4 and 8 virtual ranks (level 1 column-blocked)
+    against the committed fixture."""
     g = json.load(open(os.path.join(GOLD, "config2_65536.json")))
     q, s = anyseq.main_random_pair(65536, 65536)
     sc = g["scoring"]
-    v, aq, as_ = anyseq.construct_local_sharded(g["kind"], q, s, 4, sc["match"], sc["mismatch"], sc["gap_open"],
-                                                sc["gap_extend"])
+    v, aq, as_ = anyseq.construct_local_sharded(g["kind"], q, s, ranks, sc["match"], sc["mismatch"],
+                                                sc["gap_open"], sc["gap_extend"])
     assert v == g["score"]
     assert (hashlib.sha256(aq).hexdigest(), hashlib.sha256(as_).hexdigest()) == (g["sha_alq"], g["sha_als"])
 
