@@ -794,6 +794,10 @@ struct HandOff<int2> {
 #define ANYSEQ_IO_SKEW_POLLING 8
 #endif
 constexpr int kIoSkewPolling = ANYSEQ_IO_SKEW_POLLING;   // skewed blocks per I/O pass while a hand-off poll is out
+#ifndef ANYSEQ_IO_SLEEP
+#define ANYSEQ_IO_SLEEP 1
+#endif
+constexpr int kIoSleep = ANYSEQ_IO_SLEEP;   // s_sleep units of an affine I/O pass without progress
 
 template <int CH, bool SKEW, typename T = int32_t>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
@@ -951,7 +955,7 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             if (hprio) __builtin_amdgcn_s_setprio(0);
         }
         if (!progress) {
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(kIoSleep);
             if ((++idle & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t_start > SPIN_TICKS || err_set(err))) {
                 atomicOr(err, ERR_SPIN_TIMEOUT | 8u);
                 lds_st(prod0, (uint32_t)(nchunks * pscale));
