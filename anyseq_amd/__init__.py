@@ -96,6 +96,7 @@ _lib.anyseq_set_option.argtypes = [_c_p, _c_int]
 _lib.anyseq_last_fill_timing.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int)]
 _lib.anyseq_last_fill_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int),
                                         ctypes.POINTER(_c_i64)]
+_lib.anyseq_last_shard_plan.restype = _c_int
 _lib.anyseq_main_random_pair.argtypes = [_c_i64, _c_i64, _vp, ctypes.POINTER(_c_i64), _vp,
                                          ctypes.POINTER(_c_i64)]
 
@@ -283,6 +284,12 @@ def last_fill_stats():
     ms, n, c = ctypes.c_double(0.0), _c_int(0), _c_i64(0)
     _lib.anyseq_last_fill_stats(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(c))
     return ms.value, n.value, c.value
+
+
+def last_shard_plan() -> int:
+    """Leading Hirschberg levels of the last sharded construct that were column-blocked
+    over all ranks (0: all round-robin); resets it."""
+    return int(_lib.anyseq_last_shard_plan())
 
 
 def main_random_pair(minlen: int, maxlen: int):

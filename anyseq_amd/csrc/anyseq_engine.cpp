@@ -67,6 +67,8 @@ hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* 
                                       hipStream_t st);
 hipError_t anyseq_launch_aff_level_plan(const AffLevelPlan* plan, hipStream_t st);
 hipError_t anyseq_launch_aff_level_tail(const void* tail, int fill_groups, hipStream_t st);
+hipError_t anyseq_launch_rows_check(const void* rows, size_t nwords, uint32_t sentinel, const void* probs, int nprobs,
+                                    uint32_t* out, int inject, hipStream_t st);
 hipError_t anyseq_launch_fill_prep_planned(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
                                            void* sent, size_t sent_max_bytes, uint32_t sent_value,
                                            const uint32_t* sent_n16, hipStream_t st);
@@ -82,6 +84,7 @@ constexpr int CPU_BLOCK_WIDTH = 1024;              // iteration_cpu.impala:1 (hb
 thread_local std::string g_last_error;
 thread_local double g_fill_ms = 0.0;
 thread_local int g_fill_launches = 0;
+thread_local int g_shard_blocked_levels = 0;   // anyseq_last_shard_plan
 thread_local int64_t g_fill_cells = 0;
 
 void set_last_error(const std::string& m) { g_last_error = m; }
@@ -331,6 +334,12 @@ int waves_per_group() {
     const int nw = g_tuning.NW;
     return (nw == 3 || nw == 4 || nw == 7) ? nw : 8;
 }
+// affine fill: 3 or 4 compute waves per workgroup (one per SIMD), or 7 (two per SIMD
+// beside the I/O wave: the steady state fits 256 VGPRs)
+int aff_waves_per_group() {
+    const int nw = g_tuning.NWa;
+    return (nw == 3 || nw == 7) ? nw : 4;
+}
 
 // ---------------------------------------------------------------- fill --
 // Prepares one batched fill launch over `probs` (host copies; device pointers set):
@@ -366,7 +375,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     C.pending = false;
     const bool aff = fp.affine != 0;
     // the affine fill has one row per lane and hands (G, F) pairs over (twice the row bytes)
-    const int R = aff ? 1 : rows_per_lane(), NW = aff ? (g_tuning.NWa == 3 ? 3 : 4) : waves_per_group();
+    const int R = aff ? 1 : rows_per_lane(), NW = aff ? (aff_waves_per_group()) : waves_per_group();
     const int vpc = aff ? 2 : 1;
     // Persistent grid: at most `grid` groups are in flight, and a group finishes only after
     // its predecessor in the same problem (it consumes that group's last chunk), so the
@@ -789,7 +798,7 @@ int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const ui
     fp.alpha = cd.alpha;
     const uint8_t *dq = cd.q, *ds = cd.s;
     const int wpad = (m + 63) & ~63;
-    const int NW = g_tuning.NWa == 3 ? 3 : 4;
+    const int NW = aff_waves_per_group();
     int32_t* res = (int32_t*)E.fc.ctr.get(128) + 4;
     HIPCHECK(hipMemsetAsync(res, kind == KIND_LOCAL ? 0 : 0x80, 4, st));
     const bool two = g_tuning.fronts > 1 && n >= 2 * 64 * NW;
@@ -1141,7 +1150,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     // the device plan sizes the hand-off rows for the worst split of every level; past a
     // few GB (genome-length halves) the host-built levels keep the exact sizes
     auto plan_rowbuf_bytes = [&]() {
-        const int NWa = g_tuning.NWa == 3 ? 3 : 4;
+        const int NWa = aff_waves_per_group();
         size_t mx = 0;
         for (int p2 = pw; p2 > MIN_PART_WIDTH_HB; p2 /= 2) {
             const int h2 = p2 / 2, parts = (m + h2 - 1) / p2;
@@ -1160,7 +1169,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         // (aff_level_plan_kernel builds the level from the splits on the device), prep,
         // fill, row-to-column, join -- and the splits come back in ONE download after the
         // last level, instead of a download and a host rebuild per level.
-        const int NWa = g_tuning.NWa == 3 ? 3 : 4;
+        const int NWa = aff_waves_per_group();
         struct Lev {
             int pw, half, parts, bpp, bound, nh, slots, grid, want;
             size_t rowbuf_bytes;
@@ -1217,7 +1226,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         void* partial = E.joinbuf.get(std::max<size_t>(max_joinbuf, 16));
         // per level: header (8 words: sentinel uint4s, bound check, cells (u64), tail counter)
         // then one error word per level
-        const size_t tail_words = (size_t)std::max(nlev, 1) * 9;
+        // + with ANYSEQ_CHECK_ROWS, 8 words per level of the hand-off row check
+        const int check_rows = env_int("ANYSEQ_CHECK_ROWS", 0);   // (read per call: tests toggle it)
+        const size_t tail_words = (size_t)std::max(nlev, 1) * (check_rows ? 17 : 9);
         uint32_t* d_tail = (uint32_t*)E.pl_hdr.get(tail_words * 4 + 16);
         uint32_t* d_hdr = d_tail;
         uint32_t* d_err = d_tail + 8 * nlev;
@@ -1233,6 +1244,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             register_static_range(rowpool, max_rowpool);
         }
         HIPCHECK(hipMemsetAsync(d_tail, 0, tail_words * 4, st));
+        uint32_t* d_rchk = d_tail + 9 * (size_t)nlev;   // check words of level li at + 8 * li
+        if (check_rows) HIPCHECK(hipMemsetD32Async(d_rchk, 0xffffffffu, 8 * (size_t)nlev, st));
         static std::atomic<int32_t> g_plan_epoch{0x40000};
         uint32_t* ctr = (uint32_t*)meta;
         std::vector<AffLevelPlan> plans((size_t)nlev);
@@ -1301,6 +1314,16 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li], st));
             HIPCHECK(anyseq_launch_fill_affine(NWa, d_probs, d_groups, L.slots, ctr, d_err + li, &fpl, L.grid, st));
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li + 1], st));
+            if (check_rows) {
+                // the invariant the next launch relies on: every hand-off row word is the
+                // sentinel again (ANYSEQ_CHECK_ROWS=2 first leaves a stale word past w in
+                // level 1's first half with a ring, and puts it back once found: the check's
+                // own test, the construct then fails with the check's message)
+                uint32_t* w = d_rchk + 8 * (size_t)li;
+                HIPCHECK(hipMemsetAsync(w, 0, 4, st));
+                const int inject = check_rows == 2 && li == 0;
+                HIPCHECK(anyseq_launch_rows_check(rowbuf, max_rowbuf / 4, 0x80808080u, d_probs, L.nh, w, inject, st));
+            }
             AffLevelTail T{};
             T.parts = d_parts;
             T.jobs = d_jobs;
@@ -1336,14 +1359,22 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             stage_check(st, "affine level (device plan)");
         }
         HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + 1) * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(h_tail, d_tail, (size_t)nlev * 9 * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(h_tail, d_tail, (size_t)nlev * (check_rows ? 17 : 9) * 4, hipMemcpyDeviceToHost, st));
         {
             const hipError_t e = stream_wait_spin(st);
             if (e != hipSuccess) fail("affine construct levels failed: %s", hipGetErrorString(e));
         }
         bool any_err = false;
         for (int li = 0; li < nlev; ++li) any_err |= h_tail[8 * nlev + li] != 0;
+        for (int li = 0; check_rows && li < nlev; ++li) any_err |= h_tail[9 * nlev + 8 * li] != 0;
         E.pl_dirty = any_err;
+        for (int li = 0; check_rows && li < nlev; ++li) {
+            const uint32_t* c = h_tail + 9 * nlev + 8 * li;
+            if (c[0])
+                fail("hand-off row invariant broken after planned level %d: %u non-sentinel word(s), the first at "
+                     "word %u = half %d, ring slot %d, column %d (half width %d)", li + 1, c[0], c[1], (int)c[2],
+                     (int)c[3], (int)c[4], (int)c[5]);
+        }
         for (int li = 0; li < nlev; ++li) {
             const uint32_t err = h_tail[8 * nlev + li];
             g_stage_level = li + 1;
@@ -1443,7 +1474,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                 l1.pbest = pbest0;
                 l1.pstride = (size_t)2 * parts;
                 l1.st = st;
+                l1.E = &E;
                 l1_blocked = true;
+                g_shard_blocked_levels = 1;
                 continue;
             }
             for (int v = 0; v < nviews; ++v) {
@@ -1937,6 +1970,12 @@ void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells) {
     g_fill_ms = 0.0;
     g_fill_launches = 0;
     g_fill_cells = 0;
+}
+
+int anyseq_last_shard_plan(void) {
+    const int v = g_shard_blocked_levels;
+    g_shard_blocked_levels = 0;
+    return v;
 }
 
 void anyseq_main_random_pair(int64_t minlen, int64_t maxlen, char* query, int64_t* lenq, char* subject,

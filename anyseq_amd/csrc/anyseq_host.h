@@ -163,6 +163,7 @@ SeqCodes prepare_codes(Engine& E, const uint8_t* dq, int n, const uint8_t* ds, i
 Engine& engine();
 int rows_per_lane();
 int waves_per_group();
+int aff_waves_per_group();
 
 FillParams make_params(int kind, const anyseq_scoring& sc);
 // An affine problem of kind `kind` over the whole matrix (or a shard of it): its
@@ -219,6 +220,7 @@ struct ShardLevel1 {
     int32_t* pbest = nullptr;      // view 0's two best cells; view v at + v * pstride
     size_t pstride = 0;
     hipStream_t st = nullptr;      // the construct's stream (level 1 is ordered on it)
+    Engine* E = nullptr;           // the construct's engine (held under E->mu by the caller)
 };
 
 struct ConstructShards {

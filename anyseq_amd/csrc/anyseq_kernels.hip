@@ -3333,6 +3333,7 @@ hipError_t anyseq_launch_fill_affine(int NW, const anyseq::DPProblem* probs, con
     using namespace anyseq;
     // (the asm steady state holds ~150 fixed VGPRs: at most 2 waves per SIMD, NW <= 7)
     if (NW == 3) return launch_fill_aff_n<3>(probs, groups, ngroups, dq, err, *fp, grid, st);
+    if (NW == 7) return launch_fill_aff_n<7>(probs, groups, ngroups, dq, err, *fp, grid, st);
     return launch_fill_aff_n<4>(probs, groups, ngroups, dq, err, *fp, grid, st);
 }
 
@@ -3398,6 +3399,82 @@ hipError_t anyseq_launch_aff_level_plan(const anyseq::AffLevelPlan* plan, hipStr
 
 // One launch per level boundary of the device-planned construct (aff_level_tail_kernel):
 // `fill_groups` workgroups at least, so the next level's sentinel fill spreads over the chip.
+// Hand-off row invariant of the device-planned levels: between
+// planned launches every word of the reused hand-off row buffer holds the sentinel
+// (each consumer puts it back after a read; the I/O wave also on the columns past w).
+// Debug check (ANYSEQ_CHECK_ROWS=1), run after each planned fill before the level's
+// tail launch: out[0] counts non-sentinel words, out[1] the first (lowest) one's index,
+// and the map kernel names its half, ring slot and column from the level's
+// descriptors (out[2..5]: half, slot, column, half width; -1 when the word lies in no
+// half's ring).  inject: first store a stale word past w of the first half with a ring
+// (the check's own regression test), and put it back once found.
+namespace anyseq {
+__global__ __launch_bounds__(256) void rows_check_kernel(const uint32_t* __restrict__ rows, size_t nwords,
+                                                         uint32_t sentinel, uint32_t* out) {
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    const size_t n4 = nwords / 4;
+    const uint4* r4 = reinterpret_cast<const uint4*>(rows);
+    for (size_t i = tid; i < n4; i += nth) {
+        const uint4 v = r4[i];
+        if (v.x != sentinel || v.y != sentinel || v.z != sentinel || v.w != sentinel) {
+            const uint32_t k = v.x != sentinel ? 0 : v.y != sentinel ? 1 : v.z != sentinel ? 2 : 3;
+            atomicAdd(&out[0], 1u);
+            atomicMin(&out[1], (uint32_t)(4 * i + k));
+        }
+    }
+    for (size_t i = 4 * n4 + tid; i < nwords; i += nth)
+        if (rows[i] != sentinel) {
+            atomicAdd(&out[0], 1u);
+            atomicMin(&out[1], (uint32_t)i);
+        }
+}
+__global__ void rows_check_map_kernel(const DPProblem* __restrict__ probs, int nprobs, int32_t* rows, uint32_t* out,
+                                      int repair) {
+    if (threadIdx.x != 0 || out[0] == 0) return;
+    int32_t* w = rows + out[1];
+    // (the check's own test: the injected word is put back, so later levels run on clean rows)
+    if (repair) *w = (int32_t)0x80808080u;
+    out[2] = out[3] = out[4] = 0xffffffffu;
+    for (int p = 0; p < nprobs; ++p) {
+        const DPProblem& P = probs[p];
+        if (P.ngroups <= 1 || !P.rowbuf) continue;
+        const size_t span = (size_t)P.nslots * P.wpad * 2;   // (G, F) int pairs
+        if (w >= P.rowbuf && w < P.rowbuf + span) {
+            const size_t off = (size_t)(w - P.rowbuf);
+            out[2] = (uint32_t)p;
+            out[3] = (uint32_t)(off / ((size_t)P.wpad * 2));
+            out[4] = (uint32_t)((off % ((size_t)P.wpad * 2)) / 2);
+            out[5] = (uint32_t)P.w;
+            return;
+        }
+    }
+}
+// the first half with a hand-off ring: a stale G word at column w of its first slot
+// (past the half's last column; column wpad-1 when w is a multiple of 64)
+__global__ void rows_inject_kernel(const DPProblem* __restrict__ probs, int nprobs) {
+    if (threadIdx.x != 0) return;
+    for (int p = 0; p < nprobs; ++p) {
+        const DPProblem& P = probs[p];
+        if (P.ngroups <= 1 || !P.rowbuf) continue;
+        P.rowbuf[2 * (size_t)min(P.w, P.wpad - 1)] = 0x12345678;
+        return;
+    }
+}
+}  // namespace anyseq
+
+hipError_t anyseq_launch_rows_check(const void* rows, size_t nwords, uint32_t sentinel, const void* probs, int nprobs,
+                                    uint32_t* out, int inject, hipStream_t st) {
+    if (inject)
+        hipLaunchKernelGGL(anyseq::rows_inject_kernel, dim3(1), dim3(64), 0, st, (const anyseq::DPProblem*)probs,
+                           nprobs);
+    const int grid = (int)std::max<size_t>(1, std::min<size_t>(2048, (nwords / 4 + 255) / 256));
+    hipLaunchKernelGGL(anyseq::rows_check_kernel, dim3(grid), dim3(256), 0, st, (const uint32_t*)rows, nwords,
+                       sentinel, out);
+    hipLaunchKernelGGL(anyseq::rows_check_map_kernel, dim3(1), dim3(64), 0, st, (const anyseq::DPProblem*)probs,
+                       nprobs, (int32_t*)rows, out, inject);
+    return hipGetLastError();
+}
+
 hipError_t anyseq_launch_aff_level_tail(const void* tail, int fill_groups, hipStream_t st) {
     const anyseq::AffLevelTail& t = *(const anyseq::AffLevelTail*)tail;
     const int grid = std::max(std::max(1, t.nslices * t.nparts), t.has_next ? fill_groups : 1);

@@ -812,11 +812,25 @@ void check_level1(const ShardLevel1& J, int N) {
 }
 
 // Emulated ranks (anyseq_construct_local_sharded): N in-process shards, view g = rank g.
+// The column-blocked level 1 runs its shards' fills concurrently: emulated ranks need
+// 3N-2 streams (fill + transport) and N co-resident grids of >= 8 workgroups (one per
+// XCD); one rank per GPU needs its fill and up to 4 transport streams.  When the
+// process cannot give it that, the construct deals level 1 round-robin like the later
+// levels instead of failing (same result, bit for bit).
+int hw_queues_available() { return env_int("GPU_MAX_HW_QUEUES", 4) - 2; }   // less the engine's and torch's
+int max_local_level1(int num_cus) { return std::max(1, num_cus / 8 - 8); }
+bool level1_local_possible(int N, int num_cus) {
+    return N >= 2 && N <= max_local_level1(num_cus) && 3 * N - 2 <= hw_queues_available();
+}
+bool level1_rccl_possible(int rank, int world) {
+    return world >= 2 && 1 + 2 * ((rank > 0) + (rank < world - 1)) <= hw_queues_available();
+}
+
 void level1_local(const ShardLevel1& J, int N) {
     check_level1(J, N);
-    Engine& E = engine();   // (the construct holds E.mu)
+    Engine& E = *J.E;   // (the construct holds E.mu; no engine() here: it would release retired blocks mid-call)
     std::vector<Shard>& shards = local_shards();
-    const int max_local = std::max(1, E.num_cus / 8 - 8);
+    const int max_local = max_local_level1(E.num_cus);
     if (N > max_local) fail("sharded construct: at most %d emulated ranks on this device (got %d)", max_local, N);
     if ((int)shards.size() < N) shards.resize(N);
     check_hw_queues(3 * N - 2);
@@ -873,7 +887,7 @@ void level1_rccl(const ShardLevel1& J) {
     if (!g_rccl || g_rccl->rank < 0) fail("anyseq_shard_init has not been called");
     RcclState& R = *g_rccl;
     check_level1(J, R.world);
-    Engine& E = engine();   // (the construct holds E.mu)
+    Engine& E = *J.E;   // (the construct holds E.mu)
     Shard& S = R.shard;
     S.init();
     check_hw_queues(1 + 2 * ((R.rank > 0) + (R.rank < R.world - 1)));
@@ -1040,11 +1054,13 @@ int anyseq_construct_local_sharded(int kind, const anyseq_scoring* sc, const cha
                                    const char* subject, int lens, int nshards, char* alQuery, char* alSubject,
                                    int64_t* score) {
     try {
-        if (nshards < 1 || nshards > 64) fail("sharded construct: 1..64 local shards");
+        if (nshards < 1 || nshards > 64) fail("sharded construct: 1..64 local shards (level 1 column-blocked when the "
+                                              "device and GPU_MAX_HW_QUEUES allow it, else round-robin)");
         ConstructShards cs;
         cs.world = nshards;
         cs.local = true;
-        cs.level1 = [nshards](const ShardLevel1& J) { level1_local(J, nshards); };
+        if (level1_local_possible(nshards, engine().num_cus))
+            cs.level1 = [nshards](const ShardLevel1& J) { level1_local(J, nshards); };
         const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
                                             lens, alQuery, alSubject, cs);
         if (score) *score = v;
@@ -1072,7 +1088,7 @@ int anyseq_shard_construct(int kind, const anyseq_scoring* sc, const char* query
         cs.max_u8 = [comm](uint8_t* p, size_t n, hipStream_t st) {
             NCCLCHECK(ncclAllReduce(p, p, n, ncclUint8, ncclMax, comm, st));
         };
-        cs.level1 = [](const ShardLevel1& J) { level1_rccl(J); };
+        if (level1_rccl_possible(cs.rank, cs.world)) cs.level1 = [](const ShardLevel1& J) { level1_rccl(J); };
         const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
                                             lens, alQuery, alSubject, cs);
         if (score) *score = v;

@@ -22,7 +22,7 @@ Other workloads: --config 1 (configs[1]: NW linear score, 65536^2), --config 3
 Every line carries:
   * roofline  — the dominant kernel (the DP fill) against the §8(d) model of 4 B
     per cell (peak 8 TB/s), plus the VALU-issue ceiling of the same kernel
-    (``roofline.valu``) and the PMC-measured HBM bytes when a profile of this
+    (``roofline.valu_model``) and the PMC-measured HBM bytes when a profile of this
     build exists under profiles/ (``traffic``);
   * cpu_baseline — the oracle restatement of the same workload (a bounded
     prefix sample), at T = 4 (the reference's get_thread_count(),
@@ -67,7 +67,8 @@ METRIC = "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; % of HBM roofline"
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each); default: WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=65536)
@@ -371,10 +372,8 @@ def score_bench(args, world, rank, local_rank):
         args.kind, args.sharded = args.kind or "semiglobal", True
         args.gap_open = args.gap_open or -2
     kind = args.kind or "global"
-    # the sharded path's fill + transport streams each need a hardware queue of their own
-    # (anyseq_shard.cpp check_hw_queues); HIP reads this at its first call
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    if world > 1 or args.sharded:
+        raise_hw_queues()
     import torch
     import anyseq_amd as A
 
@@ -510,6 +509,7 @@ def launch_ranks(args) -> int:
     argv = [a for a in sys.argv[1:]]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr", "127.0.0.1", f"--master-port={args.master_port}", os.path.abspath(__file__)] + argv
+    raise_hw_queues()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     return subprocess.run(cmd, env=env).returncode
 
@@ -532,18 +532,32 @@ def anchor_run(args):
         return {"error": repr(e)}
 
 
+def raise_hw_queues(minimum: int = 16) -> None:
+    """The sharded paths run concurrent fill + transport streams, each needing a hardware
+    queue of its own (anyseq_shard.cpp check_hw_queues; with too few, the column-blocked
+    level 1 falls back to round-robin).  HIP reads GPU_MAX_HW_QUEUES at its first call,
+    so this runs before anything imports torch or anyseq_amd."""
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < minimum:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(minimum)
+
+
 def main():
     args = parse()
     launched = "WORLD_SIZE" in os.environ
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is None:
+        args.gpus = world if launched else 1
     if args.gpus > 1 and not launched:
         raise SystemExit(launch_ranks(args))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if launched and world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1 or args.sharded or args.config == 4:
+        raise_hw_queues()
     if args.dry_run:
-        print(json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local_rank}), flush=True)
+        print(json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local_rank,
+                          "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))}), flush=True)
         return
     if args.config is None:
         args.config = 2 if world == 1 else 4

@@ -103,7 +103,7 @@ void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid);
 
 /* Named tuning option: "rows_per_lane" (1,2,4), "chunk" (16,32 steps per block),
  * "waves_per_group" (3,4,7,8), "grid", "fronts" (1 or 2: score fill as one
- * front or two meeting fronts), "affine_waves_per_group" (3,4), "affine_grid",
+ * front or two meeting fronts), "affine_waves_per_group" (3,4,7), "affine_grid",
  * "ring_slots" (group hand-off rows kept per sub-problem; 0 = 4*grid+4, never
  * fewer than 2*grid+2).
  * Returns 0, or -1 for an unknown name. */
@@ -115,6 +115,11 @@ void anyseq_last_fill_timing(double* ms, int* launches);
 /* The same, plus the DP cells those launches computed (sum of h*w of their
  * sub-problems).  Both reset the counters. */
 void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells);
+/* Plan of the calling thread's most recent sharded construct (anyseq_shard_construct,
+ * anyseq_construct_local_sharded): the number of leading Hirschberg levels whose
+ * halves were column-blocked over all ranks (0: every level dealt round-robin, e.g.
+ * when GPU_MAX_HW_QUEUES is too small for the concurrent shard streams).  Resets it. */
+int anyseq_last_shard_plan(void);
 
 /* ---- column-block sharded score (build-defined) ----
  * Subject columns are split into contiguous blocks, block g = [g*m/N, (g+1)*m/N);

@@ -21,11 +21,27 @@ def test_gpus_two_launches_two_ranks():
     assert sorted(d["rank"] for d in lines) == [0, 1]
     assert all(d["world"] == 2 and d["dry_run"] for d in lines)
     assert sorted(d["local_rank"] for d in lines) == [0, 1]
+    # the sharded construct / score ranks run concurrent shard streams (advisor round 3)
+    assert all(d["hw_queues"] >= 16 for d in lines)
 
 
 def test_gpus_one_runs_in_process():
     lines = run("--gpus", "1", "--dry-run")
-    assert lines == [{"dry_run": True, "rank": 0, "world": 1, "local_rank": 0}]
+    assert [{k: d[k] for k in ("dry_run", "rank", "world", "local_rank")} for d in lines] == \
+        [{"dry_run": True, "rank": 0, "world": 1, "local_rank": 0}]
+
+
+def test_torchrun_without_gpus_flag_takes_world_from_env():
+    """`torchrun --nproc-per-node=2 bench.py` (no --gpus): world comes from WORLD_SIZE."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port=29617", os.path.join(ROOT, "bench.py"), "--dry-run"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["world"] == 2 and d["hw_queues"] >= 16 for d in lines)
 
 
 def test_world_mismatch_is_refused():

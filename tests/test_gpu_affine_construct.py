@@ -100,6 +100,25 @@ def test_affine_construct_planned_rows_stay_clean(anyseq, oracle):
         same(anyseq, oracle, kind, rnd(rng, n), rnd(rng, m), SCHEMES[it % len(SCHEMES)])
 
 
+def test_affine_construct_row_check_fires(anyseq, oracle, monkeypatch):
+    """The hand-off row invariant is checked, not timed (verdict round 3, item 1): with
+    ANYSEQ_CHECK_ROWS (on in this suite, conftest.py) a kernel scans every reused
+    hand-off row after each planned fill.  ANYSEQ_CHECK_ROWS=2 leaves one stale word past
+    w in level 1's first half with a ring: the construct must fail naming that level,
+    half and column, and the next construct (rows re-filled after the failure) must be
+    right again."""
+    rng = random.Random(60)
+    q, s = rnd(rng, 3001), rnd(rng, 2603)
+    assert anyseq.construct("local", q, s, gap_open=-2, gap_extend=-1) == \
+        oracle.affine_construct("local", q, s, 2, -1, -2, -1)
+    monkeypatch.setenv("ANYSEQ_CHECK_ROWS", "2")
+    with pytest.raises(anyseq.AnySeqError, match=r"hand-off row invariant broken after planned level 1: 1 "
+                                                 r"non-sentinel word\(s\).*half 0, ring slot 0, column \d+"):
+        anyseq.construct("local", q, s, gap_open=-2, gap_extend=-1)
+    monkeypatch.setenv("ANYSEQ_CHECK_ROWS", "1")
+    same(anyseq, oracle, "local", q, s, (2, -1, -2, -1))
+
+
 @pytest.mark.parametrize("virtual_best", [1, 0])
 def test_affine_construct_virtual_best_border(anyseq, oracle, virtual_best):
     """Local construct halves with a free end and a NORMAL border take the best of every

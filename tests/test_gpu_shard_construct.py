@@ -109,3 +109,21 @@ def test_sharded_construct_level1_path_taken(anyseq, monkeypatch):
         assert anyseq.construct_local_sharded("local", q, s, 8, 2, -1, -2, -1) == want, flag
         launches[flag] = anyseq.last_fill_stats()[1]
     assert launches["1"] - launches["0"] == 8 - 2, launches
+
+
+def test_sharded_construct_level1_queue_fallback(anyseq, monkeypatch):
+    """Advisor round 3: the column-blocked level 1 needs 3N-2 concurrent shard streams.
+    Under the box default of 4 hardware queues it must fall back to the round-robin
+    level 1 (same result, anyseq_last_shard_plan() == 0) instead of failing; with enough
+    queues it is taken (== 1)."""
+    rng = random.Random(95)
+    q = rnd(rng, 2500)
+    s = related(rng, q, 2200)
+    want = anyseq.construct("local", q, s, 2, -1, -2, -1)
+    plans = {}
+    for queues in ("4", "24"):
+        monkeypatch.setenv("GPU_MAX_HW_QUEUES", queues)   # (this process has 24; the check reads the variable)
+        anyseq.last_shard_plan()
+        assert anyseq.construct_local_sharded("local", q, s, 2, 2, -1, -2, -1) == want, queues
+        plans[queues] = anyseq.last_shard_plan()
+    assert plans == {"4": 0, "24": 1}, plans

@@ -295,3 +295,19 @@ def test_sharded_level1_column_blocks(world):
         assert LH == want_l, (kind, len(q), len(s))
         assert RH == want_r, (kind, len(q), len(s))
     assert SP.level1_best_ranks(world) == (world - 1, 0)
+
+
+def test_rccl_worker_cases_cover_column_blocked_level1():
+    """tools/rccl_ranks.py (the 2-GPU RCCL parity worker) must include constructs whose
+    level 1 is column-blocked over the ranks (level1_rccl) as well as round-robin ones,
+    and say which it expects (checked there through anyseq_last_shard_plan)."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "rccl_ranks.py")
+    spec = importlib.util.spec_from_file_location("rccl_ranks", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    blocked = [c for c in mod.CONSTRUCT_CASES if c[3]]
+    assert blocked and any(not c[3] for c in mod.CONSTRUCT_CASES)
+    for kind, n, m, exp in mod.CONSTRUCT_CASES:
+        assert mod.level1_expected(n, m, 2) == exp, (kind, n, m)
+    assert {c[0] for c in blocked} >= {"local", "semiglobal"}

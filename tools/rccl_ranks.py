@@ -10,40 +10,67 @@ anyseq_shard_score / anyseq_shard_construct, whose boundary columns and level
 columns travel over RCCL; rank 0 prints one JSON line per case and
 ALL_MATCH / MISMATCH; the exit status is 0 only if every case matches.
 
+Construct cases (CONSTRUCT_CASES): a subject longer than the query (n < m: level 1's
+transposed halves are shorter than the query, so level 1 is dealt round-robin) and
+square pairs, where level 1 is column-blocked over the ranks (level1_rccl, the
+boundary columns over RCCL send/recv); every case asserts through
+anyseq_last_shard_plan which plan ran.  RCCL_FIXTURE=1 adds the configs[2] fixture
+(tests/golden/config2_65536.json, SW affine 65536^2: score and SHA-256 of both strings).
+
 RCCL refuses two ranks on one device ("Duplicate GPU detected", ncclInvalidUsage,
 measured on the 1-GPU box), so this needs a multi-GPU node;
 tests/test_gpu_rccl_ranks.py runs it there and skips on fewer GPUs.
 """
+import hashlib
 import json
 import os
 import sys
 import time
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-import torch.distributed as dist  # noqa: E402
+SCORE_CASES = [("global", 0), ("semiglobal", 0), ("local", 0), ("global", -2), ("semiglobal", -2), ("local", -2)]
+# (kind, n, m, level 1 column-blocked?)  The column-blocked level 1 needs the halves
+# transposed and the query longer than the level's split row (anyseq_engine.cpp).
+CONSTRUCT_CASES = [("semiglobal", 8192, 16384, False), ("local", 8192, 16384, False),
+                   ("local", 16384, 16384, True), ("semiglobal", 16384, 16384, True),
+                   ("global", 12000, 9000, True)]
 
-import anyseq_amd as A  # noqa: E402
-from anyseq_amd import sharded  # noqa: E402
+
+def level1_expected(n: int, m: int, world: int) -> bool:
+    """Whether the engine column-blocks level 1 of an n x m construct over `world` ranks
+    (the same test as anyseq_engine.cpp: one part, transposed halves, len > half)."""
+    if world < 2 or n < world:
+        return False
+    half = 1
+    while half < m:
+        half *= 2
+    half //= 2
+    return n > half
 
 
 def main():
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import anyseq_amd as A
+    from anyseq_amd import sharded
+
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     A.set_device(local_rank)
     n, m = int(os.environ.get("PROBE_N", "8192")), int(os.environ.get("PROBE_M", "16384"))
-    q, s = A.main_random_pair(max(n, m), max(n, m))
-    q, s = q[:n], s[:m]
-    cases = [("global", 0), ("semiglobal", 0), ("local", 0), ("global", -2), ("semiglobal", -2), ("local", -2)]
-    ref = {c: A.score(c[0], q, s, gap_open=c[1]) for c in cases}
-    ref_c = {k: A.construct(k, q, s, gap_open=-2) for k in ("semiglobal", "local")}
+    L = max(n, m, max(c[1] for c in CONSTRUCT_CASES), max(c[2] for c in CONSTRUCT_CASES))
+    Q, S = A.main_random_pair(L, L)
+    q, s = Q[:n], S[:m]
+    ref = {c: A.score(c[0], q, s, gap_open=c[1]) for c in SCORE_CASES}
+    ref_c = {c: A.construct(c[0], Q[:c[1]], S[:c[2]], gap_open=-2) for c in CONSTRUCT_CASES}
     dist.barrier()
     sharded.init(dist, rank, world)
     sharded.load(q, s, rank, world)
     ok = True
-    for c in cases:
+    for c in SCORE_CASES:
         t = time.time()
         got = sharded.score(c[0], gap_open=c[1])
         dt = time.time() - t
@@ -52,16 +79,37 @@ def main():
         if rank == 0:
             print(json.dumps({"op": "score", "kind": c[0], "gap_open": c[1], "n": n, "m": m, "world": world,
                               "single": ref[c], "rccl": got, "match": good, "s": round(dt, 4)}), flush=True)
-    for k in ("semiglobal", "local"):
+    for c in CONSTRUCT_CASES:
+        k, cn, cm, blocked = c
         t = time.time()
-        got = sharded.construct(k, q, s, gap_open=-2)
+        A.last_shard_plan()
+        got = sharded.construct(k, Q[:cn], S[:cm], gap_open=-2)
+        plan = A.last_shard_plan()
         dt = time.time() - t
-        exp = ref_c[k]
+        exp = ref_c[c]
         good = got[0] == exp[0] and got[1] == exp[1] and got[2] == exp[2]
+        plan_ok = (plan >= 1) == blocked == level1_expected(cn, cm, world)
+        ok &= good and plan_ok
+        if rank == 0:
+            print(json.dumps({"op": "construct", "kind": k, "n": cn, "m": cm, "gap_open": -2, "world": world,
+                              "single": exp[0], "rccl": got[0], "strings_equal": good, "blocked_levels": plan,
+                              "plan_ok": plan_ok, "s": round(dt, 4)}), flush=True)
+    if os.environ.get("RCCL_FIXTURE") == "1":
+        with open(os.path.join(ROOT, "tests", "golden", "config2_65536.json")) as f:
+            fx = json.load(f)
+        Qf, Sf = A.main_random_pair(65536, 65536)
+        sc = fx["scoring"]
+        t = time.time()
+        A.last_shard_plan()
+        got = sharded.construct(fx["kind"], Qf, Sf, sc["match"], sc["mismatch"], sc["gap_open"], sc["gap_extend"])
+        plan = A.last_shard_plan()
+        dt = time.time() - t
+        h = [hashlib.sha256(x).hexdigest() for x in got[1:]]
+        good = got[0] == fx["score"] and h[0] == fx["sha_alq"] and h[1] == fx["sha_als"] and plan >= 1
         ok &= good
         if rank == 0:
-            print(json.dumps({"op": "construct", "kind": k, "gap_open": -2, "world": world, "single": exp[0],
-                              "rccl": got[0], "strings_equal": good, "s": round(dt, 4)}), flush=True)
+            print(json.dumps({"op": "fixture", "name": "config2_65536", "world": world, "score": got[0],
+                              "match": good, "blocked_levels": plan, "s": round(dt, 4)}), flush=True)
     dist.barrier()
     sharded.finalize()
     dist.destroy_process_group()
