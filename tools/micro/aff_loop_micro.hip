@@ -21,6 +21,7 @@ struct alignas(16) Sh {
     int2 next[kMaxW][16 * 32];    // each wave's out-ring
     uint32_t skew[32][8][64];     // pre-skewed subject codes (64 KiB)
     uint32_t ctr[kMaxW][8];       // prod, cons, next prod, next cons, s_filled, tail
+    uint32_t dummy[kMaxW][320];   // "st" publishing: the non-publishing lanes' store targets
 };
 
 template <int V>
@@ -48,6 +49,7 @@ __global__ __launch_bounds__(512) void micro(int nblocks, unsigned long long* ou
                    anc = la(&sh.ctr[wave][3]), asf = la(&sh.ctr[wave][4]), atl = la(&sh.ctr[wave][5]);
     const uint32_t skb = la(&sh.skew[0][0][0]) + 4u * lane, lo = 8u * (lane - 48), lid8 = 8u * lane;
     const uint32_t bvb = 0, bvs = RFL(1u);
+    const uint32_t pm63 = lane == 63 ? 0xffffffffu : 0u, pdb = lane == 63 ? 0u : la(&sh.dummy[wave][0]) + 16u * lane;
     const int ge = RFL(-1);
     const uint64_t hm = 0xffff000000000000ull, gp = 0;
     uint32_t b = 0, sp = 0, sf = 0, sc = 0, pf = 0, st, x0, x1, x2, x3, x4, be = RFL((uint32_t)nblocks);
@@ -61,13 +63,15 @@ __global__ __launch_bounds__(512) void micro(int nblocks, unsigned long long* ou
                  : [be] "s"(be), [q] "v"(q), [wm] "v"(wm), [wx] "v"(wx), [ll] "v"(ll), [lh] "v"(lh), [go] "v"(go), \
                    [ge] "s"(ge), [zlp] "v"(zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(apr), [acn] "v"(acn),     \
                    [anp] "v"(anp), [anc] "v"(anc), [asf] "v"(asf), [atl] "v"(atl), [skb] "v"(skb), [lo] "v"(lo),  \
-                   [lid8] "v"(lid8), [bvb] "v"(bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp)                \
+                   [lid8] "v"(lid8), [bvb] "v"(bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp), [pm63] "v"(pm63),   \
+                   [pdb] "v"(pdb)                                                                            \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
     if constexpr (V == 0) LOOP(ANYSEQ_AF2_L_B0_LDS_U1);
     if constexpr (V == 1) LOOP(ANYSEQ_AF2_L_B0_NONE_U1);
     if constexpr (V == 2) LOOP(ANYSEQ_AF2_G_B0_LDS_U1);
     if constexpr (V == 3) LOOP(ANYSEQ_AF2_G_B0_NONE_U1);
     if constexpr (V == 4) LOOP(ANYSEQ_AF2_L_B0_LDS_U0);
+
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
     sink[blockIdx.x * blockDim.x + threadIdx.x] = g + fdn + dg + e + hg + bx + tfg + tff + (int)st;
     if (lane == 0) out[blockIdx.x * kMaxW + wave] = c1 - c0;
