@@ -341,6 +341,34 @@ int aff_waves_per_group() {
     return (nw == 3 || nw == 7) ? nw : 4;
 }
 
+// Affine fill, waves per workgroup of one launch: a launch is bound by
+// its longest band chain (chain_steps = w + 1.28 h of its tallest problem, one step per
+// wave step) or by its total work (wave_steps over the grid's compute waves).  One
+// compute wave per SIMD (NW 4) runs a wave step in ~63 cycles; two per SIMD (NW 7) share
+// the SIMD's VALU at ~100 cycles each: 1.26x the throughput, 1.55x the chain step
+// (measured, tools/micro/aff_loop_micro.hip, profiles/r04_ab_nw_st.json).  Chain-bound
+// launches (every configs[2] Hirschberg level) keep 4; throughput-bound ones (the
+// genome-length fills, bands >> waves) take 7.  An explicit affine_waves_per_group wins.
+int aff_waves_for(int64_t chain_steps, int64_t wave_steps, int grid) {
+    if (g_tuning.NWa == 3 || g_tuning.NWa == 4 || g_tuning.NWa == 7) return g_tuning.NWa;
+    const double g = (double)std::max(grid, 1);
+    const double t4 = std::max((double)chain_steps, (double)wave_steps / (4.0 * g));
+    const double t7 = 1.55 * std::max((double)chain_steps, (double)wave_steps / (7.0 * g));
+    return t7 < 0.9 * t4 ? 7 : 4;
+}
+
+namespace {
+void aff_launch_model(const std::vector<DPProblem>& probs, int64_t& chain, int64_t& work) {
+    chain = 0;
+    work = 0;
+    for (const DPProblem& P : probs) {
+        if (P.h <= 0 || P.w <= 0) continue;
+        chain = std::max(chain, (int64_t)P.w + (int64_t)P.h * 128 / 100);
+        work += (int64_t)((P.h + 63) / 64) * ((int64_t)P.w + 64);
+    }
+}
+}  // namespace
+
 // ---------------------------------------------------------------- fill --
 // Prepares one batched fill launch over `probs` (host copies; device pointers set):
 // every allocation, upload and sentinel fill, enqueued on st.  No kernel yet.
@@ -375,7 +403,14 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     C.pending = false;
     const bool aff = fp.affine != 0;
     // the affine fill has one row per lane and hands (G, F) pairs over (twice the row bytes)
-    const int R = aff ? 1 : rows_per_lane(), NW = aff ? (aff_waves_per_group()) : waves_per_group();
+    int NW = waves_per_group();
+    const int R = aff ? 1 : rows_per_lane();
+    if (aff) {
+        int64_t chain, work;
+        aff_launch_model(probs, chain, work);
+        const int g0 = grid_req > 0 ? grid_req : (g_tuning.grida > 0 ? g_tuning.grida : E.num_cus);
+        NW = aff_waves_for(chain, work, g0);
+    }
     const int vpc = aff ? 2 : 1;
     // Persistent grid: at most `grid` groups are in flight, and a group finishes only after
     // its predecessor in the same problem (it consumes that group's last chunk), so the
@@ -1095,8 +1130,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     sp.nb = (m + MIN_PART_WIDTH_HB - 1) / MIN_PART_WIDTH_HB;
     sp.v.assign((size_t)sp.nb + 1, SPLIT_UNSET);
     std::vector<int32_t> typ((size_t)sp.nb + 1, T_H);
-    int pw = next_pow_2(m);
-    sp.bpp = pw / MIN_PART_WIDTH_HB;
+    // levels: P = 1, 2, 4, .. < nb parts, each split at its middle block (aff_part_geo)
+    sp.bpp = 0;
+    // the widest half of the level with P parts (ceil(ceil(nb / P) / 2) blocks)
+    auto level_half = [&](int P) { return MIN_PART_WIDTH_HB * (((sp.nb + P - 1) / P + 1) / 2); };
     sp.v[0] = 0;
     sp.v[sp.nb] = n;
     if (kind != KIND_GLOBAL) {
@@ -1149,11 +1186,21 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     double t_wake = now_us();
     // the device plan sizes the hand-off rows for the worst split of every level; past a
     // few GB (genome-length halves) the host-built levels keep the exact sizes
+    // a planned level's waves per workgroup, from its nominal shape (parts of n/parts rows;
+    // halves of `half` columns, transposed when taller than wide)
+    auto level_nw = [&](int half, int parts) {
+        const int64_t rows = std::max<int64_t>(1, (int64_t)n / std::max(parts, 1));
+        const bool tr = g_tuning.afft && rows > half;
+        const int64_t h = tr ? half : rows, w = tr ? rows : half;
+        const int64_t chain = w + h * 128 / 100, work = 2 * (int64_t)parts * ((h + 63) / 64) * (w + 64);
+        const int g0 = g_tuning.grida > 0 ? g_tuning.grida : E.num_cus;
+        return aff_waves_for(chain, work, g0);
+    };
     auto plan_rowbuf_bytes = [&]() {
-        const int NWa = aff_waves_per_group();
         size_t mx = 0;
-        for (int p2 = pw; p2 > MIN_PART_WIDTH_HB; p2 /= 2) {
-            const int h2 = p2 / 2, parts = (m + h2 - 1) / p2;
+        for (int parts = 1; parts < sp.nb; parts *= 2) {
+            const int h2 = level_half(parts);
+            const int NWa = level_nw(h2, parts);
             const int maxh = g_tuning.afft ? h2 : std::max(h2, n);
             const int bound = std::max(1, ((maxh + 63) / 64 + NWa - 1) / NWa);
             const int grid = std::max(1, std::min(g_tuning.grida > 0 ? g_tuning.grida : E.num_cus, 2 * parts * bound));
@@ -1164,28 +1211,28 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         }
         return mx;
     };
+    bool planned = false;
     if (!sharded && g_tuning.devplan && plan_rowbuf_bytes() <= ((size_t)8 << 30) && n < 8192 * 4096 - 1) {
         // Device-planned levels: every level is enqueued up front -- plan
         // (aff_level_plan_kernel builds the level from the splits on the device), prep,
         // fill, row-to-column, join -- and the splits come back in ONE download after the
         // last level, instead of a download and a host rebuild per level.
-        const int NWa = aff_waves_per_group();
         struct Lev {
-            int pw, half, parts, bpp, bound, nh, slots, grid, want;
+            int half, parts, bound, nh, slots, grid, want, nw;   // half: the level's widest half
             size_t rowbuf_bytes;
         };
         std::vector<Lev> lv;
         size_t max_meta = 0, max_rowbuf = 0, max_rowpool = 0, max_joinbuf = 0;
         int max_parts = 1;
         const int nsl = std::max(1, (n + 1 + 4095) / 4096);   // join slices of the longest possible part
-        for (int p2 = pw, b2 = sp.bpp; p2 > MIN_PART_WIDTH_HB; p2 /= 2, b2 /= 2) {
+        for (int P = 1; P < sp.nb; P *= 2) {
             Lev L;
-            L.pw = p2;
-            L.half = p2 / 2;
-            L.parts = (m + L.half - 1) / p2;
-            L.bpp = b2;
+            L.half = level_half(P);
+            L.parts = P;
             // a half runs at most `half` rows (taller ones transposed), else up to n
             const int maxh = g_tuning.afft ? L.half : std::max(L.half, n);
+            L.nw = level_nw(L.half, L.parts);
+            const int NWa = L.nw;
             L.bound = std::max(1, ((maxh + 63) / 64 + NWa - 1) / NWa);
             L.nh = 2 * L.parts;
             L.slots = L.nh * L.bound;
@@ -1260,16 +1307,16 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             AffLevelPlan& A = plans[li];
             A = AffLevelPlan{};
             A.parts = L.parts;
-            A.bpp = L.bpp;
+            A.bpp = 0;
             A.nb = sp.nb;
             A.half = L.half;
-            A.pw = L.pw;
+            A.pw = 0;
             A.m = m;
             A.n = n;
             A.kind = kind;
             A.best_bits = local ? AM_BEST_ALL : AM_BEST_LAST;
             A.afft = g_tuning.afft ? 1 : 0;
-            A.NW = NWa;
+            A.NW = L.nw;
             A.want_slots = L.want;
             A.bound = L.bound;
             A.epoch = epoch;
@@ -1312,7 +1359,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             fpl.slack = g_tuning.slack;
             fpl.dbg = nullptr;
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li], st));
-            HIPCHECK(anyseq_launch_fill_affine(NWa, d_probs, d_groups, L.slots, ctr, d_err + li, &fpl, L.grid, st));
+            HIPCHECK(anyseq_launch_fill_affine(L.nw, d_probs, d_groups, L.slots, ctr, d_err + li, &fpl, L.grid, st));
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li + 1], st));
             if (check_rows) {
                 // the invariant the next launch relies on: every hand-off row word is the
@@ -1400,11 +1447,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             score = kind == KIND_SEMIGLOBAL ? std::max(s32, 0) : s32;
             if (kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
         }
-        pw = MIN_PART_WIDTH_HB;   // (the host loop below has nothing left)
+        planned = true;   // (the host loop below has nothing left)
     }
-    while (pw > MIN_PART_WIDTH_HB) {
-        const int half = pw / 2;
-        const int parts = (m + half - 1) / pw;
+    for (int parts = 1; !planned && parts < sp.nb; parts *= 2) {
         ++g_stage_level;
         // free-end best cells, 2 per part, per view
         int32_t* pbest0 = (int32_t*)E.bmax.get((size_t)nviews * 2 * parts * 4);
@@ -1421,9 +1466,15 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         // transposed halves' bottom rows: sum of part heights <= n (parts' rows are disjoint)
         int32_t* rowpool = (int32_t*)E.outrow.get((size_t)2 * ((size_t)n + 64 * (size_t)parts) * 2 * 4);
         for (int p = 0; p < parts; ++p) {
-            const int sb = p * sp.bpp - 1, eb = std::min((p + 1) * sp.bpp - 1, sp.nb - 1);
+            const AffPartGeo pg = aff_part_geo(sp.nb, m, parts, p);
+            const int sb = pg.sb, eb = pg.eb, half = pg.lw;
             PartInfo& pi = pinfo[p];
-            pi.split_index = p * sp.bpp + sp.bpp / 2 - 1;
+            pi.split_index = pg.mid;
+            pi.lhw = pg.lw;
+            if (pg.lw <= 0 || pg.hw <= 0) {   // a one-block part: no split
+                pi.flags = 8;
+                continue;
+            }
             const int ts = tp(sb), te = tp(eb);
             if (ts == T_BEFORE || te == T_AFTER) {   // empty part: so are both halves
                 pi.flags = 4;
@@ -1431,10 +1482,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                 pi.off = sp.at(sb);
                 continue;
             }
-            int off, len;
-            sp.dims(p, off, len);
-            const int hoj_l = p * pw, hoj_r = p * pw + half;
-            const int hw = std::min(half, m - hoj_r);
+            const int off = sp.at(sb), len = sp.at(eb) - off;
+            const int hoj_l = pg.hoj_l, hoj_r = pg.hoj_r, hw = pg.hw;
             const bool sfree = ts == T_AFTER, efree = te == T_BEFORE;
             pi.off = off;
             pi.len = len;
@@ -1555,7 +1604,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         const size_t nsl = (size_t)std::max(1, (maxlen + 1 + 4095) / 4096);
         void* partial = E.joinbuf.get((size_t)parts * nsl * 8);
         // (view 0's columns: after the reduction every view holds the same)
-        HIPCHECK(anyseq_launch_aff_hb_join2(d_parts, parts, maxlen, half, LH0, LE0, RH0, RE0, pbest0, sc.gap_open,
+        HIPCHECK(anyseq_launch_aff_hb_join2(d_parts, parts, maxlen, 0, LH0, LE0, RH0, RE0, pbest0, sc.gap_open,
                                             sc.gap_extend, partial, d_spl, d_typ, level1 ? d_score : nullptr, st));
         stage_check(st, "aff_hb_join");
         HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + (level1 ? 1 : 0)) * 4, hipMemcpyDeviceToHost, st));
@@ -1578,6 +1627,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         // every split this level set lies inside its part and has a known type (the
         // next level's sub-problems are built from them)
         for (int p = 0; p < parts; ++p) {
+            if (pinfo[p].flags & 8) continue;   // a one-block part: nothing split
             const int si = pinfo[p].split_index + 1;
             const int lo = pinfo[p].off, hi = (pinfo[p].flags & 4) ? lo : lo + std::max(pinfo[p].len, 0);
             if (sp.v[si] < lo || sp.v[si] > hi || typ[si] < T_H || typ[si] > T_AFTER)
@@ -1590,8 +1640,6 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             level1 = false;
             if (kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
         }
-        pw /= 2;
-        sp.bpp /= 2;
     }
     // final 128-column blocks: each view walks its own into its strings
     std::vector<BlockInfo>& blocks = E.host_blocks;   // outlives the async upload

@@ -82,7 +82,7 @@ struct Tuning {
     int NW = 4;
     int grid = 0;
     int fronts = 2;
-    int NWa = 4;     // affine fill: compute waves per workgroup (3 or 4)
+    int NWa = 0;     // affine fill: compute waves per workgroup (3, 4 or 7; 0 = chosen per launch)
     int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
     int affasm = 1;  // affine fill: bit 0 asm steady state; bit 1 no asm epilogue; bits 2/3 none for best-all / other
     int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
@@ -164,6 +164,7 @@ Engine& engine();
 int rows_per_lane();
 int waves_per_group();
 int aff_waves_per_group();
+int aff_waves_for(int64_t chain_steps, int64_t wave_steps, int grid);
 
 FillParams make_params(int kind, const anyseq_scoring& sc);
 // An affine problem of kind `kind` over the whole matrix (or a shard of it): its

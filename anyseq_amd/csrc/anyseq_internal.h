@@ -146,7 +146,31 @@ struct PartInfo {
     int32_t emode;        // affine construct: border mode of the reversed right half (the part's end)
     int32_t flags;        // affine construct: bit 0 free start, bit 1 free end, bit 2 empty part
     int32_t empty_type;   // affine construct, empty part: the type its split inherits
+    int32_t lhw;          // affine construct: left-half width (the parts' widths vary, aff_part_geo)
 };
+
+// Part p of a Hirschberg level of the build-defined affine construct (DESIGN.md §3.4,
+// oracle aff_part): the level has P = 2^(k-1) parts; part p holds the 128-column blocks
+// [floor(p nb / P), floor((p+1) nb / P)) and splits at block floor((2p+1) nb / 2P), its
+// middle, so every level fills ~nm / 2^(k-1) cells for any m (nb a power of two: the
+// reference construct's next_pow_2 parts).  sb / mid / eb: logical split indices of the
+// part's start, split and end; lw / hw: the halves' widths (a one-block part has a zero
+// one and no split).
+struct AffPartGeo {
+    int32_t sb, mid, eb, hoj_l, hoj_r, lw, hw;
+};
+__host__ __device__ inline AffPartGeo aff_part_geo(int nb, int m, int P, int p) {
+    const int64_t b0 = (int64_t)p * nb / P, b1 = (int64_t)(p + 1) * nb / P, bm = (int64_t)(2 * p + 1) * nb / (2 * P);
+    AffPartGeo a;
+    a.sb = (int32_t)b0 - 1;
+    a.eb = (int32_t)b1 - 1;
+    a.mid = (int32_t)bm - 1;
+    a.hoj_l = (int32_t)(b0 * 128);
+    a.hoj_r = (int32_t)(bm * 128);
+    a.lw = a.hoj_r - a.hoj_l;
+    a.hw = (int32_t)(b1 * 128 < m ? b1 * 128 : m) - a.hoj_r;
+    return a;
+}
 
 // One final-level 128-column block (iteration_*:121-173).
 struct BlockInfo {

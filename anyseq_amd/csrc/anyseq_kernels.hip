@@ -2333,6 +2333,7 @@ __global__ __launch_bounds__(256) void aff_hb_join_kernel(const PartInfo* __rest
     __shared__ int sv[256], sk[256];
     const PartInfo pi = parts[blockIdx.x];
     const int off = pi.off, len = pi.len;
+    if (pi.flags & 8) return;   // a one-block part (aff_part_geo): nothing to split
     if (pi.flags & 4) {
         if (threadIdx.x == 0) {
             splits[pi.split_index + 1] = off;
@@ -2341,7 +2342,7 @@ __global__ __launch_bounds__(256) void aff_hb_join_kernel(const PartInfo* __rest
         return;
     }
     const bool sfree = pi.flags & 1, efree = pi.flags & 2;
-    const int bLH = aff_top_h(pi.smode, half - 1, go, ge), bLE = sfree ? kAffNeg : bLH;
+    const int bLH = aff_top_h(pi.smode, pi.lhw - 1, go, ge), bLE = sfree ? kAffNeg : bLH;
     const int bRH = aff_top_h(pi.emode, pi.rhw - 1, go, ge), bRE = efree ? kAffNeg : bRH;
     int best = -2147483647, key = 0x7fffffff;   // key: 0 BEFORE, 1 AFTER, 2 + 2 (i + 1) + type
     if (threadIdx.x == 0) {
@@ -2416,9 +2417,9 @@ __global__ __launch_bounds__(256) void aff_hb_join_slice_kernel(const PartInfo* 
     const PartInfo pi = parts[part];
     const int off = pi.off, len = pi.len;
     int best = -2147483647, key = 0x7fffffff;
-    if (!(pi.flags & 4)) {
+    if (!(pi.flags & 12)) {
         const bool sfree = pi.flags & 1, efree = pi.flags & 2;
-        const int bLH = aff_top_h(pi.smode, half - 1, go, ge), bLE = sfree ? kAffNeg : bLH;
+        const int bLH = aff_top_h(pi.smode, pi.lhw - 1, go, ge), bLE = sfree ? kAffNeg : bLH;
         const int bRH = aff_top_h(pi.emode, pi.rhw - 1, go, ge), bRE = efree ? kAffNeg : bRH;
         if (slice == 0 && threadIdx.x == 0) {
             if (efree && pbest[2 * part] > best) {
@@ -2468,6 +2469,7 @@ __global__ void aff_hb_join_final_kernel(const PartInfo* __restrict__ parts, int
     const int part = blockIdx.x * blockDim.x + threadIdx.x;
     if (part >= nparts) return;
     const PartInfo pi = parts[part];
+    if (pi.flags & 8) return;
     if (pi.flags & 4) {
         splits[pi.split_index + 1] = pi.off;
         types[pi.split_index + 1] = pi.empty_type;
@@ -2588,19 +2590,23 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
         int off = 0, len = 0, hoj_l = 0, hoj_r = 0, hw = 0;
         bool sfree = false, efree = false;
         if (p < a.parts) {
-            const int sb = p * a.bpp - 1, eb = min((p + 1) * a.bpp - 1, a.nb - 1);
+            const AffPartGeo pg = aff_part_geo(a.nb, a.m, a.parts, p);
+            const int sb = pg.sb, eb = pg.eb;
             const int ts = a.typ[sb + 1], te = a.typ[eb + 1];
-            pi.split_index = p * a.bpp + a.bpp / 2 - 1;
+            pi.split_index = pg.mid;
+            pi.lhw = pg.lw;
             off = a.spl[sb + 1];
-            if (stop || ts == T_BEFORE || te == T_AFTER) {   // empty part: so are both halves
+            if (pg.lw <= 0 || pg.hw <= 0) {   // a one-block part: no split, no halves
+                pi.flags = 8;
+            } else if (stop || ts == T_BEFORE || te == T_AFTER) {   // empty part: so are both halves
                 pi.flags = 4;
                 pi.empty_type = ts == T_BEFORE ? T_BEFORE : T_AFTER;
                 pi.off = off;
             } else {
                 len = a.spl[eb + 1] - off;
-                hoj_l = p * a.pw;
-                hoj_r = p * a.pw + a.half;
-                hw = min(a.half, a.m - hoj_r);
+                hoj_l = pg.hoj_l;
+                hoj_r = pg.hoj_r;
+                hw = pg.hw;
                 sfree = ts == T_AFTER;
                 efree = te == T_BEFORE;
                 pi.off = off;
@@ -2609,7 +2615,7 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
                 pi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : aff_free_bm(a.kind, hoj_l == 0);
                 pi.emode = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : aff_free_bm(a.kind, hoj_r + hw == a.m);
                 pi.flags = (sfree ? 1 : 0) | (efree ? 2 : 0);
-                gl = aff_half_geo(a, len, a.half);
+                gl = aff_half_geo(a, len, pg.lw);
                 gr = aff_half_geo(a, len, hw);
             }
             a.parts_out[p] = pi;
@@ -2715,7 +2721,7 @@ __global__ __launch_bounds__(1024) void aff_level_tail_kernel(const AffLevelTail
     const int part = b / max(t.nslices, 1), slice = b % max(t.nslices, 1);
     const PartInfo pi = b < nj ? t.parts[part] : PartInfo{};
     // slices past the part's candidates (the slice count covers the longest possible part)
-    const bool idle = b < nj && (pi.flags & 4 || (slice > 0 && slice * t.slice_len - 1 >= pi.len));
+    const bool idle = b < nj && (pi.flags & 12 || (slice > 0 && slice * t.slice_len - 1 >= pi.len));
     // partials: write-through (sc1) stores, drained before the counter, read back with sc1
     // loads -- no L2 write-back fence, which would also flush the sentinel rows
     int2* partial = reinterpret_cast<int2*>(t.partial);
@@ -2726,7 +2732,7 @@ __global__ __launch_bounds__(1024) void aff_level_tail_kernel(const AffLevelTail
         int best = -2147483647, key = 0x7fffffff;
         if (!(pi.flags & 4)) {
             const bool sfree = pi.flags & 1, efree = pi.flags & 2;
-            const int bLH = aff_top_h(pi.smode, t.half - 1, t.go, t.ge), bLE = sfree ? kAffNeg : bLH;
+            const int bLH = aff_top_h(pi.smode, pi.lhw - 1, t.go, t.ge), bLE = sfree ? kAffNeg : bLH;
             const int bRH = aff_top_h(pi.emode, pi.rhw - 1, t.go, t.ge), bRE = efree ? kAffNeg : bRH;
             const RowToCol JL = t.jobs[2 * part], JR = t.jobs[2 * part + 1];
             if (slice == 0 && threadIdx.x == 0) {
@@ -2814,6 +2820,7 @@ __global__ __launch_bounds__(1024) void aff_level_tail_kernel(const AffLevelTail
         const int part = p0 + (int)threadIdx.x;
         if ((int)threadIdx.x >= np) continue;
         const PartInfo pi = t.parts[part];
+        if (pi.flags & 8) continue;   // a one-block part: nothing to split
         if (pi.flags & 4) {
             t.splits[pi.split_index + 1] = pi.off;
             t.types[pi.split_index + 1] = pi.empty_type;

@@ -943,6 +943,24 @@ static void half_body(void* p, Index i) {
     aff_fill(t->q, t->h, t->s, t->w, c->sc, t->bm, t->colH, t->colE, &t->best_all, &t->best_last);
 }
 
+/* Part geometry of a Hirschberg level of the build-defined affine construct (round 4,
+ * DESIGN.md §3.4): level k has 2^(k-1) parts, part p the 128-column blocks
+ * [floor(p nb / P), floor((p+1) nb / P)) with P = 2^(k-1), split at block
+ * floor((2p+1) nb / 2P) -- every part at its middle block, so every level fills ~nm / 2^(k-1)
+ * cells whatever m is.  When nb is a power of two these are exactly the reference
+ * construct's parts (next_pow_2(m) wide, split at half width, align.impala:237-290),
+ * which the linear compat construct keeps.  The levels end once no part has 2 blocks. */
+typedef struct { Index sb, mid, eb, hoj_l, hoj_r, lw, hw; } AffPart;
+static AffPart aff_part(Index nb, Index m, Index P, Index p) {
+    AffPart a;
+    const Index b0 = p * nb / P, b1 = (p + 1) * nb / P, bm = (2 * p + 1) * nb / (2 * P);
+    a.sb = b0 - 1; a.eb = b1 - 1; a.mid = bm - 1;
+    a.hoj_l = b0 * MIN_PART_WIDTH_HB; a.hoj_r = bm * MIN_PART_WIDTH_HB;
+    a.lw = a.hoj_r - a.hoj_l;
+    a.hw = imin(b1 * MIN_PART_WIDTH_HB, m) - a.hoj_r;
+    return a;
+}
+
 /* Returns the level-1 join value (the optimal score; semiglobal: with the empty
  * alignment's 0) or INT64_MIN when m <= 128 (no level); writes the alignment
  * unless a local / semiglobal level-1 value is <= 0 (the empty alignment). */
@@ -957,41 +975,40 @@ static int64_t aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8
     IV(spl, -1) = 0;
     IV(spl, nb - 1) = n;
     if (kind != SCHEME_GLOBAL) { IV(typ, -1) = T_AFTER; IV(typ, nb - 1) = T_BEFORE; }
-    Index pw = next_pow_2(m);
-    Index bpp = pw / MIN_PART_WIDTH_HB;
     Score *LH = (Score*)malloc(sizeof(Score) * (size_t)(n + 1)), *LE = (Score*)malloc(sizeof(Score) * (size_t)(n + 1));
     Score *RH = (Score*)malloc(sizeof(Score) * (size_t)(n + 1)), *RE = (Score*)malloc(sizeof(Score) * (size_t)(n + 1));
     HalfTask* tasks = (HalfTask*)malloc(sizeof(HalfTask) * (size_t)(2 * nb + 2));
     Index* tpart = (Index*)malloc(sizeof(Index) * (size_t)(nb + 1));   /* part -> its first task, -1: none */
     int64_t score = INT64_MIN;
     int level1 = 1;
-    while (pw > MIN_PART_WIDTH_HB) {
-        const Index half = pw / 2;
-        const Index parts = (m + half - 1) / pw;
+    for (Index P = 1; P < nb; P *= 2) {   /* level k: P = 2^(k-1) parts (nb > 1) */
+        const Index parts = P;
         Index nt = 0;
         for (Index p = 0; p < parts; ++p) {   /* this level's half fills */
-            const Index sb = p * bpp - 1, eb = imin((p + 1) * bpp - 1, nb - 1);
-            const int ts = IV(typ, sb), te = IV(typ, eb);
+            const AffPart a = aff_part(nb, m, P, p);
+            const int ts = IV(typ, a.sb), te = IV(typ, a.eb);
             tpart[p] = -1;
+            if (a.lw <= 0 || a.hw <= 0) continue;   /* a one-block part: no split */
             if (ts == T_BEFORE || te == T_AFTER) continue;
-            if (IV(spl, sb) == SPLIT_UNSET || IV(spl, eb) == SPLIT_UNSET) { g_error = 1; continue; }
-            const Index off = IV(spl, sb), len = IV(spl, eb) - off;
+            if (IV(spl, a.sb) == SPLIT_UNSET || IV(spl, a.eb) == SPLIT_UNSET) { g_error = 1; continue; }
+            const Index off = IV(spl, a.sb), len = IV(spl, a.eb) - off;
             if (len <= 0) continue;
-            const Index hoj_l = p * pw, hoj_r = p * pw + half, hw = imin(half, m - hoj_r);
             tpart[p] = nt;
             HalfTask* L = &tasks[nt++];
-            L->q = (Acc){Q, off, 1}; L->s = (Acc){S, hoj_l, 1}; L->h = len; L->w = half;
-            L->bm = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, hoj_l == 0);
+            L->q = (Acc){Q, off, 1}; L->s = (Acc){S, a.hoj_l, 1}; L->h = len; L->w = a.lw;
+            L->bm = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, a.hoj_l == 0);
             L->colH = LH + off; L->colE = LE + off;
             HalfTask* R = &tasks[nt++];
-            R->q = (Acc){Q, off + len - 1, -1}; R->s = (Acc){S, hoj_r + hw - 1, -1}; R->h = len; R->w = hw;
-            R->bm = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : free_bm(kind, hoj_r + hw == m);
+            R->q = (Acc){Q, off + len - 1, -1}; R->s = (Acc){S, a.hoj_r + a.hw - 1, -1}; R->h = len; R->w = a.hw;
+            R->bm = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : free_bm(kind, a.hoj_r + a.hw == m);
             R->colH = RH + off; R->colE = RE + off;
         }
         HalfCtx hc = {tasks, sc};
         parallel_for(0, nt, half_body, &hc);
         for (Index p = 0; p < parts; ++p) {   /* joins */
-            const Index sb = p * bpp - 1, eb = imin((p + 1) * bpp - 1, nb - 1), mid = p * bpp + bpp / 2 - 1;
+            const AffPart a = aff_part(nb, m, P, p);
+            if (a.lw <= 0 || a.hw <= 0) continue;
+            const Index sb = a.sb, eb = a.eb, mid = a.mid;
             const int ts = IV(typ, sb), te = IV(typ, eb);
             if (ts == T_BEFORE || te == T_AFTER) {   /* empty part: so are both halves */
                 IV(typ, mid) = ts == T_BEFORE ? T_BEFORE : T_AFTER;
@@ -1000,8 +1017,7 @@ static int64_t aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8
             }
             if (IV(spl, sb) == SPLIT_UNSET || IV(spl, eb) == SPLIT_UNSET) { g_error = 1; continue; }
             const Index off = IV(spl, sb), len = IV(spl, eb) - off;
-            const Index hoj_l = p * pw, hoj_r = p * pw + half;
-            const Index hw = imin(half, m - hoj_r);
+            const Index hoj_l = a.hoj_l, hoj_r = a.hoj_r, hw = a.hw;
             const int lbm = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, hoj_l == 0);
             const int rbm = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : free_bm(kind, hoj_r + hw == m);
             const int sfree = ts == T_AFTER, efree = te == T_BEFORE;
@@ -1013,7 +1029,7 @@ static int64_t aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8
                 if (sfree) bestR = kind == SCHEME_LOCAL ? R->best_all : R->best_last;
             }
             /* index -1: the halves' top borders at the midline (a FREE top border is no gap) */
-            const Score bLH = bm_top(lbm, sc, half - 1), bLE = sfree ? ANEG : bLH;
+            const Score bLH = bm_top(lbm, sc, a.lw - 1), bLE = sfree ? ANEG : bLH;
             const Score bRH = bm_top(rbm, sc, hw - 1), bRE = efree ? ANEG : bRH;
             Score best = SCORE_MIN_VALUE; Index idx = -1; int type = T_H;
             if (efree && bestL > best) { best = bestL; type = T_BEFORE; }
@@ -1033,8 +1049,6 @@ static int64_t aff_construct_hb(int kind, const uint8_t* Q, Index n, const uint8
         }
         if (level1 && kind != SCHEME_GLOBAL && score <= 0) goto done;   /* the empty alignment */
         level1 = 0;
-        pw /= 2;
-        bpp /= 2;
     }
     for (Index b = 0; b < nb; ++b) {
         const int ts = IV(typ, b - 1), te = IV(typ, b);

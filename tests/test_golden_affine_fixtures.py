@@ -63,3 +63,14 @@ def test_config3_fixture(anyseq, oracle):
     q, s = genome.synthetic_related_pair(4_641_652, 0.9)
     # the 262144^2 optimum takes ~2 min single-threaded: the rescoring alone here
     check(oracle, g, q[:g["lq"]], s[:g["ls"]], full_optimum=False)
+
+
+@pytest.mark.parametrize("name", ["config2_nonpow2", "config3_nonpow2"])
+def test_nonpow2_fixtures(anyseq, oracle, name):
+    g = json.load(open(os.path.join(GOLD, name + ".json")))
+    if name.startswith("config2"):
+        q, s = anyseq.main_random_pair(65536, 65536)
+    else:
+        from anyseq_amd import genome
+        q, s = genome.synthetic_related_pair(4_641_652, 0.9)
+    check(oracle, g, q[:g["lq"]], s[:g["ls"]], full_optimum=name.startswith("config2"))

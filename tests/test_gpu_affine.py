@@ -93,8 +93,10 @@ def test_affine_bytes_and_similar(anyseq, oracle, kind):
     assert gpu(anyseq, kind, base, s2, sc) == ora(oracle, kind, base, s2, sc)
 
 
-@pytest.mark.parametrize("nw", [3, 4])
+@pytest.mark.parametrize("nw", [3, 4, 7])
 def test_affine_waves_per_group(anyseq, oracle, nw):
+    """Forced compute waves per workgroup (7: two per SIMD beside the I/O wave) give the
+    same scores and constructs; 0 (the default) chooses per launch."""
     rng = random.Random(27)
     anyseq.set_option("affine_waves_per_group", nw)
     try:
@@ -102,8 +104,9 @@ def test_affine_waves_per_group(anyseq, oracle, nw):
             q, s = rnd(rng, 2600), rnd(rng, 1900)
             sc = (2, -1, -3, -1)
             assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, nw)
+            assert anyseq.construct(kind, q, s, *sc) == oracle.affine_construct(kind, q, s, *sc), (kind, nw)
     finally:
-        anyseq.set_option("affine_waves_per_group", 4)
+        anyseq.set_option("affine_waves_per_group", 0)
 
 
 def test_affine_rejects_bad_scoring(anyseq):

@@ -42,6 +42,19 @@ def test_config3_semiglobal_affine_prefix(anyseq):
     check(anyseq, g, q[:g["lq"]], s[:g["ls"]])
 
 
+@pytest.mark.parametrize("name", ["config2_nonpow2", "config3_nonpow2"])
+def test_nonpow2_fixtures(anyseq, name):
+    """Subject lengths whose 128-column block count is not a power of two: every level's
+    parts split at their middle block (aff_part_geo, round 4), the oracle's rule."""
+    g = json.load(open(os.path.join(GOLD, name + ".json")))
+    if name.startswith("config2"):
+        q, s = anyseq.main_random_pair(65536, 65536)
+    else:
+        from anyseq_amd import genome
+        q, s = genome.synthetic_related_pair(4_641_652, 0.9)
+    check(anyseq, g, q[:g["lq"]], s[:g["ls"]])
+
+
 def test_config3_genome_length_construct(anyseq):
     """configs[3] and configs[4] at full genome length (4.64 Mbp x 4.64 Mbp, synthetic related
     pair; the oracle cannot reach this size, so parity is by properties): the construct's

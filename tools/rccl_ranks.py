@@ -32,20 +32,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCORE_CASES = [("global", 0), ("semiglobal", 0), ("local", 0), ("global", -2), ("semiglobal", -2), ("local", -2)]
 # (kind, n, m, level 1 column-blocked?)  The column-blocked level 1 needs the halves
 # transposed and the query longer than the level's split row (anyseq_engine.cpp).
-CONSTRUCT_CASES = [("semiglobal", 8192, 16384, False), ("local", 8192, 16384, False),
+CONSTRUCT_CASES = [("semiglobal", 8000, 16384, False), ("local", 8000, 16500, False),
                    ("local", 16384, 16384, True), ("semiglobal", 16384, 16384, True),
                    ("global", 12000, 9000, True)]
 
 
 def level1_expected(n: int, m: int, world: int) -> bool:
     """Whether the engine column-blocks level 1 of an n x m construct over `world` ranks
-    (the same test as anyseq_engine.cpp: one part, transposed halves, len > half)."""
-    if world < 2 or n < world:
+    (the same test as anyseq_engine.cpp: one part, transposed halves, len > the left
+    half's width; level 1 splits at the middle 128-column block, aff_part_geo)."""
+    if world < 2 or n < world or m <= 128:
         return False
-    half = 1
-    while half < m:
-        half *= 2
-    half //= 2
+    nb = (m + 127) // 128
+    half = 128 * (nb // 2)
     return n > half
 
 
