@@ -140,14 +140,20 @@ int anyseq_shard_finalize(void);
 /* The same sharded fill with `nshards` shards inside this process on the current
  * device (device copies instead of RCCL between them). */
 /* Sharded affine construct (align.impala:237-311 distributed by level):
- * every rank calls it with the whole pair after anyseq_shard_init; the half fills of
- * each Hirschberg level and the final 128-column blocks are dealt round-robin to the
- * ranks, the level's boundary columns are all-reduced over RCCL, and every rank returns
- * the same score and strings (sparse i+j+1 layout, lenq+lens bytes each). */
+ * every rank calls it with the whole pair after anyseq_shard_init.  Level 1's two
+ * halves are column-blocked over ALL ranks (rank g fills query columns
+ * [g*lenq/N, (g+1)*lenq/N) of both, boundary columns over RCCL send/recv); the half
+ * fills of the later levels and the final 128-column blocks are dealt round-robin; the
+ * level columns are all-reduced over RCCL, and every rank returns the same score and
+ * strings (sparse i+j+1 layout, lenq+lens bytes each).  When GPU_MAX_HW_QUEUES leaves
+ * too few hardware queues for level 1's concurrent transport streams, level 1 is dealt
+ * round-robin too (same result; anyseq_last_shard_plan reports which plan ran). */
 int anyseq_shard_construct(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
                            int lens, char* alQuery, char* alSubject, int64_t* score);
 /* The same plan with `nshards` virtual ranks in this process on one device (one fill
- * launch per rank per level): the 1-GPU parity check of the sharded construct. */
+ * launch per rank per level): the 1-GPU parity check of the sharded construct.  Its
+ * column-blocked level 1 needs 3*nshards-2 streams and nshards co-resident grids
+ * (nshards <= CUs/8 - 8); otherwise level 1 is dealt round-robin. */
 int anyseq_construct_local_sharded(int kind, const anyseq_scoring* sc, const char* query, int lenq,
                                    const char* subject, int lens, int nshards, char* alQuery, char* alSubject,
                                    int64_t* score);

@@ -91,6 +91,31 @@ def step_x(e, u, L, lut, pub="shift"):
         e(f"ds_write_b128 %[pa], v[{AO0 + 2 * (u - 1)}:{AO0 + 2 * u + 1}] offset:{16 * (u // 2)}")
 
 
+def step_es(e, u, pub="none"):
+    """X-space local step with the E update split (round 4 experiment): E + ge from the
+    previous E alone, hge = X + go + ge beside hg = X + go, E' = max3(E + ge, hge, zl + ge):
+    one more instruction, but the E recurrence is X -> hge -> E -> X (3 links, was 4)."""
+    tg = "%[tfg]" if u == 0 else TG(u - 1)
+    tf = "%[tff]" if u == 0 else TF(u - 1)
+    g = "%[cur]" if u == 0 else OG(u - 1)
+    f = "%[fd]" if u == 0 else OF(u - 1)
+    dg = "%[dg]" if u == 0 else ("%[tfg]" if u == 1 else TG(u - 2))
+    if u % 4 == 0:
+        e(f"v_perm_b32 v{WB}, %[lh], %[ll], {v(SW + u // 4)}")
+    e(f"v_add_u32_e32 %[e], %[ge], %[e]")
+    e(f"v_add_u32_sdwa v{AA}, {dg}, sext(v{WB}) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "
+      f"src1_sel:BYTE_{u % 4}")
+    e("v_max3_i32 %[e], %[e], %[hg], %[zl]")       # hg holds X + go + ge here
+    e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
+    e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
+    e(f"v_max3_i32 {OG(u)}, v{AA}, %[e], {tf}")
+    e(f"v_add_u32_e32 %[hg], %[go], {OG(u)}")
+    e(f"v_max_i32_e32 {OF(u)}, {tf}, %[hg]")
+    e(f"v_add_u32_e32 %[hg], %[ge], %[hg]")       # + ge for the next E
+    if u % 2 == 1:
+        e(f"v_max3_i32 %[best], %[best], {OG(u - 1)}, {OG(u)}")
+
+
 def block(variant):
     out = []
     e = out.append
@@ -112,6 +137,8 @@ def block(variant):
             step_x(e, u, True, True, pub="ds")
         elif variant == "G_l":
             step_x(e, u, False, True)
+        elif variant == "L_es_np":
+            step_es(e, u)
         else:
             raise ValueError(variant)
     e(f"v_mov_b32_e32 %[cur], {OG(31)}")
@@ -124,7 +151,7 @@ def block(variant):
     return out
 
 
-VARIANTS = ["L_cur", "L_x", "L_xl", "L_xl_np", "L_xl_ds", "G_cur", "G_l"]
+VARIANTS = ["L_cur", "L_x", "L_xl", "L_xl_np", "L_xl_ds", "G_cur", "G_l", "L_es_np"]
 
 
 def main():

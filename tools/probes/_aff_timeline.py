@@ -58,7 +58,9 @@ for front, sel in (("fwd", a[:, 0] < 2048), ("rev", a[:, 0] >= 2048)):
     print(f"  end lag:   LDS hop median {np.median(de[~glob]):.3f} us, HBM hop median {np.median(de[glob]):.3f} us")
     for k in range(NW):
         m = band[1:] % NW == k
-        print(f"   into slot {k}: start lag {np.median(d[m]):.3f}, end lag {np.median(de[m]):.3f}")
+        mk = band % NW == k
+        print(f"   into slot {k}: start lag {np.median(d[m]):.3f}, end lag {np.median(de[m]):.3f}; "
+              f"slot-{k} steady duration median {np.median(dur[mk]):.2f} us")
     q4 = len(d) // 4
     print("  start lag by chain quarter:", " ".join(f"{np.mean(d[i*q4:(i+1)*q4]):.3f}" for i in range(4)))
 
