@@ -1458,16 +1458,17 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         pinfo.assign((size_t)parts, PartInfo{});
         std::vector<RowToColJob> jobs;
         int half_index = 0;   // the level's half fills in part order: left 2k, right 2k+1
-        ShardLevel1 l1;
-        bool l1_blocked = false;
+        ShardLevel lvl;
+        bool blocked = false;
         if (sharded) {   // rows a rank does not fill are zero in the SUM reduction
             for (int32_t* b : {LH0, LE0, RH0, RE0}) HIPCHECK(hipMemsetAsync(b, 0, nviews * nn * 4, st));
         }
         // transposed halves' bottom rows: sum of part heights <= n (parts' rows are disjoint)
         int32_t* rowpool = (int32_t*)E.outrow.get((size_t)2 * ((size_t)n + 64 * (size_t)parts) * 2 * 4);
+        const int best_bits = local ? AM_BEST_ALL : AM_BEST_LAST;
         for (int p = 0; p < parts; ++p) {
             const AffPartGeo pg = aff_part_geo(sp.nb, m, parts, p);
-            const int sb = pg.sb, eb = pg.eb, half = pg.lw;
+            const int sb = pg.sb, eb = pg.eb;
             PartInfo& pi = pinfo[p];
             pi.split_index = pg.mid;
             pi.lhw = pg.lw;
@@ -1491,43 +1492,66 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             pi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : free_bm(kind, hoj_l == 0);
             pi.emode = te == T_H ? BM_NORMAL : te == T_E ? BM_EPAID : free_bm(kind, hoj_r + hw == m);
             pi.flags = (sfree ? 1 : 0) | (efree ? 2 : 0);
-            if (len <= 0) continue;
-            const int best_bits = local ? AM_BEST_ALL : AM_BEST_LAST;
+        }
+        // Column-blocked level: with world >= 2 * parts every part runs
+        // over its own subgroup of ranks (both halves transposed, each rank a block of
+        // the part's query rows); else the halves are dealt round-robin.
+        if (sharded && shards->blocked && world >= 2 * parts && g_tuning.afft && env_int("ANYSEQ_SHARD_L1", 1) != 0) {
+            blocked = true;
+            for (int p = 0; p < parts; ++p) {
+                const PartInfo& pi = pinfo[p];
+                const int r0 = (int)((int64_t)p * world / parts), G = (int)((int64_t)(p + 1) * world / parts) - r0;
+                if ((pi.flags & 12) == 0 && pi.len > 0 && pi.len < G) blocked = false;
+            }
+        }
+        if (blocked) {
+            auto tam = [](int am) {
+                return (am & AM_CLAMP) |
+                       ((am & AM_BEST_LASTCOL) == AM_BEST_LAST ? AM_BEST_LASTCOL : (am & AM_BEST_LASTCOL));
+            };
+            lvl.kind = kind;
+            lvl.sc = sc;
+            lvl.fp = fp;
+            lvl.LH = LH0;
+            lvl.LE = LE0;
+            lvl.RH = RH0;
+            lvl.RE = RE0;
+            lvl.nn = nn;
+            lvl.pstride = (size_t)2 * parts;
+            lvl.st = st;
+            lvl.E = &E;
+            for (int p = 0; p < parts; ++p) {
+                const PartInfo& pi = pinfo[p];
+                if ((pi.flags & 12) || pi.len <= 0) continue;   // no halves: the part's ranks idle
+                const AffPartGeo pg = aff_part_geo(sp.nb, m, parts, p);
+                const bool sfree = pi.flags & 1, efree = pi.flags & 2;
+                ShardPart T;
+                T.cq = cq;
+                T.cs = cs;
+                T.off = pi.off;
+                T.len = pi.len;
+                T.soff = pg.hoj_l;
+                T.mw = pg.lw + pg.hw;
+                T.half = pg.lw;
+                T.bm_l = transposed_bm(pi.smode);
+                T.am_l = tam((pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0));
+                T.bm_r = transposed_bm(pi.emode);
+                T.am_r = tam((pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0));
+                T.pbest = pbest0 + 2 * p;
+                T.r0 = (int)((int64_t)p * world / parts);
+                T.G = (int)((int64_t)(p + 1) * world / parts) - T.r0;
+                lvl.parts.push_back(T);
+            }
+            if (g_shard_blocked_levels == g_stage_level - 1) g_shard_blocked_levels = g_stage_level;
+        }
+        for (int p = 0; p < parts && !blocked; ++p) {
+            const PartInfo& pi = pinfo[p];
+            if ((pi.flags & 12) || pi.len <= 0) continue;
+            const AffPartGeo pg = aff_part_geo(sp.nb, m, parts, p);
+            const int off = pi.off, len = pi.len, half = pg.lw, hoj_l = pg.hoj_l, hoj_r = pg.hoj_r, hw = pg.hw;
+            const bool sfree = pi.flags & 1, efree = pi.flags & 2;
             // (half_index advances on every rank, so all ranks agree on the owners)
             const int ol = owner(half_index++), orr = owner(half_index++);
-            if (level1 && sharded && shards->level1 && parts == 1 && g_tuning.afft && len > half && len >= world &&
-                env_int("ANYSEQ_SHARD_L1", 1) != 0) {
-                // column-blocked level 1: both halves transposed, every
-                // rank fills a block of query columns of both
-                auto tam = [](int am) {
-                    return (am & AM_CLAMP) |
-                           ((am & AM_BEST_LASTCOL) == AM_BEST_LAST ? AM_BEST_LASTCOL : (am & AM_BEST_LASTCOL));
-                };
-                l1.kind = kind;
-                l1.sc = sc;
-                l1.fp = fp;
-                l1.cq = cq;
-                l1.cs = cs;
-                l1.n = n;
-                l1.m = m;
-                l1.half = half;
-                l1.bm_l = transposed_bm(pi.smode);
-                l1.am_l = tam((pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0));
-                l1.bm_r = transposed_bm(pi.emode);
-                l1.am_r = tam((pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0));
-                l1.LH = LH0;
-                l1.LE = LE0;
-                l1.RH = RH0;
-                l1.RE = RE0;
-                l1.nn = nn;
-                l1.pbest = pbest0;
-                l1.pstride = (size_t)2 * parts;
-                l1.st = st;
-                l1.E = &E;
-                l1_blocked = true;
-                g_shard_blocked_levels = 1;
-                continue;
-            }
             for (int v = 0; v < nviews; ++v) {
                 const size_t vo = (size_t)v * nn;
                 int32_t* pb = pbest0 + (size_t)v * 2 * parts;
@@ -1571,9 +1595,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             }
             pending_fill = true;
         }
-        if (l1_blocked) {   // (every view's best cells were reset above: no view has probs)
-            shards->level1(l1);
-            stage_check(st, "sharded level 1");
+        if (blocked) {   // (every view's best cells were reset above: no view has probs)
+            shards->blocked(lvl);
+            stage_check(st, "sharded column-blocked level");
         }
         if (!d_up) {
             char* d = (char*)E.parts.get(pb + jb + 16);

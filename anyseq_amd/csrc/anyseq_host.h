@@ -202,25 +202,34 @@ void set_last_error(const std::string& m);
 // the ranks' output strings merge by a byte-wise max.  local: `world` virtual ranks in
 // this process, one fill launch each, sharing the buffers (no reduction needed).
 //
-// Level 1 is column-blocked instead (ShardLevel1, when its halves run transposed):
-// the two halves are the two fronts of one transposed problem (subject rows, query
-// columns) split at row `half`, so rank g fills query columns [g*n/N, (g+1)*n/N) of
-// BOTH halves with the score sharding's boundary-column transport (anyseq_shard.cpp),
-// and writes its segment of the level's columns (the halves' bottom rows).
-struct ShardLevel1 {
+// Column-blocked levels: a part's two halves, both transposed
+// (subject columns as rows, query rows as columns), are the two fronts of ONE problem
+// split at row `half` (the left half's width) -- so a part runs on a subgroup of ranks
+// with the score sharding's boundary-column transport (anyseq_shard.cpp): rank g of
+// the subgroup fills the part's query rows [off + g*len/G, off + (g+1)*len/G) of both
+// halves and writes its segment of the level's columns (the halves' bottom rows).
+// Level k with P parts is column-blocked when world >= 2P (P = 1: level 1 over all
+// ranks; P = 2: each part over half of them; ...); part p takes ranks
+// [p*world/P, (p+1)*world/P).
+struct ShardPart {
+    const uint8_t* cq = nullptr;   // query codes: the transposed halves' columns start at cq + off
+    const uint8_t* cs = nullptr;   // subject codes: their rows start at cs + soff
+    int off = 0, len = 0;          // the part's query rows
+    int soff = 0, mw = 0, half = 0;   // its subject columns; forward half rows [0, half), reversed [half, mw)
+    int bm_l = 0, am_l = 0;        // border mode / kind bits of the transposed forward half
+    int bm_r = 0, am_r = 0;        // ... of the transposed reversed half
+    int32_t* pbest = nullptr;      // view 0's two best cells of the part; view v at + v * pstride
+    int r0 = 0, G = 1;             // its rank subgroup
+};
+struct ShardLevel {
     int kind = 0;
     anyseq_scoring sc{};
     FillParams fp{};
-    const uint8_t* cq = nullptr;   // query codes: the transposed halves' columns
-    const uint8_t* cs = nullptr;   // subject codes: their rows
-    int n = 0, m = 0, half = 0;    // forward half: subject rows [0, half); reversed: [half, m)
-    int bm_l = 0, am_l = 0;        // border mode / kind bits of the transposed forward half
-    int bm_r = 0, am_r = 0;        // ... of the transposed reversed half
+    std::vector<ShardPart> parts;
     int32_t *LH = nullptr, *LE = nullptr, *RH = nullptr, *RE = nullptr;   // view 0; view v at + v * nn
     size_t nn = 0;
-    int32_t* pbest = nullptr;      // view 0's two best cells; view v at + v * pstride
     size_t pstride = 0;
-    hipStream_t st = nullptr;      // the construct's stream (level 1 is ordered on it)
+    hipStream_t st = nullptr;      // the construct's stream (the level is ordered on it)
     Engine* E = nullptr;           // the construct's engine (held under E->mu by the caller)
 };
 
@@ -229,7 +238,7 @@ struct ConstructShards {
     bool local = false;
     std::function<void(int32_t*, size_t, hipStream_t)> sum_i32, max_i32;
     std::function<void(uint8_t*, size_t, hipStream_t)> max_u8;
-    std::function<void(const ShardLevel1&)> level1;   // column-blocked level 1 (null: round-robin)
+    std::function<void(const ShardLevel&)> blocked;   // column-blocked levels (null: round-robin)
 };
 int64_t construct_affine_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n,
                              const uint8_t* ds, int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st,

@@ -754,22 +754,23 @@ int64_t shard_score_rccl(int kind, const anyseq_scoring& sc) {
 
 
 // ---------------------------------------------------------------------------
-// Column-blocked level 1 of the sharded affine construct (DESIGN.md §6.2,
-// align.impala:254-259).  Level 1's halves, both transposed (subject codes as rows),
+// Column-blocked levels of the sharded affine construct (DESIGN.md §6.2,
+// align.impala:254-259).  A part's halves, both transposed (subject codes as rows),
 // are the two fronts of ONE problem split at row `half`: the forward half is the top
-// front, the reversed one the bottom front.  Shard g fills query columns
-// [c0, c0 + w) of both with the score sharding's boundary-column transport, and its
-// two bottom rows become its segment of the level's columns (zero elsewhere, so the
-// construct's SUM reduction assembles them).  The halves' border modes and kind bits
-// replace the score's; a last-column best cell belongs to the shard that holds the
-// half's last column (the reversed half's: the first).
-void level1_setup(Shard& S, int N, const ShardLevel1& J, int view, std::vector<DPProblem>& probs) {
+// front, the reversed one the bottom front.  Shard g of the part's rank subgroup fills
+// query columns [c0, c0 + w) of both with the score sharding's boundary-column
+// transport, and its two bottom rows become its segment of the level's columns (zero
+// elsewhere, so the construct's SUM reduction assembles them).  The halves' border
+// modes and kind bits replace the score's; a last-column best cell belongs to the
+// shard that holds the half's last column (the reversed half's: the first).
+void part_setup(Shard& S, const ShardLevel& J, const ShardPart& T, int view, std::vector<DPProblem>& probs) {
+    const int N = T.G;
     int h1 = 0, h2 = 0;
     probs.clear();
-    setup_shard(S, N, J.kind, J.sc, J.cs, J.m, J.cq + S.c0, J.n, probs, h1, h2, false, J.half);
+    setup_shard(S, N, J.kind, J.sc, T.cs + T.soff, T.mw, T.cq + T.off + S.c0, T.len, probs, h1, h2, false, T.half);
     const bool holds_last[2] = {S.g == N - 1, S.g == 0};
-    const int bm[2] = {J.bm_l, J.bm_r}, am[2] = {J.am_l, J.am_r};
-    int32_t* pb = J.pbest + (size_t)view * J.pstride;
+    const int bm[2] = {T.bm_l, T.bm_r}, am[2] = {T.am_l, T.am_r};
+    int32_t* pb = T.pbest + (size_t)view * J.pstride;
     for (int f = 0; f < 2; ++f) {
         DPProblem& P = probs[f];
         int a = am[f];
@@ -781,8 +782,8 @@ void level1_setup(Shard& S, int N, const ShardLevel1& J, int view, std::vector<D
     // bottom row (kernel value space, G or X) -> H / E of the level's columns; a global
     // (G space) block's frame is shifted by its first column in the half (as the score
     // combine's), which the job's column offset takes out
-    const size_t vo = (size_t)view * J.nn;
-    const int cr = J.n - S.c0 - S.w;   // the block's first column in the reversed half
+    const size_t vo = (size_t)view * J.nn + (size_t)T.off;
+    const int cr = T.len - S.c0 - S.w;   // the block's first column in the reversed half
     const bool glob = J.kind == KIND_GLOBAL;
     S.h_jobs[0] = RowToCol{S.top.out_row.p, J.LH + vo + S.c0, J.LE + vo + S.c0, S.w, h1 - 1,
                            probs[0].amode != 0 ? 1 : 0, glob ? S.c0 : 0};
@@ -793,30 +794,36 @@ void level1_setup(Shard& S, int N, const ShardLevel1& J, int view, std::vector<D
 }
 
 // After a shard's fill: its column segments, then the construct's stream waits for it.
-void level1_finish(Shard& S, const ShardLevel1& J) {
+void part_finish(Shard& S, const ShardLevel& J) {
     HIPCHECK(anyseq_launch_aff_row_to_col(S.jobs.p, 2, S.w, -J.sc.gap_extend, S.st));
     HIPCHECK(hipEventRecord(S.ready, S.st));
     HIPCHECK(hipStreamWaitEvent(J.st, S.ready, 0));
 }
 
-hipEvent_t level1_event() {
+hipEvent_t level_event() {
     static hipEvent_t ev = nullptr;
     if (!ev) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     return ev;
 }
 
-void check_level1(const ShardLevel1& J, int N) {
-    if (J.n < N) fail("sharded construct level 1: %d query columns cannot be split over %d ranks", J.n, N);
-    if (J.half < 1 || J.half >= J.m) fail("internal: sharded level 1 split %d of %d rows", J.half, J.m);
+void check_part(const ShardPart& T) {
+    if (T.len < T.G) fail("sharded construct: %d query rows cannot be split over %d ranks", T.len, T.G);
+    if (T.half < 1 || T.half >= T.mw) fail("internal: sharded part split %d of %d columns", T.half, T.mw);
     if (g_tuning.R != 1) fail("sharded construct: rows_per_lane must be 1");
 }
 
-// Emulated ranks (anyseq_construct_local_sharded): N in-process shards, view g = rank g.
-// The column-blocked level 1 runs its shards' fills concurrently: emulated ranks need
-// 3N-2 streams (fill + transport) and N co-resident grids of >= 8 workgroups (one per
-// XCD); one rank per GPU needs its fill and up to 4 transport streams.  When the
-// process cannot give it that, the construct deals level 1 round-robin like the later
-// levels instead of failing (same result, bit for bit).
+// A shard's place: its part's subgroup, its column block of the part's query rows.
+void place_shard(Shard& S, const ShardPart& T, int rank) {
+    S.g = rank - T.r0;
+    S.c0 = block_c0(S.g, T.G, T.len);
+    S.w = block_c0(S.g + 1, T.G, T.len) - S.c0;
+}
+
+// The blocked levels run their shards' fills concurrently: emulated ranks need 3N-2
+// streams (fill + transport) and N co-resident grids of >= 8 workgroups (one per XCD);
+// one rank per GPU needs its fill and up to 4 transport streams.  When the process
+// cannot give it that, the construct deals every level round-robin instead of failing
+// (same result, bit for bit).
 int hw_queues_available() { return env_int("GPU_MAX_HW_QUEUES", 4) - 2; }   // less the engine's and torch's
 int max_local_level1(int num_cus) { return std::max(1, num_cus / 8 - 8); }
 bool level1_local_possible(int N, int num_cus) {
@@ -826,48 +833,75 @@ bool level1_rccl_possible(int rank, int world) {
     return world >= 2 && 1 + 2 * ((rank > 0) + (rank < world - 1)) <= hw_queues_available();
 }
 
-void level1_local(const ShardLevel1& J, int N) {
-    check_level1(J, N);
+// Emulated ranks (anyseq_construct_local_sharded): N in-process shards, view g = rank g;
+// every part's subgroup at once, transport links inside each subgroup only.
+void blocked_local(const ShardLevel& J, int N) {
+    for (const ShardPart& T : J.parts) check_part(T);
     Engine& E = *J.E;   // (the construct holds E.mu; no engine() here: it would release retired blocks mid-call)
     std::vector<Shard>& shards = local_shards();
     const int max_local = max_local_level1(E.num_cus);
     if (N > max_local) fail("sharded construct: at most %d emulated ranks on this device (got %d)", max_local, N);
     if ((int)shards.size() < N) shards.resize(N);
     check_hw_queues(3 * N - 2);
-    for (int g = 0; g < N; ++g) {
+    std::vector<int> part_of(N, -1);
+    for (size_t p = 0; p < J.parts.size(); ++p)
+        for (int r = J.parts[p].r0; r < J.parts[p].r0 + J.parts[p].G; ++r) part_of[r] = (int)p;
+    std::vector<int> act;   // the ranks with a part at this level
+    for (int g = 0; g < N; ++g)
+        if (part_of[g] >= 0) act.push_back(g);
+    for (int g : act) {
+        const ShardPart& T = J.parts[part_of[g]];
         shards[g].init();
-        if (g + 1 < N) lazy_stream(shards[g].top.s_send);
-        if (g > 0) lazy_stream(shards[g].bot.s_send);
+        place_shard(shards[g], T, g);
+        if (shards[g].g + 1 < T.G) lazy_stream(shards[g].top.s_send);
+        if (shards[g].g > 0) lazy_stream(shards[g].bot.s_send);
     }
     // behind the construct's stream: the level's zeroed columns and reset best cells
-    HIPCHECK(hipEventRecord(level1_event(), J.st));
+    HIPCHECK(hipEventRecord(level_event(), J.st));
     std::vector<std::vector<DPProblem>> probs(N);
-    for (int g = 0; g < N; ++g) {
-        Shard& S = shards[g];
-        HIPCHECK(hipStreamWaitEvent(S.st, level1_event(), 0));
-        S.g = g;
-        S.c0 = block_c0(g, N, J.n);
-        S.w = block_c0(g + 1, N, J.n) - S.c0;
-        level1_setup(S, N, J, g, probs[g]);
+    for (int g : act) {
+        HIPCHECK(hipStreamWaitEvent(shards[g].st, level_event(), 0));
+        part_setup(shards[g], J, J.parts[part_of[g]], g, probs[g]);
     }
-    for (int g = 0; g < N; ++g)   // a copy lands in a neighbour's left_in after its sentinel fill
-        for (int k = 0; k < N; ++k)
+    for (int g : act)   // a copy lands in a neighbour's left_in after its sentinel fill
+        for (int k : act)
             if (k != g) {
                 if (shards[g].top.s_send) HIPCHECK(hipStreamWaitEvent(shards[g].top.s_send, shards[k].ready, 0));
                 if (shards[g].bot.s_send) HIPCHECK(hipStreamWaitEvent(shards[g].bot.s_send, shards[k].ready, 0));
             }
-    const int grid = grid_per_shard(E, N);
-    for (int g = 0; g < N; ++g) fill_prepare(E, shards[g].fc, probs[g], J.fp, shards[g].st, grid);
-    for (int g = 0; g < N; ++g) fill_launch(shards[g].fc);
-    std::vector<Xfer> xs = local_xfers(shards, N, E.device);
+    const int grid = grid_per_shard(E, (int)act.size());
+    for (int g : act) fill_prepare(E, shards[g].fc, probs[g], J.fp, shards[g].st, grid);
+    for (int g : act) fill_launch(shards[g].fc);
+    std::vector<Xfer> xs;
+    for (const ShardPart& T : J.parts) {   // links inside the subgroup
+        for (int g = T.r0; g + 1 < T.r0 + T.G; ++g) {
+            Shard &A = shards[g], &B = shards[g + 1];
+            Xfer x;
+            x.device = E.device;
+            x.src = &A.top;   // top: g -> g+1
+            x.dst = (int32_t*)B.top.left_in.p;
+            x.dst_e = (int32_t*)B.top.left_in_e.p;
+            x.flag = (uint32_t*)B.top.left_flag.p;
+            x.h = A.top.h;
+            xs.push_back(x);
+            Xfer y;
+            y.device = E.device;
+            y.src = &B.bot;   // bottom: g+1 -> g
+            y.dst = (int32_t*)A.bot.left_in.p;
+            y.dst_e = (int32_t*)A.bot.left_in_e.p;
+            y.flag = (uint32_t*)A.bot.left_flag.p;
+            y.h = B.bot.h;
+            xs.push_back(y);
+        }
+    }
     std::vector<std::thread> th = start_xfers(xs);
     std::vector<Shard*> sp;
-    for (int g = 0; g < N; ++g) sp.push_back(&shards[g]);
+    for (int g : act) sp.push_back(&shards[g]);
     bool ok = true;
     std::string err;
-    for (int g = 0; g < N; ++g) {
+    for (int g : act) {
         try {
-            wait_stream(shards[g].st, 120.0, "sharded construct level 1");
+            wait_stream(shards[g].st, 120.0, "sharded construct level");
             fill_finish(shards[g].fc);
         } catch (const Failure& f) {
             ok = false;
@@ -875,44 +909,72 @@ void level1_local(const ShardLevel1& J, int N) {
         }
     }
     finish_xfers(th, xs, sp, ok);
-    for (int g = 0; g < N; ++g)
+    for (int g : act)
         for (Front* f : {&shards[g].top, &shards[g].bot})
             if (f->s_send) wait_stream(f->s_send, 30.0, "shard transport");
     if (!ok) fail("%s", err.c_str());
-    for (int g = 0; g < N; ++g) level1_finish(shards[g], J);
+    for (int g : act) part_finish(shards[g], J);
 }
 
-// One rank per GPU (anyseq_shard_construct): this rank's block over RCCL.
-void level1_rccl(const ShardLevel1& J) {
+// One rank per GPU (anyseq_shard_construct): this rank's block of its part over RCCL.
+void blocked_rccl(const ShardLevel& J) {
     if (!g_rccl || g_rccl->rank < 0) fail("anyseq_shard_init has not been called");
     RcclState& R = *g_rccl;
-    check_level1(J, R.world);
+    for (const ShardPart& T : J.parts) check_part(T);
+    const ShardPart* mine = nullptr;
+    for (const ShardPart& T : J.parts)
+        if (R.rank >= T.r0 && R.rank < T.r0 + T.G) mine = &T;
+    if (!mine) return;   // no part for this rank at this level (its columns stay zero)
+    const ShardPart& T = *mine;
     Engine& E = *J.E;   // (the construct holds E.mu)
     Shard& S = R.shard;
     S.init();
-    check_hw_queues(1 + 2 * ((R.rank > 0) + (R.rank < R.world - 1)));
-    if (R.rank > 0) {
+    place_shard(S, T, R.rank);
+    const bool has_left = S.g > 0, has_right = S.g + 1 < T.G;
+    check_hw_queues(1 + 2 * ((int)has_left + (int)has_right));
+    if (has_left) {
         lazy_stream(S.top.s_recv);
         lazy_stream(S.bot.s_send);
     }
-    if (R.rank < R.world - 1) {
+    if (has_right) {
         lazy_stream(S.top.s_send);
         lazy_stream(S.bot.s_recv);
     }
-    HIPCHECK(hipEventRecord(level1_event(), J.st));
-    HIPCHECK(hipStreamWaitEvent(S.st, level1_event(), 0));
-    S.g = R.rank;
-    S.c0 = block_c0(R.rank, R.world, J.n);
-    S.w = block_c0(R.rank + 1, R.world, J.n) - S.c0;
+    HIPCHECK(hipEventRecord(level_event(), J.st));
+    HIPCHECK(hipStreamWaitEvent(S.st, level_event(), 0));
     std::vector<DPProblem> probs;
-    level1_setup(S, R.world, J, 0, probs);
+    part_setup(S, J, T, 0, probs);
     fill_async(E, S.fc, probs, J.fp, S.st, grid_per_shard(E, 1));
-    std::vector<Xfer> xs = rccl_xfers(R, E.device);
+    // links inside the subgroup only: rank g's neighbours g-1 / g+1 (link a joins ranks a
+    // and a+1 on the communicators of rccl_xfers)
+    std::vector<Xfer> xs;
+    auto add = [&](Front* f, bool recv, int peer, ncclComm_t c) {
+        Xfer x;
+        x.device = E.device;
+        x.src = f;
+        x.recv = recv;
+        x.peer = peer;
+        x.comm = c;
+        x.dst = recv ? (int32_t*)f->left_in.p : nullptr;
+        x.dst_e = recv ? (int32_t*)f->left_in_e.p : nullptr;
+        x.flag = recv ? (uint32_t*)f->left_flag.p : nullptr;
+        x.h = f->h;
+        xs.push_back(x);
+    };
+    const int g = R.rank;
+    if (has_left) {
+        add(&S.top, true, g - 1, R.comm[(g - 1) % 2]);
+        add(&S.bot, false, g - 1, R.comm[2 + (g - 1) % 2]);
+    }
+    if (has_right) {
+        add(&S.top, false, g + 1, R.comm[g % 2]);
+        add(&S.bot, true, g + 1, R.comm[2 + g % 2]);
+    }
     std::vector<std::thread> th = start_xfers(xs);
     bool ok = true;
     std::string err;
     try {
-        wait_stream(S.st, 300.0, "sharded construct level 1");
+        wait_stream(S.st, 300.0, "sharded construct level");
         fill_finish(S.fc);
     } catch (const Failure& f) {
         ok = false;
@@ -922,7 +984,7 @@ void level1_rccl(const ShardLevel1& J) {
     if (!ok) fail("%s", err.c_str());
     for (hipStream_t t : {S.top.s_send, S.top.s_recv, S.bot.s_send, S.bot.s_recv})
         if (t) wait_stream(t, 60.0, "shard transport");
-    level1_finish(S, J);
+    part_finish(S, J);
 }
 
 }  // namespace
@@ -1060,7 +1122,7 @@ int anyseq_construct_local_sharded(int kind, const anyseq_scoring* sc, const cha
         cs.world = nshards;
         cs.local = true;
         if (level1_local_possible(nshards, engine().num_cus))
-            cs.level1 = [nshards](const ShardLevel1& J) { level1_local(J, nshards); };
+            cs.blocked = [nshards](const ShardLevel& J) { blocked_local(J, nshards); };
         const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
                                             lens, alQuery, alSubject, cs);
         if (score) *score = v;
@@ -1088,7 +1150,7 @@ int anyseq_shard_construct(int kind, const anyseq_scoring* sc, const char* query
         cs.max_u8 = [comm](uint8_t* p, size_t n, hipStream_t st) {
             NCCLCHECK(ncclAllReduce(p, p, n, ncclUint8, ncclMax, comm, st));
         };
-        if (level1_rccl_possible(cs.rank, cs.world)) cs.level1 = [](const ShardLevel1& J) { level1_rccl(J); };
+        if (level1_rccl_possible(cs.rank, cs.world)) cs.blocked = [](const ShardLevel& J) { blocked_rccl(J); };
         const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
                                             lens, alQuery, alSubject, cs);
         if (score) *score = v;

@@ -120,3 +120,27 @@ def level1_best_ranks(world: int):
     """Ranks holding the last column of (forward, reversed) half: a last-column best
     cell (semiglobal free end) is theirs alone; every rank's cells count for local."""
     return world - 1, 0
+
+
+# Column-blocked levels beyond level 1 (DESIGN.md §6.2, anyseq_engine.cpp): level k has
+# P = 2^(k-1) parts and is column-blocked when world >= 2P; part p runs over the ranks
+# [p*world/P, (p+1)*world/P) exactly like level 1 over all ranks, on its own query rows
+# [off, off+len) and subject columns.
+
+def blocked_level(parts: int, world: int) -> bool:
+    """Whether a level of `parts` parts is column-blocked over `world` ranks."""
+    return world >= 2 * parts
+
+
+def part_subgroup(p: int, parts: int, world: int):
+    """(first rank, ranks) of part p's subgroup."""
+    r0 = p * world // parts
+    return r0, (p + 1) * world // parts - r0
+
+
+def part_segments(rank: int, r0: int, G: int, off: int, length: int):
+    """((first, w) of LH, (first, w) of RH) written by `rank` of a part's subgroup: its
+    block of the part's query rows, LH indexed by query position, RH by the reversed
+    half's column (distance from the part's end, plus off)."""
+    c0, w = block(rank - r0, G, length)
+    return (off + c0, w), (off + length - c0 - w, w)

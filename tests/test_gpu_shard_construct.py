@@ -47,15 +47,35 @@ def test_sharded_construct_multi_level(anyseq):
 
 @pytest.mark.parametrize("ranks", [4, 8])
 def test_sharded_construct_config2(anyseq, ranks):
-    """configs[2] (SW affine 65536^2) over 4 and 8 virtual ranks (level 1 column-blocked)
-    against the committed fixture."""
+    """configs[2] (SW affine 65536^2) over 4 and 8 virtual ranks against the committed
+    fixture: levels 1..log2(ranks) column-blocked over rank subgroups (level 1 over all
+    ranks, level 2's two parts over half of them each, at 8 ranks level 3's four parts
+    over two each), the rest dealt round-robin."""
     g = json.load(open(os.path.join(GOLD, "config2_65536.json")))
     q, s = anyseq.main_random_pair(65536, 65536)
     sc = g["scoring"]
+    anyseq.last_shard_plan()
     v, aq, as_ = anyseq.construct_local_sharded(g["kind"], q, s, ranks, sc["match"], sc["mismatch"],
                                                 sc["gap_open"], sc["gap_extend"])
+    assert anyseq.last_shard_plan() == {4: 2, 8: 3}[ranks]
     assert v == g["score"]
     assert (hashlib.sha256(aq).hexdigest(), hashlib.sha256(as_).hexdigest()) == (g["sha_alq"], g["sha_als"])
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_sharded_construct_blocked_levels(anyseq, kind):
+    """Levels >= 2 column-blocked over rank subgroups (uneven at 5 and 6 ranks: subgroups
+    of 2 and 3) against the single-GPU construct: random and related pairs, one part
+    empty or one block wide at the deeper levels (short subjects)."""
+    rng = random.Random(96)
+    shapes = [(3000, 2600), (2500, 4100), (1800, 700), (4000, 3900)]
+    for i, (n, m) in enumerate(shapes):
+        sc = SCHEMES[i % len(SCHEMES)]
+        q = rnd(rng, n)
+        s = related(rng, q, m) if i % 2 == 0 else rnd(rng, m)
+        want = anyseq.construct(kind, q, s, *sc)
+        for ns in (4, 5, 6, 8):
+            assert anyseq.construct_local_sharded(kind, q, s, ns, *sc) == want, (kind, n, m, sc, ns)
 
 
 def related(rng, q, m):
@@ -96,19 +116,23 @@ def test_sharded_construct_level1_column_blocks(anyseq, kind):
 
 
 def test_sharded_construct_level1_path_taken(anyseq, monkeypatch):
-    """The column-blocked level 1 runs one fill per rank (round-robin: the two halves'
-    owners only), and both plans give the single-GPU result."""
+    """The column-blocked levels run one fill per rank (round-robin: the halves' owners
+    only: 2 at level 1, 4 at level 2, 8 at level 3), and both plans give the single-GPU
+    result."""
     rng = random.Random(94)
     q = rnd(rng, 3000)
     s = related(rng, q, 2600)
     want = anyseq.construct("local", q, s, 2, -1, -2, -1)
-    launches = {}
+    launches, plans = {}, {}
     for flag in ("1", "0"):
         monkeypatch.setenv("ANYSEQ_SHARD_L1", flag)
         anyseq.last_fill_stats()
+        anyseq.last_shard_plan()
         assert anyseq.construct_local_sharded("local", q, s, 8, 2, -1, -2, -1) == want, flag
         launches[flag] = anyseq.last_fill_stats()[1]
-    assert launches["1"] - launches["0"] == 8 - 2, launches
+        plans[flag] = anyseq.last_shard_plan()
+    assert plans == {"1": 3, "0": 0}, plans
+    assert launches["1"] - launches["0"] >= (8 - 2) + (8 - 4) - 2, launches
 
 
 def test_sharded_construct_level1_queue_fallback(anyseq, monkeypatch):

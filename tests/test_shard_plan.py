@@ -311,3 +311,99 @@ def test_rccl_worker_cases_cover_column_blocked_level1():
     for kind, n, m, exp in mod.CONSTRUCT_CASES:
         assert mod.level1_expected(n, m, 2) == exp, (kind, n, m)
     assert {c[0] for c in blocked} >= {"local", "semiglobal"}
+
+
+# ------------------------- column-blocked levels >= 2 over rank subgroups (§6.2) --
+def _blocked_worker(rank, world, port, levels, results):
+    """Every part of a level runs over its own subgroup of ranks like level 1 over all
+    of them: rank g fills its block of the part's query rows of both transposed halves
+    (pure-Python stand-in fill), ships boundary columns to its neighbours INSIDE the
+    subgroup, and writes its bottom rows into zeroed LH / RH at part_segments; one SUM
+    all-reduce must give every part's halves' columns."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    gap = -1
+    for kind_name, q, s, parts in levels:
+        kind = KINDS[kind_name]
+        n = len(q)
+        LH = torch.zeros(n, dtype=torch.int64)
+        RH = torch.zeros(n, dtype=torch.int64)
+        P = len(parts)
+        assert SP.blocked_level(P, world)
+        for p, (off, ln, soff, mw, half) in enumerate(parts):
+            r0, G = SP.part_subgroup(p, P, world)
+            if not (r0 <= rank < r0 + G):
+                continue
+            g = rank - r0
+            (c0, w), (rb, _) = SP.part_segments(rank, r0, G, off, ln)
+            qp, sp_ = q[off:off + ln], s[soff:soff + mw]
+            blk = qp[c0 - off:c0 - off + w]
+            rows_f, rows_r = sp_[:half], sp_[half:][::-1]
+            lt = None
+            if g > 0:
+                t = torch.zeros(len(rows_f), dtype=torch.int64)
+                dist.recv(t, src=rank - 1)
+                lt = [int(x) + SP.left_shift_top(kind, g, G, ln, gap) for x in t]
+            Ht = _fill(kind, rows_f, blk, lt)
+            if g < G - 1:
+                dist.send(torch.tensor([row[w - 1] for row in Ht], dtype=torch.int64), dst=rank + 1)
+            lb = None
+            if g < G - 1:
+                t = torch.zeros(len(rows_r), dtype=torch.int64)
+                dist.recv(t, src=rank + 1)
+                lb = [int(x) + SP.left_shift_bottom(kind, g, G, ln, gap) for x in t]
+            Hb = _fill(kind, rows_r, blk[::-1], lb)
+            if g > 0:
+                dist.send(torch.tensor([row[w - 1] for row in Hb], dtype=torch.int64), dst=rank - 1)
+            for k in range(w):
+                LH[c0 + k] = Ht[-1][k] + SP.level1_frame(kind, c0 - off, gap)
+                RH[rb + k] = Hb[-1][k] + SP.level1_frame(kind, rb - off, gap)
+        dist.all_reduce(LH, op=dist.ReduceOp.SUM)
+        dist.all_reduce(RH, op=dist.ReduceOp.SUM)
+        out.append((LH.tolist(), RH.tolist()))
+    if rank == 0:
+        results.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4, 5])
+def test_sharded_level2_column_blocks(world):
+    """Level 2 (two parts) column-blocked over two rank subgroups at world 4 and 5
+    (uneven subgroups 2 + 3): the assembled columns equal the whole halves' bottom rows
+    of both parts, as anyseq_shard.cpp blocked_rccl / blocked_local build them."""
+    import torch.multiprocessing as mp
+    rng = random.Random(77 + world)
+    levels = []
+    for kind in KINDS:
+        q = bytes(rng.choice(b"ACGT") for _ in range(37))
+        s = bytes(rng.choice(b"ACGT") for _ in range(30))
+        # parts (query off, len, subject off, columns, left-half width): rows split at 17
+        parts = [(0, 17, 0, 15, 8), (17, 20, 15, 15, 7)]
+        levels.append((kind, q, s, parts))
+    ctx = mp.get_context("spawn")
+    results = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_blocked_worker, args=(r, world, port, levels, results)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = results.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for (kind, q, s, parts), (LH, RH) in zip(levels, got):
+        k = KINDS[kind]
+        wantL, wantR = [0] * len(q), [0] * len(q)
+        for off, ln, soff, mw, half in parts:
+            qp, sp_ = q[off:off + ln], s[soff:soff + mw]
+            wl = _fill(k, sp_[:half], qp, None)[-1]
+            wr = _fill(k, sp_[half:][::-1], qp[::-1], None)[-1]
+            wantL[off:off + ln] = wl
+            wantR[off:off + ln] = wr
+        assert LH == wantL, (kind, world)
+        assert RH == wantR, (kind, world)
+    assert SP.part_subgroup(1, 2, 5) == (2, 3) and not SP.blocked_level(4, 7)
