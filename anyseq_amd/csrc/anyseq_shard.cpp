@@ -163,9 +163,17 @@ struct RcclState {
 };
 std::unique_ptr<RcclState> g_rccl;
 
-int chunk_rows() {
-    const int c = env_int("ANYSEQ_SHARD_CHUNK", 1024);
-    return std::max(64, c / 64 * 64);
+// Rows per transported chunk of a front of h rows: 1024 up to 256K rows, then h/256
+// (a power of two, at most 16384), so a genome-length front (4.64M rows) ships ~280
+// chunks per direction instead of ~4500 host-thread send calls, for a start lag of one
+// chunk per rank (16384 rows ~ 0.6 ms of a ~1 s rank fill).  Both sides of a link
+// derive it from the same front height.  ANYSEQ_SHARD_CHUNK forces it.
+int chunk_rows(int h) {
+    const int forced = env_int("ANYSEQ_SHARD_CHUNK", 0);
+    if (forced > 0) return std::max(64, forced / 64 * 64);
+    int c = 1024;
+    while (c < 16384 && (int64_t)c * 256 < (int64_t)h) c *= 2;
+    return c;
 }
 
 // Host-side wait with a deadline: a lost message must not hang the caller.
@@ -218,16 +226,16 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     if (inT) HIPCHECK(hipMemsetAsync(inT, 0x80, (size_t)h1 * 4, S.st));
     if (inB) HIPCHECK(hipMemsetAsync(inB, 0x80, (size_t)h2 * 4, S.st));
     // chunk-ready flags of the received columns (the transport sets flag k after chunk k)
-    const int CR = chunk_rows();
+    const int CRT = chunk_rows(h1), CRB = chunk_rows(h2);
     uint32_t* flT = nullptr;
     uint32_t* flB = nullptr;
     if (inT && !direct) {
-        flT = (uint32_t*)S.top.left_flag.get((size_t)((h1 + CR - 1) / CR) * 4);
-        HIPCHECK(hipMemsetAsync(flT, 0, (size_t)((h1 + CR - 1) / CR) * 4, S.st));
+        flT = (uint32_t*)S.top.left_flag.get((size_t)((h1 + CRT - 1) / CRT) * 4);
+        HIPCHECK(hipMemsetAsync(flT, 0, (size_t)((h1 + CRT - 1) / CRT) * 4, S.st));
     }
     if (inB && !direct) {
-        flB = (uint32_t*)S.bot.left_flag.get((size_t)((h2 + CR - 1) / CR) * 4);
-        HIPCHECK(hipMemsetAsync(flB, 0, (size_t)((h2 + CR - 1) / CR) * 4, S.st));
+        flB = (uint32_t*)S.bot.left_flag.get((size_t)((h2 + CRB - 1) / CRB) * 4);
+        HIPCHECK(hipMemsetAsync(flB, 0, (size_t)((h2 + CRB - 1) / CRB) * 4, S.st));
     }
     if (direct) {   // local direct mode: the neighbours poll these columns themselves
         HIPCHECK(hipMemsetAsync(colT, 0x80, (size_t)h1 * 4, S.st));
@@ -260,7 +268,7 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     P.left_in = inT;
     P.left_in_e = inTe;
     P.left_flag = flT;
-    P.left_chunk = CR;
+    P.left_chunk = CRT;
     P.out_col_e = colTe;
     P.out_f_last = colTe ? colTe + h1 : nullptr;
     S.lT = inT;
@@ -278,6 +286,7 @@ void setup_shard(Shard& S, int N, int kind, const anyseq_scoring& sc, const uint
     P.left_in = inB;
     P.left_in_e = inBe;
     P.left_flag = flB;
+    P.left_chunk = CRB;
     P.out_col_e = colBe;
     P.out_f_last = colBe ? colBe + h2 : nullptr;
     P.left_shift = shB * ng;
@@ -308,7 +317,7 @@ struct Xfer {
 void run_xfer(Xfer* x) {
     try {
         HIPCHECK(hipSetDevice(x->device));
-        const int CR = chunk_rows();
+        const int CR = chunk_rows(x->h);
         for (int r0 = 0; r0 < x->h; r0 += CR) {
             const int r1 = std::min(x->h, r0 + CR);
             // affine: E rows follow the H rows; the last chunk's E carries one more
@@ -651,7 +660,7 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
                         f == &shards[g].top ? "top" : "bot", pv, lv[0], lv[1], lv[2], lv[3], oc[0], oc[1], oc[2],
                         oc[3]);
                 if (f->left_flag.p) {
-                    const int nfl = (f->h + chunk_rows() - 1) / chunk_rows();
+                    const int nfl = (f->h + chunk_rows(f->h) - 1) / chunk_rows(f->h);
                     std::vector<uint32_t> fl((size_t)nfl);
                     (void)hipMemcpy(fl.data(), f->left_flag.p, (size_t)nfl * 4, hipMemcpyDeviceToHost);
                     for (uint32_t x : fl) fprintf(stderr, " %u", x);

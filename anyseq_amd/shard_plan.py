@@ -57,8 +57,19 @@ def split_columns(g: int, nshards: int, w: int):
     return range(-1, w if g == nshards - 1 else w - 1)
 
 
-def chunks(h: int, chunk_rows: int = 1024):
-    """Row chunks [r0, r1) shipped per message, and the band count each waits for."""
+def chunk_rows_for(h: int) -> int:
+    """Rows per transported chunk of a front of h rows (anyseq_shard.cpp chunk_rows):
+    1024, doubled while 256 chunks would not cover h, at most 16384."""
+    c = 1024
+    while c < 16384 and c * 256 < h:
+        c *= 2
+    return c
+
+
+def chunks(h: int, chunk_rows: int = 0):
+    """Row chunks [r0, r1) shipped per message, and the band count each waits for
+    (chunk_rows 0: the engine's adaptive size)."""
+    chunk_rows = chunk_rows or chunk_rows_for(h)
     out = []
     for r0 in range(0, h, chunk_rows):
         r1 = min(h, r0 + chunk_rows)

@@ -128,6 +128,8 @@ def test_plan_partition_and_chunks():
         blocks = [SP.block(g, N, m) for g in range(N)]
         assert blocks[0][0] == 0 and sum(w for _, w in blocks) == m
         assert all(blocks[g][0] + blocks[g][1] == blocks[g + 1][0] for g in range(N - 1))
+    assert SP.chunk_rows_for(65536) == 1024 and SP.chunk_rows_for(4_641_652) == 16384
+    assert len(SP.chunks(4_641_652)) == 284   # genome-length front: ~280 sends, not ~4500
     ch = SP.chunks(2500, 1024)
     assert ch == [(0, 1024, 16), (1024, 2048, 32), (2048, 2500, 40)]
 
