@@ -319,6 +319,10 @@ B_WB = 160                                       # LUT weight bytes of 4 steps
 
 
 NEG_INF = -(1 << 29)   # kAffNeg
+# gen_aff2 step order (round 4): 1 = no VALU reads the previous instruction's result
+REORDER = int(os.environ.get("ANYSEQ_GEN_REORDER", "1"))
+# gen_aff2 LDS publish (round 4): 1 = the slot address once per block, counter inside the exec window
+SLIM = int(os.environ.get("ANYSEQ_GEN_SLIM", "1"))
 AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
@@ -413,6 +417,26 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
         """Lanes 48..63 of the (G, F) pair `reg` hold 16 columns of chunk b-2: half
         `half` of the next band's top row (LDS: always written -- a dummy slot and
         counter 0 while b < 2 -- so the counted lgkmcnt waits stay fixed)."""
+        if pub == "lds" and SLIM:
+            # round 4: the slot address once per block (half 1 reuses it through the
+            # offset field), the counter written by the same 16 lanes inside the exec
+            # window, exec restored to all lanes (the loop runs with every lane active)
+            if half == 0:
+                e("s_sub_u32 %[x2], %[b], 2")
+                e("s_lshl_b32 %[x2], %[x2], 8")
+                e("s_and_b32 %[x2], %[x2], 4095")
+                e("s_add_u32 %[x2], %[x2], %[nb]")
+                e(f"v_add_u32_e32 v{B_VT}, %[x2], %[lo]")
+            # counter: 2(b-2) + half + 1 halves published (0 while b < 2)
+            e("s_lshl_b32 %[x2], %[b], 1")
+            e(f"s_sub_u32 %[x2], %[x2], {3 - half}")
+            e("s_max_i32 %[x2], %[x2], 0")
+            e(f"v_mov_b32_e32 v{B_VT2}, %[x2]")
+            e("s_mov_b64 exec, %[hm]")
+            e(f"ds_write_b64 v{B_VT}, v[{reg}:{reg + 1}] offset:{128 * half}")
+            e(f"ds_write_b32 %[anp], v{B_VT2}")
+            e("s_mov_b64 exec, -1")
+            return
         if pub == "glob":
             e("s_cmp_lt_u32 %[b], 2")
             e(f"s_cbranch_scc1 L_nopub{half}{k}_%=")
@@ -509,6 +533,14 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
             sw = v(cs + u // 4)
             tg = "%[tfg]" if u == 0 else TG_(u - 1)
             tf = "%[tff]" if u == 0 else TF_(u - 1)
+            # Instruction order (round 4): no VALU reads the result of the instruction
+            # right before it -- E's max3 first, the DPP moves between the E pair, the
+            # shift-register moves between OG -> hg -> F-down, the best after hg.
+            if REORDER:
+                if L:
+                    e("v_max3_i32 %[e], %[e], %[hg], %[zlp]")
+                else:
+                    e("v_max_i32_e32 %[e], %[e], %[hg]")
             if lut:
                 if u % 4 == 0:
                     e(f"v_perm_b32 v{B_WB}, %[lh], %[ll], {sw}")
@@ -518,16 +550,32 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
                 e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
                 e(f"v_cndmask_b32_e32 v{B_AW}, %[wx], %[wm], vcc")
                 e(f"v_add_u32_e32 v{B_AA}, {dg}, v{B_AW}")
-            if L:
-                e("v_max3_i32 %[e], %[e], %[hg], %[zlp]")
-                e("v_add_u32_e32 %[e], %[ge], %[e]")
+            sr = u >= 2 and pub != "none"
+            if REORDER:
+                e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
+                if L:
+                    e("v_add_u32_e32 %[e], %[ge], %[e]")
+                e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_max3_i32 {OG_(u)}, v{B_AA}, %[e], {tf}")
+                if sr:
+                    e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
+                if L and u % 2 == 1 and not epi:
+                    e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
+                if sr:
+                    e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_max_i32_e32 {OF_(u)}, {tf}, %[hg]")
             else:
-                e("v_max_i32_e32 %[e], %[e], %[hg]")
-            e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
-            e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
-            e(f"v_max3_i32 {OG_(u)}, v{B_AA}, %[e], {tf}")
-            e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
-            e(f"v_max_i32_e32 {OF_(u)}, {tf}, %[hg]")
+                if L:
+                    e("v_max3_i32 %[e], %[e], %[hg], %[zlp]")
+                    e("v_add_u32_e32 %[e], %[ge], %[e]")
+                else:
+                    e("v_max_i32_e32 %[e], %[e], %[hg]")
+                e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_max3_i32 {OG_(u)}, v{B_AA}, %[e], {tf}")
+                e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
+                e(f"v_max_i32_e32 {OF_(u)}, {tf}, %[hg]")
             if epi:
                 if L:
                     # best over real cells only (cnt >= 0: column <= w-1)
@@ -540,11 +588,12 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
                 e("v_cndmask_b32_e32 %[ec], %[ec], %[e], vcc")
                 e(f"v_cndmask_b32_e32 %[fc], %[fc], {OF_(u)}, vcc")
                 e("v_add_u32_e32 %[cnt], -1, %[cnt]")
-            if L and u % 2 == 1 and not epi:
-                e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
-            if u >= 2 and pub != "none":
-                e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-                e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            if not REORDER:
+                if L and u % 2 == 1 and not epi:
+                    e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
+                if sr:
+                    e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+                    e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
             if u == 16 and pub != "none":
                 publish(k, 0, AO0 + 6)             # cell pair of step 15: steps 0..15 in lanes 48..63
                 event(k, 1, EVB + 2)               # producer: first half of chunk EVB published

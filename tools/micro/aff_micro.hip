@@ -42,13 +42,16 @@ __global__ __launch_bounds__(512) void micro(int nblocks, unsigned long long* ou
         if constexpr (V == 5) AFFM_RUN(AFFM_G_cur);
         if constexpr (V == 6) AFFM_RUN(AFFM_G_l);
         if constexpr (V == 7) AFFM_RUN(AFFM_L_es_np);
+        if constexpr (V == 8) AFFM_RUN(AFFM_L_ro);
+        if constexpr (V == 9) AFFM_RUN(AFFM_L_ro_np);
+        if constexpr (V == 10) AFFM_RUN(AFFM_G_ro);
     }
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
     sink[blockIdx.x * blockDim.x + threadIdx.x] = cur + fd + dg + e + hg + best + (int)z + (int)zb;
     if (lane == 0) out[blockIdx.x * 8 + wave] = c1 - c0;
 }
 
-static const char* kNames[] = {"L_cur", "L_x", "L_xl", "L_xl_np", "L_xl_ds", "G_cur", "G_l", "L_es_np"};
+static const char* kNames[] = {"L_cur", "L_x", "L_xl", "L_xl_np", "L_xl_ds", "G_cur", "G_l", "L_es_np", "L_ro", "L_ro_np", "G_ro"};
 
 template <int V>
 void run(int waves, int wgs) {
@@ -99,5 +102,8 @@ int main() {
     all<5>();
     all<6>();
     all<7>();
+    all<8>();
+    all<9>();
+    all<10>();
     return 0;
 }

@@ -116,6 +116,39 @@ def step_es(e, u, pub="none"):
         e(f"v_max3_i32 %[best], %[best], {OG(u - 1)}, {OG(u)}")
 
 
+def step_ro(e, u, L, pub=True):
+    """X-space (L) / G-space LUT step with the instructions reordered so that no VALU
+    reads the result of the instruction right before it (round 4 experiment):
+    e1 = max3(e, hg, zl) first, the DPP moves between the E pair, the shift-register
+    moves between OG -> hg -> OF, and the best after hg."""
+    tg = "%[tfg]" if u == 0 else TG(u - 1)
+    tf = "%[tff]" if u == 0 else TF(u - 1)
+    g = "%[cur]" if u == 0 else OG(u - 1)
+    f = "%[fd]" if u == 0 else OF(u - 1)
+    dg = "%[dg]" if u == 0 else ("%[tfg]" if u == 1 else TG(u - 2))
+    if L:
+        e("v_max3_i32 %[e], %[e], %[hg], %[zl]")
+    else:
+        e("v_max_i32_e32 %[e], %[e], %[hg]")
+    if u % 4 == 0:
+        e(f"v_perm_b32 v{WB}, %[lh], %[ll], {v(SW + u // 4)}")
+    e(f"v_add_u32_sdwa v{AA}, {dg}, sext(v{WB}) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "
+      f"src1_sel:BYTE_{u % 4}")
+    e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
+    if L:
+        e("v_add_u32_e32 %[e], %[ge], %[e]")
+    e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
+    e(f"v_max3_i32 {OG(u)}, v{AA}, %[e], {tf}")
+    if pub and u >= 2:
+        e(f"v_mov_b32_dpp {OF(u - 1)}, {OF(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    e(f"v_add_u32_e32 %[hg], %[go], {OG(u)}")
+    if L and u % 2 == 1:
+        e(f"v_max3_i32 %[best], %[best], {OG(u - 1)}, {OG(u)}")
+    if pub and u >= 2:
+        e(f"v_mov_b32_dpp {OG(u - 1)}, {OG(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    e(f"v_max_i32_e32 {OF(u)}, {tf}, %[hg]")
+
+
 def block(variant):
     out = []
     e = out.append
@@ -139,6 +172,12 @@ def block(variant):
             step_x(e, u, False, True)
         elif variant == "L_es_np":
             step_es(e, u)
+        elif variant == "L_ro":
+            step_ro(e, u, True)
+        elif variant == "L_ro_np":
+            step_ro(e, u, True, pub=False)
+        elif variant == "G_ro":
+            step_ro(e, u, False)
         else:
             raise ValueError(variant)
     e(f"v_mov_b32_e32 %[cur], {OG(31)}")
@@ -151,7 +190,7 @@ def block(variant):
     return out
 
 
-VARIANTS = ["L_cur", "L_x", "L_xl", "L_xl_np", "L_xl_ds", "G_cur", "G_l", "L_es_np"]
+VARIANTS = ["L_cur", "L_x", "L_xl", "L_xl_np", "L_xl_ds", "G_cur", "G_l", "L_es_np", "L_ro", "L_ro_np", "G_ro"]
 
 
 def main():

@@ -54,6 +54,24 @@ __global__ void k(int iters, unsigned long long* out, int* sink) {
         if (T == 10) asm volatile(REP8("v_mov_b32 %0, %8\nv_mov_b32 %1, %8\nv_mov_b32 %2, %8\nv_mov_b32 %3, %8\n"
                                       "v_mov_b32 %4, %9\nv_mov_b32 %5, %9\nv_mov_b32 %6, %9\nv_mov_b32 %7, %9\n")
                                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(y));
+        if (T == 11) asm volatile(REP8("v_add_u32_sdwa %0, %0, sext(%8) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n"
+                                       "v_add_u32_sdwa %1, %1, sext(%8) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2\n"
+                                       "v_add_u32_sdwa %2, %2, sext(%8) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3\n"
+                                       "v_add_u32_sdwa %3, %3, sext(%8) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n"
+                                       "v_add_u32_sdwa %4, %4, sext(%9) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n"
+                                       "v_add_u32_sdwa %5, %5, sext(%9) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2\n"
+                                       "v_add_u32_sdwa %6, %6, sext(%9) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3\n"
+                                       "v_add_u32_sdwa %7, %7, sext(%9) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n")
+                                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(y));
+        if (T == 12) asm volatile(REP8("v_perm_b32 %0, %8, %9, %0\nv_perm_b32 %1, %8, %9, %1\nv_perm_b32 %2, %8, %9, %2\nv_perm_b32 %3, %8, %9, %3\n"
+                                       "v_perm_b32 %4, %8, %9, %4\nv_perm_b32 %5, %8, %9, %5\nv_perm_b32 %6, %8, %9, %6\nv_perm_b32 %7, %8, %9, %7\n")
+                                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(y));
+        // the affine step's mix without dependencies: 2 dpp, 2 max3, 2 add, 1 max, 1 sdwa add per 8
+        if (T == 13) asm volatile(REP8("v_mov_b32_dpp %0, %8 wave_shr:1 row_mask:0xf bank_mask:0xf\nv_max3_i32 %1, %8, %9, %1\n"
+                                       "v_add_u32 %2, %8, %9\nv_add_u32_sdwa %3, %3, sext(%8) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n"
+                                       "v_mov_b32_dpp %4, %9 wave_shr:1 row_mask:0xf bank_mask:0xf\nv_max3_i32 %5, %8, %9, %5\n"
+                                       "v_add_u32 %6, %8, %9\nv_max_i32 %7, %8, %9\n")
+                                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(x), "v"(y));
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     sink[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
@@ -62,7 +80,8 @@ __global__ void k(int iters, unsigned long long* out, int* sink) {
 
 const char* names[] = {"v_add indep", "v_max indep", "v_max3 indep", "v_mov_dpp indep", "cmp_sdwa+cndmask pairs",
                        "v_add dep chain", "v_max3 dep chain", "max3->nop1->dpp chain", "2x max3/dpp chains",
-                       "cmp_sdwa indep", "v_mov indep"};
+                       "cmp_sdwa indep", "v_mov indep", "v_add_sdwa(byte sext) indep", "v_perm indep",
+                       "affine step mix indep"};
 
 template <int T>
 void run(int waves) {
@@ -83,6 +102,6 @@ void run_all() { run<T>(1); run<T>(4); run<T>(8); }
 
 int main() {
     run_all<0>(); run_all<1>(); run_all<2>(); run_all<3>(); run_all<4>(); run_all<5>(); run_all<6>(); run_all<7>();
-    run_all<8>(); run_all<9>(); run_all<10>();
+    run_all<8>(); run_all<9>(); run_all<10>(); run_all<11>(); run_all<12>(); run_all<13>();
     return 0;
 }

@@ -2,7 +2,7 @@
 # Round 4: latency micros, band timeline (stamps build), kernel trace of configs[2].
 set -o pipefail
 O=gpurun_out/r04f; mkdir -p $O
-for b in pingpong_micro lat_micro step_lat aff_micro; do
+for b in isa_micro pingpong_micro lat_micro step_lat aff_micro; do
   timeout -k 10 60 tools/micro/bin/$b > $O/$b.txt 2>&1 || exit 1
 done
 timeout -k 10 120 python -u tools/probes/_aff_timeline.py $O/tl > $O/timeline.txt 2>&1 || exit 1
