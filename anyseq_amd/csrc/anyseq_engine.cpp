@@ -483,7 +483,10 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     C.NW = NW;
     C.h_probs = probs;
     // staged in pinned memory (a truly asynchronous copy); the previous launch of this
-    // context has completed (fill_finish / fill_collect), so the staging area is free
+    // context has completed (fill_finish / fill_collect), so the staging area is free.
+    // (Coherent allocation + the kernel's descriptor digest guard against the round-start
+    // fault's suspected mechanism, a stale cached staging line; that mechanism is an
+    // unproven inference)
     char* pin = (char*)C.pin.get(64 + ub + 16);
     C.err_host = (uint32_t*)pin;
     memcpy(pin + 64, C.h_probs.data(), pb);
