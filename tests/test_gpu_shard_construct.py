@@ -151,3 +151,18 @@ def test_sharded_construct_level1_queue_fallback(anyseq, monkeypatch):
         assert anyseq.construct_local_sharded("local", q, s, 2, 2, -1, -2, -1) == want, queues
         plans[queues] = anyseq.last_shard_plan()
     assert plans == {"4": 0, "24": 1}, plans
+
+
+def test_sharded_construct_nonpow2_fixture(anyseq):
+    """The non-power-of-two fixture (65536 x 60001 local, parts split at their middle
+    block) over 4 emulated ranks: levels 1 and 2 column-blocked over rank subgroups."""
+    g = json.load(open(os.path.join(GOLD, "config2_nonpow2.json")))
+    q, s = anyseq.main_random_pair(65536, 65536)
+    s = s[:g["ls"]]
+    sc = g["scoring"]
+    anyseq.last_shard_plan()
+    v, aq, as_ = anyseq.construct_local_sharded(g["kind"], q, s, 4, sc["match"], sc["mismatch"], sc["gap_open"],
+                                                sc["gap_extend"])
+    assert anyseq.last_shard_plan() == 2
+    assert v == g["score"]
+    assert (hashlib.sha256(aq).hexdigest(), hashlib.sha256(as_).hexdigest()) == (g["sha_alq"], g["sha_als"])
