@@ -66,6 +66,9 @@ hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* 
                                       int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows,
                                       hipStream_t st);
 hipError_t anyseq_launch_aff_level_plan(const AffLevelPlan* plan, hipStream_t st);
+hipError_t anyseq_launch_aff_final(const AffFinalPlan* plan, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
+                                   int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als,
+                                   hipStream_t st);
 hipError_t anyseq_launch_aff_level_tail(const void* tail, int fill_groups, hipStream_t st);
 hipError_t anyseq_launch_rows_check(const void* rows, size_t nwords, uint32_t sentinel, const void* probs, int nprobs,
                                     uint32_t* out, int inject, hipStream_t st);
@@ -301,6 +304,7 @@ void init_tuning_locked() {
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
     g_tuning.virtbest = env_int("ANYSEQ_VIRT_BEST", g_tuning.virtbest);
     g_tuning.devplan = env_int("ANYSEQ_AFF_DEVPLAN", g_tuning.devplan);
+    g_tuning.devfinal = env_int("ANYSEQ_AFF_DEVFINAL", g_tuning.devfinal);
     g_tuning_init = true;
 }
 
@@ -1174,7 +1178,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             as = aq + L;
         }
     };
-    HIPCHECK(hipStreamSynchronize(st));   // h_status is rewritten by the first level's download
+    // (the host-built levels rewrite h_status in their first download: they synchronise
+    // with its upload first, below; the device-planned levels download it at the end)
     auto tp = [&](int idx) { return typ[idx + 1]; };
     int64_t score = INT64_MIN;
     bool level1 = true;
@@ -1214,7 +1219,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         }
         return mx;
     };
-    bool planned = false;
+    bool planned = false, dev_final = false;
     if (!sharded && g_tuning.devplan && plan_rowbuf_bytes() <= ((size_t)8 << 30) && n < 8192 * 4096 - 1) {
         // Device-planned levels: every level is enqueued up front -- plan
         // (aff_level_plan_kernel builds the level from the splits on the device), prep,
@@ -1278,11 +1283,24 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         // then one error word per level
         // + with ANYSEQ_CHECK_ROWS, 8 words per level of the hand-off row check
         const int check_rows = env_int("ANYSEQ_CHECK_ROWS", 0);   // (read per call: tests toggle it)
-        const size_t tail_words = (size_t)std::max(nlev, 1) * (check_rows ? 17 : 9);
+        // + one word: the final level's split-table check (aff_final_blocks_kernel)
+        const size_t tail_words = (size_t)std::max(nlev, 1) * (check_rows ? 17 : 9) + 1;
         uint32_t* d_tail = (uint32_t*)E.pl_hdr.get(tail_words * 4 + 16);
         uint32_t* d_hdr = d_tail;
         uint32_t* d_err = d_tail + 8 * nlev;
         uint32_t* h_tail = (uint32_t*)E.pl_pin.get(tail_words * 4 + 16);
+        // the final level on the device too, right behind the levels (no host round trip):
+        // its block table, list of tall blocks and (worst case) HBM slab
+        const int64_t slab_bound = ((int64_t)n + 127 * (int64_t)sp.nb) * 128;
+        dev_final = g_tuning.devfinal && slab_bound <= ((int64_t)4 << 30);
+        BlockInfo* d_fblocks = nullptr;
+        int32_t* d_tall = nullptr;
+        uint8_t* d_fpred = nullptr;
+        if (dev_final) {
+            d_fblocks = (BlockInfo*)E.blocks.get((size_t)sp.nb * sizeof(BlockInfo));
+            d_tall = (int32_t*)E.tall.get(((size_t)sp.nb + 1) * 4);
+            d_fpred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(slab_bound, 16));
+        }
         while ((int)E.pl_ev.size() < 2 * nlev) {
             hipEvent_t ev;
             HIPCHECK(hipEventCreate(&ev));
@@ -1408,8 +1426,27 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             HIPCHECK(anyseq_launch_aff_level_tail(&T, T.has_next && T.nsent16 ? 1024 : 1, st));
             stage_check(st, "affine level (device plan)");
         }
+        uint32_t* d_ferr = d_tail + tail_words - 1;
+        if (dev_final) {
+            AffFinalPlan F{};
+            F.spl = d_spl;
+            F.typ = d_typ;
+            F.score = d_score;
+            F.blocks = d_fblocks;
+            F.tall = d_tall;
+            F.err = d_ferr;
+            F.nb = sp.nb;
+            F.n = n;
+            F.m = m;
+            F.kind = kind;
+            F.small_rows = kPredSmallRows;
+            g_stage_level = nlev + 1;
+            HIPCHECK(anyseq_launch_aff_final(&F, dq, ds, d_fpred, sc.match, sc.mismatch, sc.gap_open, sc.gap_extend,
+                                             d_alq, d_als, st));
+            stage_check(st, "aff_final (device plan)");
+        }
         HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + 1) * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(h_tail, d_tail, (size_t)nlev * (check_rows ? 17 : 9) * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(h_tail, d_tail, tail_words * 4, hipMemcpyDeviceToHost, st));
         {
             const hipError_t e = stream_wait_spin(st);
             if (e != hipSuccess) fail("affine construct levels failed: %s", hipGetErrorString(e));
@@ -1445,6 +1482,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         for (size_t i = 1; i < nsv; ++i)
             if (sp.v[i] < sp.v[i - 1] || sp.v[i] > n || typ[i] < T_H || typ[i] > T_AFTER)
                 fail("internal: planned levels left split %zu = %d (type %d)", i - 1, sp.v[i], typ[i]);
+        if (dev_final && h_tail[tail_words - 1])
+            fail("internal: the device final level found a bad split table (the host check passed)");
         if (nlev > 0) {
             const int32_t s32 = h_status[2 * nsv];
             score = kind == KIND_SEMIGLOBAL ? std::max(s32, 0) : s32;
@@ -1452,6 +1491,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         }
         planned = true;   // (the host loop below has nothing left)
     }
+    if (!planned) HIPCHECK(hipStreamSynchronize(st));   // h_status: its upload before the first download
     for (int parts = 1; !planned && parts < sp.nb; parts *= 2) {
         ++g_stage_level;
         // free-end best cells, 2 per part, per view
@@ -1668,6 +1708,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             if (kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
         }
     }
+    if (dev_final) return score;   // (the final level is done: enqueued behind the levels)
     // final 128-column blocks: each view walks its own into its strings
     std::vector<BlockInfo>& blocks = E.host_blocks;   // outlives the async upload
     blocks.clear();
@@ -2030,6 +2071,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "slack") g_tuning.slack = value;
     else if (n == "virtual_best") g_tuning.virtbest = value;
     else if (n == "affine_device_plan") g_tuning.devplan = value;
+    else if (n == "affine_device_final") g_tuning.devfinal = value;
     else return -1;
     return 0;
 }

@@ -92,6 +92,7 @@ struct Tuning {
     int afflut = 1;      // affine fill: v_perm weight table when the pair has <= 8 symbols
     int slack = 0;       // affine fill: half chunks a band starts behind the structural minimum
     int devplan = 1;     // affine construct: Hirschberg levels planned on the device (one download)
+    int devfinal = 1;    // affine construct, device-planned: the final level's blocks built on the device too
     int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe
 };
 extern Tuning g_tuning;
@@ -133,6 +134,7 @@ struct Engine {
     DevBuf q, s, outcol, outrow, L, R, spl, parts, bmax, bind, blocks, pred, alq, als;
     DevBuf LE, RE, typ, pos;   // affine construct
     DevBuf status;             // affine construct: splits | types | score of a level (one download)
+    DevBuf tall;               // affine construct, device final level: the tall blocks' list
     DevBuf joinbuf;            // affine construct: per-slice partial maxima of the level's joins
     PinBuf pin_up, pin_down;   // construct: staged uploads / downloads of a level
     PinBuf pin_blocks;         // construct: the final level's block table

@@ -265,12 +265,24 @@ struct AffLevelTail {
 };
 
 // Affine final level (aff_predwalk_kernel): blocks of at most `lds_rows` rows (the
-// launch's tallest block, at most kPredLdsMaxRows) keep their predecessor bytes and
-// query rows and subject columns in LDS ((rows + 127) x 128 + rows + 128 bytes,
-// <= 160 KiB); taller ones use
-// an HBM slab.
+// launch's tallest block, at most kPredLdsMaxRows) keep their predecessor bytes (plus
+// a spare row for the walk's path record) and query rows in LDS ((rows + 128) x 128 +
+// rows bytes, <= 160 KiB); taller ones use an HBM slab.
 constexpr int kPredLdsMaxRows = 1140;
-inline int pred_lds_bytes(int rows) { return (rows + 127) * 128 + ((rows + 15) & ~15) + 128; }
+// the device final level's first launch: LDS slabs of up to this many rows (78 KB:
+// two workgroups per CU); taller blocks go to its second launch
+constexpr int kPredSmallRows = 480;
+// Device-planned final level (aff_final_blocks_kernel): the block table from the splits.
+struct AffFinalPlan {
+    const int32_t* spl;    // nb + 1 splits (rows), spl[0] = 0, spl[nb] = n
+    const int32_t* typ;    // nb + 1 types (T_*)
+    const int32_t* score;  // the level-1 value
+    BlockInfo* blocks;     // nb entries
+    int32_t* tall;         // 1 + nb: count, then the blocks taller than small_rows
+    uint32_t* err;         // set to 1 on a bad split table
+    int nb, n, m, kind, small_rows;
+};
+inline int pred_lds_bytes(int rows) { return (rows + 128) * 128 + ((rows + 15) & ~15); }
 
 // Device-side error codes written to the error word.
 enum : uint32_t { ERR_NONE = 0, ERR_SPIN_TIMEOUT = 1, ERR_BAD_DESC = 0x100 };

@@ -3054,34 +3054,141 @@ __device__ __forceinline__ void aff_walk_block(const BlockInfo& bi, int2 x, cons
     }
 }
 
+// The same walk over an LDS slab, by the whole wave in lock step (every value is
+// wave-uniform: scalar registers and branches, no exec-mask juggling), recording
+// only the path: position p = i + j + 1 gets (i + 1) << 2 | op (1 both symbols,
+// 2 a gap in the query, 3 a gap in the subject; 0 the position a diagonal move
+// skips) in bytes 126-127 of slab row p, which the walk has left behind (it reads
+// anti-diagonals i + j < p from then on; row h + 127 is the slab's spare row).  The
+// symbols are fetched afterwards by all lanes (aff_trace_out).  Returns the recorded
+// range [lo, hi] of positions.
+__device__ __forceinline__ int2 aff_walk_trace(const BlockInfo& bi, int2 x, uint8_t* slab) {
+    // (readfirstlane: the values are uniform, and the compiler must know it)
+    const bool free_start = __builtin_amdgcn_readfirstlane(bi.smode) >= BM_FREE_LOCAL;
+    const int e_end = __builtin_amdgcn_readfirstlane(bi.e_end);
+    int i = __builtin_amdgcn_readfirstlane(e_end == 2 ? x.x : bi.h - 1);
+    int j = __builtin_amdgcn_readfirstlane(e_end == 2 ? x.y : bi.w - 1);
+    int st = e_end == 1 ? 1 : 0;
+    const int hi = i + j + 1;
+    int lo = hi + 1;
+    auto rec = [&](int p, int ii, int op) {
+        *reinterpret_cast<uint16_t*>(slab + p * 128 + 126) = (uint16_t)(((ii + 1) << 2) | op);
+    };
+    while (i >= 0 || j >= 0) {
+        const int p = i + j + 1;
+        if (i < 0 || j < 0) {
+            if (free_start) break;   // the path starts on the border
+            if (i < 0) {
+                rec(p, i, 2);
+                --j;
+            } else {
+                rec(p, i, 3);
+                --i;
+            }
+            lo = p;
+            continue;
+        }
+        const int pb = __builtin_amdgcn_readfirstlane((int)slab[(i + j) * 128 + j]);
+        if (st == 0) {
+            const int hs = pb & 3;
+            if (hs == 3) break;   // clamped: the path starts after this cell
+            if (hs == 0) {
+                rec(p, i, 1);
+                rec(p - 1, 0, 0);
+                lo = p - 1;
+                --i;
+                --j;
+            } else {
+                st = hs;
+            }
+        } else if (st == 1) {
+            rec(p, i, 2);
+            lo = p;
+            st = (pb & 4) ? 1 : 0;
+            --j;
+        } else {
+            rec(p, i, 3);
+            lo = p;
+            st = (pb & 8) ? 2 : 0;
+            --i;
+        }
+    }
+    return make_int2(lo, hi);
+}
+
+// The recorded path's symbols, one position per lane: sparse i+j+1 output at oi+oj+p.
+__device__ __forceinline__ void aff_trace_out(const BlockInfo& bi, int2 r, const uint8_t* slab,
+                                              const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
+                                              uint8_t* alq, uint8_t* als) {
+    const int64_t base = (int64_t)bi.oi + bi.oj;
+    for (int p = r.x + (int)threadIdx.x; p <= r.y; p += 64) {
+        const int t = *reinterpret_cast<const uint16_t*>(slab + p * 128 + 126);
+        const int op = t & 3;
+        if (op == 0) continue;
+        const int i = (t >> 2) - 1, j = p - 1 - i;
+        alq[base + p] = op == 2 ? (uint8_t)'_' : Q[bi.oi + i];
+        als[base + p] = op == 3 ? (uint8_t)'_' : S[bi.oj + j];
+    }
+}
 
 // Final level, one wave per 128-column block: predecessors (aff_pred_block), then
-// lane 0 walks them (aff_walk_block) in the same launch.  A block of h <=
-// kPredLdsRows rows keeps its query rows and its (h + 127) x 128 predecessor
-// bytes in LDS (lds_rows: the launch's tallest block, capped), so neither the
-// sweep's query reads nor the walk's dependent reads go to HBM; taller blocks (long
-// vertical gaps) use the HBM slab at pred_base.
+// the walk in the same launch.  A block of h <= lds_rows rows (the launch's tallest
+// block, capped at kPredLdsMaxRows) keeps its query rows and its (h + 127) x 128
+// predecessor bytes in LDS, so neither the sweep's query reads nor the walk's
+// dependent reads go to HBM, and the whole wave walks it (aff_walk_trace); taller
+// blocks (long vertical gaps) use the HBM slab at pred_base and lane 0's walk
+// (aff_walk_block).
+//
+// Launch modes: list == nullptr walks block blockIdx.x (defer: skips blocks taller than
+// lds_rows and those the path does not touch, flags bit 2 -- aff_final_blocks_kernel's
+// table); else the workgroups walk the blocks list[1 .. list[0]] in turn (the tall
+// blocks deferred by the first launch).
+__device__ void aff_predwalk_one(BlockInfo* __restrict__ blocks, int b, const uint8_t* __restrict__ Q,
+                                 const uint8_t* __restrict__ S, uint8_t* __restrict__ pred, int match, int mismatch,
+                                 int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows, uint8_t* pw_lds);
+
 __global__ __launch_bounds__(64) void aff_predwalk_kernel(BlockInfo* __restrict__ blocks, int nblocks,
                                                           const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
                                                           uint8_t* __restrict__ pred, int match, int mismatch, int go,
-                                                          int ge, uint8_t* alq, uint8_t* als, int lds_rows) {
+                                                          int ge, uint8_t* alq, uint8_t* als, int lds_rows,
+                                                          const int32_t* __restrict__ list, int defer) {
     extern __shared__ __attribute__((aligned(16))) uint8_t pw_lds[];
+    if (list) {
+        const int cnt = min(list[0], nblocks);
+        for (int k = blockIdx.x; k < cnt; k += gridDim.x) {
+            aff_predwalk_one(blocks, list[1 + k], Q, S, pred, match, mismatch, go, ge, alq, als, lds_rows, pw_lds);
+            __syncthreads();   // (the next block reuses the LDS slab)
+        }
+        return;
+    }
     const int b = blockIdx.x;
     if (b >= nblocks) return;
+    if (defer) {
+        const BlockInfo bi = blocks[b];
+        if ((bi.flags & 4) || bi.h > lds_rows) return;
+    }
+    aff_predwalk_one(blocks, b, Q, S, pred, match, mismatch, go, ge, alq, als, lds_rows, pw_lds);
+}
+
+__device__ void aff_predwalk_one(BlockInfo* __restrict__ blocks, int b, const uint8_t* __restrict__ Q,
+                                 const uint8_t* __restrict__ S, uint8_t* __restrict__ pred, int match, int mismatch,
+                                 int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows, uint8_t* pw_lds) {
     const BlockInfo bi = blocks[b];
+    if (bi.flags & 4) return;                 // the path does not touch the block
     if (bi.e_end == 2 && bi.h <= 0) return;   // the path ended at the block's corner
     int2 x = make_int2(0, 0);
-    if (bi.h > 0 && bi.h <= lds_rows) {
-        uint8_t* qs = pw_lds + (lds_rows + 127) * 128;   // h query rows, then the 128 subject columns
-        uint8_t* ss = qs + ((bi.h + 15) & ~15);
-        for (int i = threadIdx.x; i < bi.h; i += 64) qs[i] = Q[bi.oi + i];
-        for (int j = threadIdx.x; j < bi.w; j += 64) ss[j] = S[bi.oj + j];
+    if (bi.h >= 0 && bi.h <= lds_rows) {
+        uint8_t* qs = pw_lds + (lds_rows + 128) * 128;   // the slab (+ the spare row), then h query rows
+        if (bi.h > 0) {
+            for (int i = threadIdx.x; i < bi.h; i += 64) qs[i] = Q[bi.oi + i];
+            __syncthreads();
+            x = aff_pred_block(bi, (const uint8_t*)qs, S, pw_lds, match, mismatch, go, ge);
+            __syncthreads();
+        }
+        // (the walk's dependent reads are all LDS: an HBM read per step would cost ~1 us)
+        const int2 r = aff_walk_trace(bi, x, pw_lds);
         __syncthreads();
-        x = aff_pred_block(bi, (const uint8_t*)qs, S, pw_lds, match, mismatch, go, ge);
-        __syncthreads();
-        // (the walk's reads of predecessors and symbols are all LDS: its steps are
-        // dependent, and an HBM read per step would cost ~1 us each)
-        if (threadIdx.x == 0) aff_walk_block(bi, x, (const uint8_t*)qs, (const uint8_t*)ss, (const uint8_t*)pw_lds, alq, als);
+        aff_trace_out(bi, r, pw_lds, Q, S, alq, als);
     } else {
         uint8_t* slab = pred + bi.pred_base;
         if (bi.h > 0) {
@@ -3095,6 +3202,50 @@ __global__ __launch_bounds__(64) void aff_predwalk_kernel(BlockInfo* __restrict_
         blocks[b].xi = x.x;
         blocks[b].xj = x.y;
     }
+}
+
+// The final level's block table from the last level's splits (device-planned
+// constructs), so the final level is enqueued behind the levels with
+// no host round trip: block b spans rows [spl[b], spl[b+1]) and columns [128b,
+// 128b + 128), its start / end types typ[b] / typ[b+1] (the host builder's rules,
+// aff_construct_hb).  Blocks the path does not touch -- and every block when the
+// level-1 value says the empty alignment (kind != global, <= 0) -- get flags bit 2.
+// Blocks taller than small_rows go to `tall` (count, then indices) for the second
+// predwalk launch; those taller than kPredLdsMaxRows use the HBM slab at (oi + 127 b)
+// x 128 (no scan: the slabs of consecutive blocks abut).  Any split out of order or
+// range, or type out of range, sets *err and leaves every block skipped.
+__global__ __launch_bounds__(1024) void aff_final_blocks_kernel(const AffFinalPlan a) {
+    __shared__ int bad, ntall;
+    if (threadIdx.x == 0) {
+        bad = 0;
+        ntall = 0;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i <= a.nb; i += blockDim.x) {
+        const int v = a.spl[i], t = a.typ[i];
+        const bool ok = v >= 0 && v <= a.n && (i == 0 || a.spl[i - 1] <= v) && t >= T_H && t <= T_AFTER;
+        if (!ok) atomicOr(&bad, 1);
+    }
+    __syncthreads();
+    if (bad && threadIdx.x == 0) *a.err = 1u;
+    const bool stop = bad || (a.kind != KIND_GLOBAL && *a.score <= 0);
+    for (int b = threadIdx.x; b < a.nb; b += blockDim.x) {
+        BlockInfo bi{};
+        const int ts = a.typ[b], te = a.typ[b + 1];
+        bi.oi = a.spl[b];
+        bi.h = a.spl[b + 1] - bi.oi;
+        bi.oj = b * 128;   // (the final blocks' width, align.impala:18)
+        bi.w = min(128, a.m - bi.oj);
+        bi.pred_base = ((int64_t)bi.oi + 127 * (int64_t)b) * 128;
+        bi.smode = ts == T_H ? BM_NORMAL : ts == T_E ? BM_EFREE : aff_free_bm(a.kind, bi.oj == 0);
+        bi.e_end = te == T_H ? 0 : te == T_E ? 1 : 2;
+        bi.flags = (a.kind == KIND_LOCAL ? 1 : 0) | (bi.oj + bi.w == a.m ? 2 : 0);
+        if (stop || ts == T_BEFORE || te == T_AFTER) bi.flags |= 4;
+        a.blocks[b] = bi;
+        if (!(bi.flags & 4) && bi.h > a.small_rows) a.tall[1 + atomicAdd(&ntall, 1)] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) a.tall[0] = ntall;
 }
 
 // --------------------------------------------------------------- launchers --
@@ -3510,7 +3661,32 @@ hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* 
         attr_set = 1;
     }
     hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(nblocks), dim3(64), bytes, st, (anyseq::BlockInfo*)blocks,
-                       nblocks, Q, S, pred, match, mismatch, go, ge, alq, als, lds_rows);
+                       nblocks, Q, S, pred, match, mismatch, go, ge, alq, als, lds_rows, nullptr, 0);
+    return hipGetLastError();
+}
+
+// Device-planned final level: the block table (aff_final_blocks_kernel), the blocks of
+// at most small_rows rows (one workgroup each, LDS slabs of small_rows rows), then the
+// taller ones from the list (at most 256 workgroups, the largest LDS slab or HBM).
+hipError_t anyseq_launch_aff_final(const anyseq::AffFinalPlan* plan, const uint8_t* Q, const uint8_t* S,
+                                   uint8_t* pred, int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als,
+                                   hipStream_t st) {
+    const anyseq::AffFinalPlan& a = *plan;
+    if (a.nb <= 0) return hipSuccess;
+    static int attr_set = 0;
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void*)anyseq::aff_predwalk_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 anyseq::pred_lds_bytes(anyseq::kPredLdsMaxRows));
+        if (e != hipSuccess) return e;
+        attr_set = 1;
+    }
+    hipLaunchKernelGGL(anyseq::aff_final_blocks_kernel, dim3(1), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(a.nb), dim3(64), anyseq::pred_lds_bytes(a.small_rows), st,
+                       a.blocks, a.nb, Q, S, pred, match, mismatch, go, ge, alq, als, a.small_rows, nullptr, 1);
+    hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(std::min(a.nb, 256)), dim3(64),
+                       anyseq::pred_lds_bytes(anyseq::kPredLdsMaxRows), st, a.blocks, a.nb, Q, S, pred, match,
+                       mismatch, go, ge, alq, als, anyseq::kPredLdsMaxRows, a.tall, 0);
     return hipGetLastError();
 }
 

@@ -24,7 +24,10 @@ struct alignas(16) Sh {
     uint32_t dummy[kMaxW][320];   // "st" publishing: the non-publishing lanes' store targets
 };
 
-template <int V>
+// IOV > 0: the last wave of the workgroup (wave 4 of 5: on SIMD 0 beside compute wave 0)
+// stands in for the fill's I/O wave: passes of IOV independent VALU adds, each pass
+// followed by s_sleep IOS (0: none), until every compute wave is done.
+template <int V, int IOV = 0, int IOS = 1>
 __global__ __launch_bounds__(512) void micro(int nblocks, unsigned long long* out, int* sink) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     Sh& sh = *reinterpret_cast<Sh*>(smem);
@@ -35,7 +38,25 @@ __global__ __launch_bounds__(512) void micro(int nblocks, unsigned long long* ou
         (&sh.next[0][0])[i] = make_int2(0, 0);
     }
     if (lane < 8) sh.ctr[wave][lane] = 0x7fffffffu;
+    __shared__ uint32_t ndone;
+    if (threadIdx.x == 0) ndone = 0;
     __syncthreads();
+    if (IOV > 0 && wave == (int)(blockDim.x >> 6) - 1) {
+        const uint32_t nc = (blockDim.x >> 6) - 1;
+        int a0 = lane, a1 = lane + 1, a2 = lane + 2, a3 = lane + 3;
+        unsigned long long passes = 0;
+        while (__hip_atomic_load(&ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < nc) {
+#pragma unroll
+            for (int i = 0; i < IOV / 4; ++i)
+                asm volatile("v_add_u32 %0, %0, 1\n v_add_u32 %1, %1, 1\n v_add_u32 %2, %2, 1\n v_add_u32 %3, %3, 1"
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+            if (IOS > 0) __builtin_amdgcn_s_sleep(IOS);
+            ++passes;
+        }
+        sink[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3;
+        if (lane == 0) out[blockIdx.x * kMaxW + wave] = passes;
+        return;
+    }
     auto la = [](void* p) { return (uint32_t)(size_t)(__attribute__((address_space(3))) char*)p; };
     int g = lane, fdn = -5, dg = lane - 1, tfg = 0, tff = -5, e = -100, hg = -2, bx = 0;
     const int q = lane & 3, wm = 3, wx = 0, go = -2, zlp = lane + 3;
@@ -73,6 +94,7 @@ __global__ __launch_bounds__(512) void micro(int nblocks, unsigned long long* ou
     if constexpr (V == 4) LOOP(ANYSEQ_AF2_L_B0_LDS_U0);
 
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
+    if (IOV > 0 && lane == 0) __hip_atomic_fetch_add(&ndone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     sink[blockIdx.x * blockDim.x + threadIdx.x] = g + fdn + dg + e + hg + bx + tfg + tff + (int)st;
     if (lane == 0) out[blockIdx.x * kMaxW + wave] = c1 - c0;
 }
@@ -112,6 +134,37 @@ void run(int waves, int wgs) {
     (void)hipFree(d_sink);
 }
 
+// compute waves 0..3 + the stand-in I/O wave: cycles per step of wave 0 (shares SIMD 0)
+// and of waves 1..3, and the I/O wave's VALU issue rate
+template <int IOV, int IOS>
+void run_io() {
+    const int nblocks = 2048, wgs = 256, waves = 5;
+    unsigned long long* d_out;
+    int* d_sink;
+    (void)hipMalloc(&d_out, 8 * kMaxW * wgs);
+    (void)hipMalloc(&d_sink, 4 * 64 * kMaxW * wgs);
+    (void)hipFuncSetAttribute((const void*)micro<0, IOV, IOS>, hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(Sh));
+    for (int rep = 0; rep < 2; ++rep)
+        hipLaunchKernelGGL((micro<0, IOV, IOS>), dim3(wgs), dim3(64 * waves), sizeof(Sh), 0, nblocks, d_out, d_sink);
+    (void)hipDeviceSynchronize();
+    std::vector<unsigned long long> h(kMaxW * wgs);
+    (void)hipMemcpy(h.data(), d_out, 8 * kMaxW * wgs, hipMemcpyDeviceToHost);
+    std::vector<double> w0, w13, io;
+    for (int g = 0; g < wgs; ++g) {
+        w0.push_back((double)h[g * kMaxW] / (nblocks * 32.0));
+        for (int w = 1; w < 4; ++w) w13.push_back((double)h[g * kMaxW + w] / (nblocks * 32.0));
+        io.push_back((double)h[g * kMaxW + 4] * IOV / (nblocks * 32.0) / (h[g * kMaxW] / (nblocks * 32.0)));
+    }
+    std::sort(w0.begin(), w0.end());
+    std::sort(w13.begin(), w13.end());
+    std::sort(io.begin(), io.end());
+    printf("io VALU/pass %3d sleep %d: wave0 cyc/step %.2f, waves1-3 %.2f; io wave VALU per cycle %.3f "
+           "(%.2f per wave0 step)\n", IOV, IOS, w0[w0.size() / 2], w13[w13.size() / 2], io[io.size() / 2],
+           io[io.size() / 2] * w0[w0.size() / 2]);
+    (void)hipFree(d_out);
+    (void)hipFree(d_sink);
+}
+
 template <int V>
 void all() {
     run<V>(1, 1);
@@ -126,5 +179,10 @@ int main() {
     all<2>();
     all<3>();
     all<4>();
+    run_io<4, 1>();
+    run_io<16, 1>();
+    run_io<64, 1>();
+    run_io<16, 0>();
+    run_io<64, 0>();
     return 0;
 }
