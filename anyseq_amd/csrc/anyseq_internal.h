@@ -266,9 +266,10 @@ struct AffLevelTail {
 
 // Affine final level (aff_predwalk_kernel): blocks of at most `lds_rows` rows (the
 // launch's tallest block, at most kPredLdsMaxRows) keep their predecessor bytes (plus
-// a spare row for the walk's path record) and query rows in LDS ((rows + 128) x 128 +
-// rows bytes, <= 160 KiB); taller ones use an HBM slab.
-constexpr int kPredLdsMaxRows = 1140;
+// a spare row for the walk's path record), query rows and the two sweeping waves'
+// ring in LDS ((rows + 128) x 128 + rows + 1 KiB, <= 160 KiB); taller ones use an HBM
+// slab.
+constexpr int kPredLdsMaxRows = 1130;
 // the device final level's first launch: LDS slabs of up to this many rows (78 KB:
 // two workgroups per CU); taller blocks go to its second launch
 constexpr int kPredSmallRows = 480;
@@ -282,7 +283,7 @@ struct AffFinalPlan {
     uint32_t* err;         // set to 1 on a bad split table
     int nb, n, m, kind, small_rows;
 };
-inline int pred_lds_bytes(int rows) { return (rows + 128) * 128 + ((rows + 15) & ~15); }
+inline int pred_lds_bytes(int rows) { return (rows + 128) * 128 + ((rows + 15) & ~15) + 1024; }
 
 // Device-side error codes written to the error word.
 enum : uint32_t { ERR_NONE = 0, ERR_SPIN_TIMEOUT = 1, ERR_BAD_DESC = 0x100 };

@@ -846,7 +846,12 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             int lim = (int)min((uint32_t)nchunks, tl >= 0x7fffffffu ? (uint32_t)nchunks
                                                                      : tl + SCH - kMaxBack / CH - 1);
             lim = min(lim, s_next + 1024 / CH);   // one batch: 16 loads in flight per lane
-            if (lim > s_next) {
+            // whole batches only (or the last one, or when the skew front gets within 16
+            // chunks): a staging pass waits for its loads, and the trailing wave frees
+            // the ring one chunk per block -- staging every chunk put a load round trip
+            // into every pass, between this pass's hand-off poll and its consumption
+            const bool batch = lim - s_next >= 1024 / CH || lim >= nchunks || s_next < sk_next + 16;
+            if (lim > s_next && batch) {
                 const int c0 = s_next * CH;
                 uint8_t v[16];
 #pragma unroll
@@ -3002,6 +3007,139 @@ __device__ __forceinline__ int2 aff_pred_block(const BlockInfo& bi, QB qrow, con
     return aff_pred_sweep<true, false>(bi, qrow, S, pred, match, mismatch, go, ge);
 }
 
+// The same predecessors by TWO waves per block, one column per lane (wave w owns
+// columns 64w .. 64w+63): lane l of wave w computes row i = d - l at its step d, so
+// a wave sweeps h + 63 anti-diagonals of one cell per lane (the single-wave sweep
+// above: h + 127 of two cells).  Wave 1's lane 0 takes its left neighbour (H, E)
+// of row i from wave 0's lane 63 through a 128-entry LDS ring; wave 1 runs kSw2Lag
+// steps behind, and both waves meet at a barrier every kSw2Chunk steps, so a row is
+// in the ring (written at wave 0's step i + 63) a chunk before wave 1 reads it and
+// is overwritten (row i + 128) only after.  Same bytes, same exit cell.
+constexpr int kSw2Chunk = 16, kSw2Lag = 80;   // kSw2Lag >= 63 + kSw2Chunk, a multiple of it
+template <bool XFREE, bool XLOCAL>
+__device__ __forceinline__ int2 aff_pred_sweep2(const BlockInfo& bi, const uint8_t* qrow, const uint8_t* __restrict__ S,
+                                                uint8_t* pred, int2* ring, int match, int mismatch, int go, int ge) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int NEG = kAffNeg;
+    const int bm = bi.smode;
+    const bool clamp = bm == BM_FREE_LOCAL;
+    const int C = (bm == BM_EFREE || bm == BM_EPAID) ? NEG : 0;
+    const bool lnormal = bm == BM_NORMAL, lzero = bm == BM_FREE_LOCAL || bm == BM_FREE_SEMI_OPEN;
+    const bool xlastcol = bi.flags & 2;
+    const int h = bi.h, w = bi.w, goe = go + ge;
+    const int j = 64 * wv + lane;
+    const bool col = j < w;
+    const int sj = col ? (int)S[bi.oj + j] : 0x100;
+    // row -1: H(-1, j) = the top border, E = F = -inf; the diagonal of row 0: H(-1, j-1)
+    int Hc = aff_top_h(bm, j, go, ge), Ec = NEG, F = NEG;
+    int dH = j == 0 ? C : aff_top_h(bm, j - 1, go, ge);
+    int xv = -2147483647, xr = 0, cv = -2147483647, cr = 0;
+    const int nsteps = h + 63;
+    const int nchunks = (nsteps + kSw2Lag + kSw2Chunk - 1) / kSw2Chunk;
+    uint8_t* pw = pred + 64 * wv * 128 + j;   // + d * 128: anti-diagonal d + 64 wv
+    for (int c = 0; c < nchunks; ++c) {
+        const int d0 = c * kSw2Chunk - (wv ? kSw2Lag : 0);
+        if (d0 + kSw2Chunk > 0 && d0 < nsteps) {
+            int qn = (d0 - lane >= 0 && d0 - lane < h) ? (int)qrow[d0 - lane] : 0x200;
+            for (int k = 0; k < kSw2Chunk; ++k) {
+                const int d = d0 + k;
+                const int i = d - lane;
+                const int q = qn;
+                qn = (i + 1 >= 0 && i + 1 < h) ? (int)qrow[i + 1] : 0x200;
+                int lH, lE;
+                if (wv == 0) {
+                    // lane 0: the block's left border at row d (>= 0)
+                    const int lb = lnormal ? go + (d + 1) * ge : (lzero ? 0 : NEG);
+                    lH = wave_shr1(lb, Hc);
+                    lE = wave_shr1(NEG, Ec);
+                } else {
+                    const int2 r = ring[d & 127];   // (H, E) of (d, 63)
+                    lH = wave_shr1(r.x, Hc);
+                    lE = wave_shr1(r.y, Ec);
+                }
+                const bool act = col && (unsigned)i < (unsigned)h;
+                const int e1 = lE + ge, e2 = lH + goe;
+                const int e = e1 > e2 ? e1 : e2;
+                const int f1 = F + ge, f2 = Hc + goe;
+                const int f = f1 > f2 ? f1 : f2;
+                const int hd = dH + (q == sj ? match : mismatch);
+                int hh = hd, src = 0;
+                if (e > hh) { hh = e; src = 1; }
+                if (f > hh) { hh = f; src = 2; }
+                if (clamp && 0 > hh) { hh = 0; src = 3; }
+                pw[d * 128] = (uint8_t)(src | (e1 > e2 ? 4 : 0) | (f1 > f2 ? 8 : 0));
+                dH = lH;
+                Hc = act ? hh : Hc;
+                Ec = act ? e : Ec;
+                F = act ? f : F;
+                if (wv == 0 && lane == 63 && i >= 0) ring[i & 127] = make_int2(hh, e);
+                if constexpr (XFREE) {
+                    if constexpr (XLOCAL) {
+                        const bool u = act && hh > xv;
+                        xv = u ? hh : xv;
+                        xr = u ? i : xr;
+                    } else {
+                        xv = (act && i == h - 1) ? hh : xv;
+                        const bool u = xlastcol && act && j == w - 1 && hh > cv;
+                        cv = u ? hh : cv;
+                        cr = u ? i : cr;
+                    }
+                }
+                if (d + 1 >= nsteps) break;
+            }
+        }
+        __syncthreads();
+    }
+    if constexpr (XFREE) {
+        // first maximum over the block: larger value, then smaller row, then smaller column
+        int v = col ? xv : -2147483647, r = XLOCAL ? xr : h - 1, cc = j;
+        for (int o = 32; o >= 1; o >>= 1) {
+            const int v2 = __shfl_xor(v, o), r2 = __shfl_xor(r, o), c2 = __shfl_xor(cc, o);
+            if (v2 > v || (v2 == v && (r2 < r || (r2 == r && c2 < cc)))) {
+                v = v2;
+                r = r2;
+                cc = c2;
+            }
+        }
+        // across the two waves (the ring is free now), then the last column's first
+        // maximum if strictly greater (semiglobal)
+        int* red = reinterpret_cast<int*>(ring);
+        if (lane == 0) {
+            red[3 * wv] = v;
+            red[3 * wv + 1] = r;
+            red[3 * wv + 2] = cc;
+        }
+        if (!XLOCAL && xlastcol && j == w - 1) {
+            red[6] = cv;
+            red[7] = cr;
+        }
+        __syncthreads();
+        v = red[0];
+        r = red[1];
+        cc = red[2];
+        const int v2 = red[3], r2 = red[4], c2 = red[5];
+        if (v2 > v || (v2 == v && (r2 < r || (r2 == r && c2 < cc)))) {
+            v = v2;
+            r = r2;
+            cc = c2;
+        }
+        if (!XLOCAL && xlastcol && red[6] > v) {
+            r = red[7];
+            cc = w - 1;
+        }
+        __syncthreads();
+        return make_int2(r, cc);
+    }
+    return make_int2(0, 0);
+}
+
+__device__ __forceinline__ int2 aff_pred_block2(const BlockInfo& bi, const uint8_t* qrow, const uint8_t* __restrict__ S,
+                                                uint8_t* pred, int2* ring, int match, int mismatch, int go, int ge) {
+    if (bi.e_end != 2) return aff_pred_sweep2<false, false>(bi, qrow, S, pred, ring, match, mismatch, go, ge);
+    if (bi.flags & 1) return aff_pred_sweep2<true, true>(bi, qrow, S, pred, ring, match, mismatch, go, ge);
+    return aff_pred_sweep2<true, false>(bi, qrow, S, pred, ring, match, mismatch, go, ge);
+}
+
 // One thread: walk from the block's end (bottom-right in state H or E, or the
 // free exit cell x) back to its start (anchored: the corner through the border's
 // gap runs; free: a clamped cell or the border); sparse i+j+1 output.
@@ -3121,7 +3259,7 @@ __device__ __forceinline__ void aff_trace_out(const BlockInfo& bi, int2 r, const
                                               const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
                                               uint8_t* alq, uint8_t* als) {
     const int64_t base = (int64_t)bi.oi + bi.oj;
-    for (int p = r.x + (int)threadIdx.x; p <= r.y; p += 64) {
+    for (int p = r.x + (int)threadIdx.x; p <= r.y; p += blockDim.x) {
         const int t = *reinterpret_cast<const uint16_t*>(slab + p * 128 + 126);
         const int op = t & 3;
         if (op == 0) continue;
@@ -3131,13 +3269,14 @@ __device__ __forceinline__ void aff_trace_out(const BlockInfo& bi, int2 r, const
     }
 }
 
-// Final level, one wave per 128-column block: predecessors (aff_pred_block), then
-// the walk in the same launch.  A block of h <= lds_rows rows (the launch's tallest
+// Final level, one workgroup (two waves) per 128-column block: predecessors, then the
+// walk in the same launch.  A block of h <= lds_rows rows (the launch's tallest
 // block, capped at kPredLdsMaxRows) keeps its query rows and its (h + 127) x 128
 // predecessor bytes in LDS, so neither the sweep's query reads nor the walk's
-// dependent reads go to HBM, and the whole wave walks it (aff_walk_trace); taller
-// blocks (long vertical gaps) use the HBM slab at pred_base and lane 0's walk
-// (aff_walk_block).
+// dependent reads go to HBM: both waves sweep it (aff_pred_sweep2), wave 0 walks it
+// in lock step (aff_walk_trace), both write the symbols.  Taller blocks (long
+// vertical gaps) use the HBM slab at pred_base, wave 0's sweep (aff_pred_sweep) and
+// lane 0's walk (aff_walk_block).
 //
 // Launch modes: list == nullptr walks block blockIdx.x (defer: skips blocks taller than
 // lds_rows and those the path does not touch, flags bit 2 -- aff_final_blocks_kernel's
@@ -3147,7 +3286,7 @@ __device__ void aff_predwalk_one(BlockInfo* __restrict__ blocks, int b, const ui
                                  const uint8_t* __restrict__ S, uint8_t* __restrict__ pred, int match, int mismatch,
                                  int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows, uint8_t* pw_lds);
 
-__global__ __launch_bounds__(64) void aff_predwalk_kernel(BlockInfo* __restrict__ blocks, int nblocks,
+__global__ __launch_bounds__(128) void aff_predwalk_kernel(BlockInfo* __restrict__ blocks, int nblocks,
                                                           const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
                                                           uint8_t* __restrict__ pred, int match, int mismatch, int go,
                                                           int ge, uint8_t* alq, uint8_t* als, int lds_rows,
@@ -3170,6 +3309,12 @@ __global__ __launch_bounds__(64) void aff_predwalk_kernel(BlockInfo* __restrict_
     aff_predwalk_one(blocks, b, Q, S, pred, match, mismatch, go, ge, alq, als, lds_rows, pw_lds);
 }
 
+#ifdef ANYSEQ_PW_PHASES   // tools/micro/pw_micro.hip: each phase repeated to time it
+__device__ int g_pw_rep = 0;
+#define PW_REPS(bit) (1 + ((g_pw_rep >> (bit)) & 1))
+#else
+#define PW_REPS(bit) 1
+#endif
 __device__ void aff_predwalk_one(BlockInfo* __restrict__ blocks, int b, const uint8_t* __restrict__ Q,
                                  const uint8_t* __restrict__ S, uint8_t* __restrict__ pred, int match, int mismatch,
                                  int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows, uint8_t* pw_lds) {
@@ -3177,25 +3322,33 @@ __device__ void aff_predwalk_one(BlockInfo* __restrict__ blocks, int b, const ui
     if (bi.flags & 4) return;                 // the path does not touch the block
     if (bi.e_end == 2 && bi.h <= 0) return;   // the path ended at the block's corner
     int2 x = make_int2(0, 0);
-    if (bi.h >= 0 && bi.h <= lds_rows) {
-        uint8_t* qs = pw_lds + (lds_rows + 128) * 128;   // the slab (+ the spare row), then h query rows
+    if (bi.h <= lds_rows) {
+        // LDS: the slab (+ the spare row), the h query rows, the two waves' ring
+        uint8_t* qs = pw_lds + (lds_rows + 128) * 128;
+        int2* ring = reinterpret_cast<int2*>(qs + ((lds_rows + 15) & ~15));
         if (bi.h > 0) {
-            for (int i = threadIdx.x; i < bi.h; i += 64) qs[i] = Q[bi.oi + i];
+            for (int i = threadIdx.x; i < bi.h; i += blockDim.x) qs[i] = Q[bi.oi + i];
             __syncthreads();
-            x = aff_pred_block(bi, (const uint8_t*)qs, S, pw_lds, match, mismatch, go, ge);
+            for (int rep = 0; rep < PW_REPS(0); ++rep)
+                x = aff_pred_block2(bi, (const uint8_t*)qs, S, pw_lds, ring, match, mismatch, go, ge);
+        }
+        // wave 0 walks (the walk's dependent reads are all LDS: an HBM read per step
+        // would cost ~1 us), both waves write the symbols
+        for (int rep = 0; rep < PW_REPS(1); ++rep) {
+            if (threadIdx.x < 64) {
+                const int2 r = aff_walk_trace(bi, x, pw_lds);
+                if (threadIdx.x == 0) ring[0] = r;
+            }
             __syncthreads();
         }
-        // (the walk's dependent reads are all LDS: an HBM read per step would cost ~1 us)
-        const int2 r = aff_walk_trace(bi, x, pw_lds);
-        __syncthreads();
-        aff_trace_out(bi, r, pw_lds, Q, S, alq, als);
+        for (int rep = 0; rep < PW_REPS(2); ++rep) aff_trace_out(bi, ring[0], pw_lds, Q, S, alq, als);
     } else {
         uint8_t* slab = pred + bi.pred_base;
-        if (bi.h > 0) {
+        if (threadIdx.x < 64) {   // (one wave: the single-wave sweep, lane 0's walk)
             x = aff_pred_block(bi, Q + bi.oi, S, slab, match, mismatch, go, ge);
             __threadfence_block();
-            __syncthreads();
         }
+        __syncthreads();
         if (threadIdx.x == 0) aff_walk_block(bi, x, Q + bi.oi, S + bi.oj, (const uint8_t*)slab, alq, als);
     }
     if (threadIdx.x == 0 && bi.e_end == 2) {
@@ -3660,14 +3813,15 @@ hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* 
         if (e != hipSuccess) return e;
         attr_set = 1;
     }
-    hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(nblocks), dim3(64), bytes, st, (anyseq::BlockInfo*)blocks,
+    hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(nblocks), dim3(128), bytes, st, (anyseq::BlockInfo*)blocks,
                        nblocks, Q, S, pred, match, mismatch, go, ge, alq, als, lds_rows, nullptr, 0);
     return hipGetLastError();
 }
 
 // Device-planned final level: the block table (aff_final_blocks_kernel), the blocks of
 // at most small_rows rows (one workgroup each, LDS slabs of small_rows rows), then the
-// taller ones from the list (at most 256 workgroups, the largest LDS slab or HBM).
+// taller ones from the list (32 workgroups in turn -- tall blocks are rare, and an
+// empty list costs little more than the launch -- the largest LDS slab or HBM).
 hipError_t anyseq_launch_aff_final(const anyseq::AffFinalPlan* plan, const uint8_t* Q, const uint8_t* S,
                                    uint8_t* pred, int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als,
                                    hipStream_t st) {
@@ -3682,9 +3836,9 @@ hipError_t anyseq_launch_aff_final(const anyseq::AffFinalPlan* plan, const uint8
         attr_set = 1;
     }
     hipLaunchKernelGGL(anyseq::aff_final_blocks_kernel, dim3(1), dim3(1024), 0, st, a);
-    hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(a.nb), dim3(64), anyseq::pred_lds_bytes(a.small_rows), st,
+    hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(a.nb), dim3(128), anyseq::pred_lds_bytes(a.small_rows), st,
                        a.blocks, a.nb, Q, S, pred, match, mismatch, go, ge, alq, als, a.small_rows, nullptr, 1);
-    hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(std::min(a.nb, 256)), dim3(64),
+    hipLaunchKernelGGL(anyseq::aff_predwalk_kernel, dim3(std::min(a.nb, 32)), dim3(128),
                        anyseq::pred_lds_bytes(anyseq::kPredLdsMaxRows), st, a.blocks, a.nb, Q, S, pred, match,
                        mismatch, go, ge, alq, als, anyseq::kPredLdsMaxRows, a.tall, 0);
     return hipGetLastError();
