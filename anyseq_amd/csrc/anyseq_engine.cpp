@@ -302,6 +302,7 @@ void init_tuning_locked() {
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
+    g_tuning.io_stage = env_int("ANYSEQ_IO_STAGE", g_tuning.io_stage);
     g_tuning.virtbest = env_int("ANYSEQ_VIRT_BEST", g_tuning.virtbest);
     g_tuning.devplan = env_int("ANYSEQ_AFF_DEVPLAN", g_tuning.devplan);
     g_tuning.devfinal = env_int("ANYSEQ_AFF_DEVFINAL", g_tuning.devfinal);
@@ -716,6 +717,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     // -1 border cells, at most go + ge, never exceed cell (0,0) >= min(match, mismatch))
     if (g_tuning.virtbest && std::min(sc.match, sc.mismatch) >= sc.gap_open + sc.gap_extend) fp.pad |= 16;
     fp.alpha = nullptr;
+    fp.io_stage = g_tuning.io_stage;
     return fp;
 }
 
@@ -2069,6 +2071,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "throttle") g_tuning.thr = value;
     else if (n == "affine_lut") g_tuning.afflut = value;
     else if (n == "slack") g_tuning.slack = value;
+    else if (n == "io_stage") g_tuning.io_stage = value;
     else if (n == "virtual_best") g_tuning.virtbest = value;
     else if (n == "affine_device_plan") g_tuning.devplan = value;
     else if (n == "affine_device_final") g_tuning.devfinal = value;

@@ -91,6 +91,7 @@ struct Tuning {
     int thr = 0;         // band 0 of every problem sleeps thr s_sleep-1 units per block (chain pace)
     int afflut = 1;      // affine fill: v_perm weight table when the pair has <= 8 symbols
     int slack = 0;       // affine fill: half chunks a band starts behind the structural minimum
+    int io_stage = 3;    // affine fill: the I/O wave's subject staging mode (io_wave; 0..3, r04o A/B)
     int devplan = 1;     // affine construct: Hirschberg levels planned on the device (one download)
     int devfinal = 1;    // affine construct, device-planned: the final level's blocks built on the device too
     int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe

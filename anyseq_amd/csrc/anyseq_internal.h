@@ -134,6 +134,7 @@ struct FillParams {
     const int32_t* alpha;
     int32_t lut_ok;
     int32_t slack;                    // affine: blocks a band starts behind the structural minimum (>= 0)
+    int32_t io_stage;                 // affine I/O wave: subject staging mode (io_wave)
 };
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).

@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "anyseq_internal.h"
 
@@ -803,7 +804,7 @@ template <int CH, bool SKEW, typename T = int32_t>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
                         uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
                         uint32_t* cons0, uint32_t* err, bool reset_in = false, int ext = 0, int pscale = 1,
-                        bool hprio = false, unsigned long long* evp = nullptr) {
+                        bool hprio = false, unsigned long long* evp = nullptr, int io_stage = 3) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
     constexpr int GR = 16;             // hand-off poll granule (columns)
@@ -817,13 +818,15 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
     const bool need_in = g_in != nullptr;
     const GLOBAL_AS uint8_t* sg = gmem(s);
     int s_next = 0, sk_next = 0, in_gran = 0;
+    int st_lim = 0;   // subject chunks whose loads are issued (s_next: stored in the ring)
+    uint8_t sv[4];    // the loaded, not yet stored subject bytes (4 x 64 columns)
     uint32_t idle = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     while (s_next < nchunks || (SKEW && sk_next < nskew) || (need_in && in_gran < ngran)) {
         bool progress = false;
         // The hand-off poll goes out first (the band chain waits on it): 128 columns from
-        // the first granule not yet in, consumed after this iteration's staging work, so
-        // the load's round trip overlaps it.  The previous group's last band stores its
+        // the first granule not yet in, consumed after this iteration's skew work, so the
+        // load's round trip overlaps it.  The previous group's last band stores its
         // bottom row straight into g_in (sc1), which the host filled with the sentinel
         // (never a kernel value): a granule is in when none of its columns < w holds it.
         T pv[2];
@@ -840,19 +843,42 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                 pv[i] = col < plim * GR && col < w ? HandOff<T>::load(g_in + col) : HandOff<T>::zero();
             }
         }
-        if (s_next < nchunks) {
+        // Subject staging (io_stage, FillParams::io_stage):
+        //  0: whatever chunks the trailing wave has freed, loaded and stored in the same
+        //     pass (a load round trip in nearly every pass, between the hand-off poll's
+        //     issue and its consumption);
+        //  1: the same in whole 1024-column batches (a round trip every 32 blocks);
+        //  2: asynchronous -- a pass stores the bytes the previous pass loaded (up to 256
+        //     columns) and issues the next loads, here, before the skew work;
+        //  3: as 2, after the poll's consumption (the poll's wait never covers a younger
+        //     staging load).
+        // The first batch (up to 1024 columns) always waits for its loads.
+        auto stage = [&]() {
+            if (io_stage >= 2 && st_lim > s_next) {   // (loaded by the previous pass)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int c = s_next * CH + i * 64 + lane;
+                    if (c < st_lim * CH) {
+                        const int p = c & (kSRing - 1);
+                        s_ring[p] = sv[i];
+                        if (p < 64) s_ring[p + kSRing] = sv[i];
+                    }
+                }
+                if (!SKEW) lds_st(s_filled, (uint32_t)st_lim);
+                s_next = st_lim;
+                progress = true;
+            }
+            if (st_lim >= nchunks) return;
             const uint32_t tl = lds_ld(tail);
             // the trailing wave in block `tl` still reads columns >= tl*CH - kMaxBack
             int lim = (int)min((uint32_t)nchunks, tl >= 0x7fffffffu ? (uint32_t)nchunks
                                                                      : tl + SCH - kMaxBack / CH - 1);
-            lim = min(lim, s_next + 1024 / CH);   // one batch: 16 loads in flight per lane
-            // whole batches only (or the last one, or when the skew front gets within 16
-            // chunks): a staging pass waits for its loads, and the trailing wave frees
-            // the ring one chunk per block -- staging every chunk put a load round trip
-            // into every pass, between this pass's hand-off poll and its consumption
-            const bool batch = lim - s_next >= 1024 / CH || lim >= nchunks || s_next < sk_next + 16;
-            if (lim > s_next && batch) {
-                const int c0 = s_next * CH;
+            if (st_lim == 0 || io_stage < 2) {
+                lim = min(lim, st_lim + 1024 / CH);   // one batch: 16 loads in flight per lane
+                const bool go_ = st_lim == 0 || io_stage == 0 || lim - st_lim >= 1024 / CH || lim >= nchunks ||
+                                 st_lim < sk_next + 16;
+                if (lim <= st_lim || !go_) return;
+                const int c0 = st_lim * CH;
                 uint8_t v[16];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -869,10 +895,21 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                     }
                 }
                 if (!SKEW) lds_st(s_filled, (uint32_t)lim);
-                s_next = lim;
+                s_next = st_lim = lim;
                 progress = true;
+            } else {
+                lim = min(lim, st_lim + 256 / CH);
+                if (lim >= st_lim + 2 || (lim >= nchunks && lim > st_lim)) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int c = st_lim * CH + i * 64 + lane;
+                        sv[i] = (c < w && c < lim * CH) ? sg[s_off + s_step * c] : (uint8_t)0;
+                    }
+                    st_lim = lim;
+                }
             }
-        }
+        };
+        if (io_stage < 3) stage();
         const int sk_avail = s_next >= nchunks ? nskew : s_next;
         if (SKEW && sk_next < sk_avail) {
             // skewed copy of block b needs raw columns 32b-64 .. 32b+31 (staged: b < s_next)
@@ -959,6 +996,7 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             }
             if (hprio) __builtin_amdgcn_s_setprio(0);
         }
+        if (io_stage == 3) stage();
         if (!progress) {
             __builtin_amdgcn_s_sleep(kIoSleep);
             if ((++idle & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t_start > SPIN_TICKS || err_set(err))) {
@@ -1847,7 +1885,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                                     &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
                                     P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc, 2, 2, fp.prio == 3,
                                     fp.dbg && first < 2048 ? fp.dbg + 16 + 4 * 4096 + 16 * (first + (P.q_step < 0 ? 2048 : 0))
-                                                           : nullptr);
+                                                           : nullptr,
+                                    fp.io_stage);
         } else {
             const int band = first + wave;
             if (band <= last) {
@@ -2547,7 +2586,7 @@ __device__ AffHalfGeo aff_half_geo(const AffLevelPlan& a, int len, int width) {
     return g;
 }
 
-// block-wide exclusive scan (1024 threads) of one 64-bit value; returns the prefix,
+// block-wide exclusive scan (64 .. 1024 threads) of one 64-bit value; returns the prefix,
 // *total the tile's sum
 __device__ int64_t block_scan_excl(int64_t v, int64_t* sh, int64_t* total) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2561,7 +2600,7 @@ __device__ int64_t block_scan_excl(int64_t v, int64_t* sh, int64_t* total) {
     __syncthreads();
     if (tid == 0) {
         int64_t acc = 0;
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
             const int64_t t = sh[i];
             sh[i] = acc;
             acc += t;
@@ -2588,7 +2627,7 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
     const bool stop = a.score && a.kind != KIND_GLOBAL && *a.score <= 0;
     RowToCol* jobs = a.jobs;
     int64_t rb_base = 0, rp_base = 0;
-    for (int t0 = 0; t0 < a.parts; t0 += 1024) {
+    for (int t0 = 0; t0 < a.parts; t0 += blockDim.x) {
         const int p = t0 + (int)threadIdx.x;
         PartInfo pi{};
         AffHalfGeo gl{}, gr{};
@@ -2713,8 +2752,9 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
 __global__ __launch_bounds__(1024) void aff_level_plan_kernel(const AffLevelPlan a) { aff_level_plan_body(a); }
 
 constexpr int kTailStage = 8192;   // partials staged in LDS per chunk of parts (64 KiB)
-__global__ __launch_bounds__(1024) void aff_level_tail_kernel(const AffLevelTail t) {
-    __shared__ int sv[1024], sk[1024];
+constexpr int kTailThreads = 1024;   // (16 waves: a join thread loads at most 4 rows of a 4096-row slice)
+__global__ __launch_bounds__(kTailThreads) void aff_level_tail_kernel(const AffLevelTail t) {
+    __shared__ int sv[kTailThreads / 64], sk[kTailThreads / 64];
     __shared__ int last;
     const int nj = t.nslices * t.nparts;
     const int b = blockIdx.x;
@@ -2789,20 +2829,27 @@ __global__ __launch_bounds__(1024) void aff_level_tail_kernel(const AffLevelTail
                 }
             }
         }
-        sv[threadIdx.x] = best;
-        sk[threadIdx.x] = key;
-        __syncthreads();
-        for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-            if ((int)threadIdx.x < o) {
-                const int v2 = sv[threadIdx.x + o], k2 = sk[threadIdx.x + o];
-                if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && k2 < sk[threadIdx.x])) {
-                    sv[threadIdx.x] = v2;
-                    sk[threadIdx.x] = k2;
-                }
+        // the first maximum (larger value, then smaller key): lanes, then the waves
+        for (int o = 32; o >= 1; o >>= 1) {
+            const int v2 = __shfl_xor(best, o), k2 = __shfl_xor(key, o);
+            if (v2 > best || (v2 == best && k2 < key)) {
+                best = v2;
+                key = k2;
             }
-            __syncthreads();
         }
-        if (threadIdx.x == 0) HandOff<int2>::store(partial + (size_t)part * t.nslices + slice, make_int2(sv[0], sk[0]));
+        if ((threadIdx.x & 63) == 0) {
+            sv[threadIdx.x >> 6] = best;
+            sk[threadIdx.x >> 6] = key;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int wv = 1; wv < (int)(blockDim.x >> 6); ++wv)
+                if (sv[wv] > best || (sv[wv] == best && sk[wv] < key)) {
+                    best = sv[wv];
+                    key = sk[wv];
+                }
+            HandOff<int2>::store(partial + (size_t)part * t.nslices + slice, make_int2(best, key));
+        }
     }
     // the last workgroup to finish
     __syncthreads();
@@ -3019,7 +3066,9 @@ constexpr int kSw2Chunk = 16, kSw2Lag = 80;   // kSw2Lag >= 63 + kSw2Chunk, a mu
 template <bool XFREE, bool XLOCAL>
 __device__ __forceinline__ int2 aff_pred_sweep2(const BlockInfo& bi, const uint8_t* qrow, const uint8_t* __restrict__ S,
                                                 uint8_t* pred, int2* ring, int match, int mismatch, int go, int ge) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // (readfirstlane: the wave index is uniform, and the compiler must know it -- else
+    // every branch on it, and on the chunk's step range, juggles exec masks)
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int NEG = kAffNeg;
     const int bm = bi.smode;
     const bool clamp = bm == BM_FREE_LOCAL;
@@ -3037,55 +3086,89 @@ __device__ __forceinline__ int2 aff_pred_sweep2(const BlockInfo& bi, const uint8
     const int nsteps = h + 63;
     const int nchunks = (nsteps + kSw2Lag + kSw2Chunk - 1) / kSw2Chunk;
     uint8_t* pw = pred + 64 * wv * 128 + j;   // + d * 128: anti-diagonal d + 64 wv
+    // one chunk of a wave's steps, specialised per wave and per clamp (no per-step branch
+    // on either)
+    auto chunk = [&](auto wv_c, auto clamp_c, int d0) {
+        constexpr int WV = decltype(wv_c)::value;
+        constexpr bool CL = decltype(clamp_c)::value;
+        // the chunk's LDS reads up front, one wait: the query bytes of the lane's 16 rows,
+        // wave 1's 16 left neighbours from the ring (a step that waits for an LDS read
+        // every step ran at ~550 cycles)
+        int qk[kSw2Chunk];
+        int2 rk[kSw2Chunk];
+#pragma unroll
+        for (int k = 0; k < kSw2Chunk; ++k) {   // (unconditional reads: one wait)
+            const int i = d0 + k - lane;
+            qk[k] = qrow[min(max(i, 0), h - 1)];
+        }
+#pragma unroll
+        for (int k = 0; k < kSw2Chunk; ++k) {
+            const int i = d0 + k - lane;
+            qk[k] = (i >= 0 && i < h) ? qk[k] : 0x200;
+        }
+        if constexpr (WV == 1) {
+#pragma unroll
+            for (int k = 0; k < kSw2Chunk; ++k) rk[k] = ring[(d0 + k) & 127];   // (H, E) of (d, 63)
+        }
+#pragma unroll
+        for (int k = 0; k < kSw2Chunk; ++k) {
+            const int d = d0 + k;
+            if (d >= nsteps) continue;   // (uniform; not a break: the loop stays unrolled)
+            const int i = d - lane;
+            int lH, lE;
+            if constexpr (WV == 0) {
+                // lane 0: the block's left border at row d (>= 0)
+                const int lb = lnormal ? go + (d + 1) * ge : (lzero ? 0 : NEG);
+                lH = wave_shr1(lb, Hc);
+                lE = wave_shr1(NEG, Ec);
+            } else {
+                lH = wave_shr1(rk[k].x, Hc);
+                lE = wave_shr1(rk[k].y, Ec);
+            }
+            const bool act = col && (unsigned)i < (unsigned)h;
+            const int e1 = lE + ge, e2 = lH + goe;
+            const int e = e1 > e2 ? e1 : e2;
+            const int f1 = F + ge, f2 = Hc + goe;
+            const int f = f1 > f2 ? f1 : f2;
+            const int hd = dH + (qk[k] == sj ? match : mismatch);
+            int hh = hd, src = 0;
+            if (e > hh) { hh = e; src = 1; }
+            if (f > hh) { hh = f; src = 2; }
+            if (CL && 0 > hh) { hh = 0; src = 3; }
+            pw[d * 128] = (uint8_t)(src | (e1 > e2 ? 4 : 0) | (f1 > f2 ? 8 : 0));
+            dH = lH;
+            Hc = act ? hh : Hc;
+            Ec = act ? e : Ec;
+            F = act ? f : F;
+            if constexpr (WV == 0)
+                if (lane == 63 && i >= 0) ring[i & 127] = make_int2(hh, e);
+            if constexpr (XFREE) {
+                if constexpr (XLOCAL) {
+                    const bool u = act && hh > xv;
+                    xv = u ? hh : xv;
+                    xr = u ? i : xr;
+                } else {
+                    xv = (act && i == h - 1) ? hh : xv;
+                    const bool u = xlastcol && act && j == w - 1 && hh > cv;
+                    cv = u ? hh : cv;
+                    cr = u ? i : cr;
+                }
+            }
+        }
+    };
+    using W0 = std::integral_constant<int, 0>;
+    using W1 = std::integral_constant<int, 1>;
+    using CT = std::integral_constant<bool, true>;
+    using CF = std::integral_constant<bool, false>;
     for (int c = 0; c < nchunks; ++c) {
         const int d0 = c * kSw2Chunk - (wv ? kSw2Lag : 0);
-        if (d0 + kSw2Chunk > 0 && d0 < nsteps) {
-            int qn = (d0 - lane >= 0 && d0 - lane < h) ? (int)qrow[d0 - lane] : 0x200;
-            for (int k = 0; k < kSw2Chunk; ++k) {
-                const int d = d0 + k;
-                const int i = d - lane;
-                const int q = qn;
-                qn = (i + 1 >= 0 && i + 1 < h) ? (int)qrow[i + 1] : 0x200;
-                int lH, lE;
-                if (wv == 0) {
-                    // lane 0: the block's left border at row d (>= 0)
-                    const int lb = lnormal ? go + (d + 1) * ge : (lzero ? 0 : NEG);
-                    lH = wave_shr1(lb, Hc);
-                    lE = wave_shr1(NEG, Ec);
-                } else {
-                    const int2 r = ring[d & 127];   // (H, E) of (d, 63)
-                    lH = wave_shr1(r.x, Hc);
-                    lE = wave_shr1(r.y, Ec);
-                }
-                const bool act = col && (unsigned)i < (unsigned)h;
-                const int e1 = lE + ge, e2 = lH + goe;
-                const int e = e1 > e2 ? e1 : e2;
-                const int f1 = F + ge, f2 = Hc + goe;
-                const int f = f1 > f2 ? f1 : f2;
-                const int hd = dH + (q == sj ? match : mismatch);
-                int hh = hd, src = 0;
-                if (e > hh) { hh = e; src = 1; }
-                if (f > hh) { hh = f; src = 2; }
-                if (clamp && 0 > hh) { hh = 0; src = 3; }
-                pw[d * 128] = (uint8_t)(src | (e1 > e2 ? 4 : 0) | (f1 > f2 ? 8 : 0));
-                dH = lH;
-                Hc = act ? hh : Hc;
-                Ec = act ? e : Ec;
-                F = act ? f : F;
-                if (wv == 0 && lane == 63 && i >= 0) ring[i & 127] = make_int2(hh, e);
-                if constexpr (XFREE) {
-                    if constexpr (XLOCAL) {
-                        const bool u = act && hh > xv;
-                        xv = u ? hh : xv;
-                        xr = u ? i : xr;
-                    } else {
-                        xv = (act && i == h - 1) ? hh : xv;
-                        const bool u = xlastcol && act && j == w - 1 && hh > cv;
-                        cv = u ? hh : cv;
-                        cr = u ? i : cr;
-                    }
-                }
-                if (d + 1 >= nsteps) break;
+        if (d0 >= 0 && d0 < nsteps) {   // (d0 is a multiple of the chunk)
+            if (wv == 0) {
+                if (clamp) chunk(W0{}, CT{}, d0);
+                else chunk(W0{}, CF{}, d0);
+            } else {
+                if (clamp) chunk(W1{}, CT{}, d0);
+                else chunk(W1{}, CF{}, d0);
             }
         }
         __syncthreads();
@@ -3212,43 +3295,36 @@ __device__ __forceinline__ int2 aff_walk_trace(const BlockInfo& bi, int2 x, uint
     auto rec = [&](int p, int ii, int op) {
         *reinterpret_cast<uint16_t*>(slab + p * 128 + 126) = (uint16_t)(((ii + 1) << 2) | op);
     };
-    while (i >= 0 || j >= 0) {
+    // inside the block: one move per iteration, branch-free on scalars.  The cell's
+    // source `eff` (0 diagonal, 1 E, 2 F, 3 clamped) is its H source in state H, else
+    // the state; a gap move takes the next state from the same byte (bit 2 E extends,
+    // bit 3 F extends: (pb >> (eff + 1)) & 1), as two iterations of the reference walk
+    // do (the state switch, then the move)
+    bool stop = false;
+    while (i >= 0 && j >= 0) {
         const int p = i + j + 1;
-        if (i < 0 || j < 0) {
-            if (free_start) break;   // the path starts on the border
-            if (i < 0) {
-                rec(p, i, 2);
-                --j;
-            } else {
-                rec(p, i, 3);
-                --i;
-            }
-            lo = p;
-            continue;
-        }
         const int pb = __builtin_amdgcn_readfirstlane((int)slab[(i + j) * 128 + j]);
-        if (st == 0) {
-            const int hs = pb & 3;
-            if (hs == 3) break;   // clamped: the path starts after this cell
-            if (hs == 0) {
-                rec(p, i, 1);
-                rec(p - 1, 0, 0);
-                lo = p - 1;
-                --i;
-                --j;
-            } else {
-                st = hs;
-            }
-        } else if (st == 1) {
-            rec(p, i, 2);
-            lo = p;
-            st = (pb & 4) ? 1 : 0;
-            --j;
-        } else {
-            rec(p, i, 3);
-            lo = p;
-            st = (pb & 8) ? 2 : 0;
-            --i;
+        const int eff = st ? st : (pb & 3);
+        if (eff == 3) {   // clamped: the path starts after this cell
+            stop = true;
+            break;
+        }
+        rec(p, i, eff + 1);
+        if (eff == 0) rec(p - 1, 0, 0);
+        lo = eff == 0 ? p - 1 : p;
+        st = ((pb >> (eff + 1)) & 1) * eff;
+        i -= eff != 1;
+        j -= eff != 2;
+    }
+    // on the border (anchored starts): the rest of the row above, or of the column left
+    if (!stop && !free_start) {
+        for (; i < 0 && j >= 0; --j) {
+            rec(j, -1, 2);
+            lo = j;
+        }
+        for (; j < 0 && i >= 0; --i) {
+            rec(i, i, 3);
+            lo = i;
         }
     }
     return make_int2(lo, hi);
@@ -3282,9 +3358,10 @@ __device__ __forceinline__ void aff_trace_out(const BlockInfo& bi, int2 r, const
 // lds_rows and those the path does not touch, flags bit 2 -- aff_final_blocks_kernel's
 // table); else the workgroups walk the blocks list[1 .. list[0]] in turn (the tall
 // blocks deferred by the first launch).
-__device__ void aff_predwalk_one(BlockInfo* __restrict__ blocks, int b, const uint8_t* __restrict__ Q,
-                                 const uint8_t* __restrict__ S, uint8_t* __restrict__ pred, int match, int mismatch,
-                                 int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows, uint8_t* pw_lds);
+__device__ __forceinline__ void aff_predwalk_one(BlockInfo* __restrict__ blocks, int b, const uint8_t* __restrict__ Q,
+                                                 const uint8_t* __restrict__ S, uint8_t* __restrict__ pred, int match,
+                                                 int mismatch, int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows,
+                                                 uint8_t* pw_lds);
 
 __global__ __launch_bounds__(128) void aff_predwalk_kernel(BlockInfo* __restrict__ blocks, int nblocks,
                                                           const uint8_t* __restrict__ Q, const uint8_t* __restrict__ S,
@@ -3315,9 +3392,10 @@ __device__ int g_pw_rep = 0;
 #else
 #define PW_REPS(bit) 1
 #endif
-__device__ void aff_predwalk_one(BlockInfo* __restrict__ blocks, int b, const uint8_t* __restrict__ Q,
-                                 const uint8_t* __restrict__ S, uint8_t* __restrict__ pred, int match, int mismatch,
-                                 int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows, uint8_t* pw_lds) {
+__device__ __forceinline__ void aff_predwalk_one(BlockInfo* __restrict__ blocks, int b, const uint8_t* __restrict__ Q,
+                                                 const uint8_t* __restrict__ S, uint8_t* __restrict__ pred, int match,
+                                                 int mismatch, int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows,
+                                                 uint8_t* pw_lds) {
     const BlockInfo bi = blocks[b];
     if (bi.flags & 4) return;                 // the path does not touch the block
     if (bi.e_end == 2 && bi.h <= 0) return;   // the path ended at the block's corner
@@ -3789,7 +3867,7 @@ hipError_t anyseq_launch_rows_check(const void* rows, size_t nwords, uint32_t se
 hipError_t anyseq_launch_aff_level_tail(const void* tail, int fill_groups, hipStream_t st) {
     const anyseq::AffLevelTail& t = *(const anyseq::AffLevelTail*)tail;
     const int grid = std::max(std::max(1, t.nslices * t.nparts), t.has_next ? fill_groups : 1);
-    hipLaunchKernelGGL(anyseq::aff_level_tail_kernel, dim3(grid), dim3(1024), 0, st, t);
+    hipLaunchKernelGGL(anyseq::aff_level_tail_kernel, dim3(grid), dim3(anyseq::kTailThreads), 0, st, t);
     return hipGetLastError();
 }
 

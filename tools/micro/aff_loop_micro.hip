@@ -99,6 +99,13 @@ __global__ __launch_bounds__(512) void micro(int nblocks, unsigned long long* ou
     if (lane == 0) out[blockIdx.x * kMaxW + wave] = c1 - c0;
 }
 
+// Which SIMD each wave of a 5-wave workgroup runs on (HW_ID bits 5:4): the fill's I/O wave
+// is wave 4 of 5.
+__global__ void simd_ids(unsigned* out) {
+    const unsigned id = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));   // HW_REG_HW_ID, 32 bits
+    if ((threadIdx.x & 63) == 0) out[blockIdx.x * 8 + (threadIdx.x >> 6)] = id;
+}
+
 static const char* kNames[] = {"L lds-pub lut", "L no-pub lut", "G lds-pub lut", "G no-pub lut", "L lds-pub cmp"};
 
 template <int V>
@@ -174,6 +181,19 @@ void all() {
 }
 
 int main() {
+    {
+        unsigned* d;
+        (void)hipMalloc(&d, 8 * 4 * 256);
+        hipLaunchKernelGGL(simd_ids, dim3(256), dim3(320), 0, 0, d);
+        std::vector<unsigned> h(8 * 256);
+        (void)hipMemcpy(h.data(), d, 8 * 4 * 256, hipMemcpyDeviceToHost);
+        for (int g = 0; g < 4; ++g) {
+            printf("WG %d (5 waves): SIMD of waves 0..4:", g);
+            for (int w = 0; w < 5; ++w) printf(" %u", (h[g * 8 + w] >> 4) & 3);
+            printf("\n");
+        }
+        (void)hipFree(d);
+    }
     all<0>();
     all<1>();
     all<2>();
