@@ -303,6 +303,7 @@ void init_tuning_locked() {
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
     g_tuning.io_stage = env_int("ANYSEQ_IO_STAGE", g_tuning.io_stage);
+    g_tuning.io_skew = env_int("ANYSEQ_IO_SKEW", g_tuning.io_skew);
     g_tuning.virtbest = env_int("ANYSEQ_VIRT_BEST", g_tuning.virtbest);
     g_tuning.devplan = env_int("ANYSEQ_AFF_DEVPLAN", g_tuning.devplan);
     g_tuning.devfinal = env_int("ANYSEQ_AFF_DEVFINAL", g_tuning.devfinal);
@@ -514,7 +515,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
                                      rowbuf_ints * 4, aff ? 0x80808080u : 0xffffffffu, pin + 64, meta + zb, ub, st));
     FillParams fpl = fp;
     fpl.epoch = epoch;
-    fpl.prio = g_tuning.prio;
+    fpl.prio = fill_prio(aff);
     fpl.throttle = g_tuning.thr;
     fpl.slack = g_tuning.slack;
     unsigned long long* dbg = nullptr;
@@ -718,6 +719,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     if (g_tuning.virtbest && std::min(sc.match, sc.mismatch) >= sc.gap_open + sc.gap_extend) fp.pad |= 16;
     fp.alpha = nullptr;
     fp.io_stage = g_tuning.io_stage;
+    fp.io_skew = g_tuning.io_skew;
     return fp;
 }
 
@@ -1377,7 +1379,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             GroupRef* d_groups = A.groups;
             FillParams fpl = fp;
             fpl.epoch = epochs[li];
-            fpl.prio = g_tuning.prio;
+            fpl.prio = fill_prio(true);
             fpl.throttle = g_tuning.thr;
             fpl.slack = g_tuning.slack;
             fpl.dbg = nullptr;
@@ -2072,6 +2074,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_lut") g_tuning.afflut = value;
     else if (n == "slack") g_tuning.slack = value;
     else if (n == "io_stage") g_tuning.io_stage = value;
+    else if (n == "io_skew") g_tuning.io_skew = value;
     else if (n == "virtual_best") g_tuning.virtbest = value;
     else if (n == "affine_device_plan") g_tuning.devplan = value;
     else if (n == "affine_device_final") g_tuning.devfinal = value;

@@ -87,11 +87,13 @@ struct Tuning {
     int affasm = 1;  // affine fill: bit 0 asm steady state; bit 1 no asm epilogue; bits 2/3 none for best-all / other
     int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
     int afft = 1;        // affine construct: run Hirschberg halves taller than wide transposed
-    int prio = 0;        // 1: compute waves at s_setprio 3; 2: the I/O wave at 3; 3: its hand-off step at 3
+    int prio = -1;       // 1: compute waves at s_setprio 3; 2: the I/O wave at 3; 3: its hand-off step at 3;
+                         // -1: per kind (affine 1, r04p A/B: +1.5-2 %; linear 0)
     int thr = 0;         // band 0 of every problem sleeps thr s_sleep-1 units per block (chain pace)
     int afflut = 1;      // affine fill: v_perm weight table when the pair has <= 8 symbols
     int slack = 0;       // affine fill: half chunks a band starts behind the structural minimum
     int io_stage = 3;    // affine fill: the I/O wave's subject staging mode (io_wave; 0..3, r04o A/B)
+    int io_skew = 0;     // affine fill: the I/O wave's skewed blocks per pass while a poll is out (0: 8)
     int devplan = 1;     // affine construct: Hirschberg levels planned on the device (one download)
     int devfinal = 1;    // affine construct, device-planned: the final level's blocks built on the device too
     int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe
@@ -167,6 +169,8 @@ Engine& engine();
 int rows_per_lane();
 int waves_per_group();
 int aff_waves_per_group();
+// the issue-priority mode of a fill launch (g_tuning.prio, per kind when -1)
+inline int fill_prio(bool affine) { return g_tuning.prio >= 0 ? g_tuning.prio : (affine ? 1 : 0); }
 int aff_waves_for(int64_t chain_steps, int64_t wave_steps, int grid);
 
 FillParams make_params(int kind, const anyseq_scoring& sc);

@@ -135,6 +135,7 @@ struct FillParams {
     int32_t lut_ok;
     int32_t slack;                    // affine: blocks a band starts behind the structural minimum (>= 0)
     int32_t io_stage;                 // affine I/O wave: subject staging mode (io_wave)
+    int32_t io_skew;                  // affine I/O wave: skewed blocks per pass while a poll is out (0: 8)
 };
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).

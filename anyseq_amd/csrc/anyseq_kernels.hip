@@ -804,7 +804,8 @@ template <int CH, bool SKEW, typename T = int32_t>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
                         uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
                         uint32_t* cons0, uint32_t* err, bool reset_in = false, int ext = 0, int pscale = 1,
-                        bool hprio = false, unsigned long long* evp = nullptr, int io_stage = 3) {
+                        bool hprio = false, unsigned long long* evp = nullptr, int io_stage = 3,
+                        int io_skew = kIoSkewPolling) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
     constexpr int GR = 16;             // hand-off poll granule (columns)
@@ -916,7 +917,7 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             // and a free slot: the trailing wave has finished block b - kSkewBlocks
             const uint32_t tl = lds_ld(tail);
             int lim = min(sk_avail, tl >= 0x7fffffffu ? nskew : (int)tl + kSkewBlocks);
-            lim = min(lim, sk_next + (plim > in_gran ? kIoSkewPolling : 8));
+            lim = min(lim, sk_next + (plim > in_gran ? io_skew : 8));
             for (int b = sk_next; b < lim; ++b) {
                 uint32_t d[8];
                 load_sbytes<32>(s_ring, (32 * b - 1 - lane) & (kSRing - 1), d);
@@ -1886,7 +1887,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                                     P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc, 2, 2, fp.prio == 3,
                                     fp.dbg && first < 2048 ? fp.dbg + 16 + 4 * 4096 + 16 * (first + (P.q_step < 0 ? 2048 : 0))
                                                            : nullptr,
-                                    fp.io_stage);
+                                    fp.io_stage, fp.io_skew > 0 ? fp.io_skew : kIoSkewPolling);
         } else {
             const int band = first + wave;
             if (band <= last) {
