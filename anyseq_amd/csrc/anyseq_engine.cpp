@@ -304,6 +304,7 @@ void init_tuning_locked() {
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
     g_tuning.io_stage = env_int("ANYSEQ_IO_STAGE", g_tuning.io_stage);
     g_tuning.io_skew = env_int("ANYSEQ_IO_SKEW", g_tuning.io_skew);
+    g_tuning.io_poll2 = env_int("ANYSEQ_IO_POLL2", g_tuning.io_poll2);
     g_tuning.virtbest = env_int("ANYSEQ_VIRT_BEST", g_tuning.virtbest);
     g_tuning.devplan = env_int("ANYSEQ_AFF_DEVPLAN", g_tuning.devplan);
     g_tuning.devfinal = env_int("ANYSEQ_AFF_DEVFINAL", g_tuning.devfinal);
@@ -707,7 +708,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.affine = sc.gap_open != 0;
     fp.dbg = nullptr;
     // affine_asm bit 0: asm steady state, bit 1: scalar row stores (diagnostics)
-    fp.pad = ((g_tuning.affasm & 1) ? 0 : 1) | (g_tuning.affasm & 2) | (g_tuning.affasm & 12);
+    fp.pad = ((g_tuning.affasm & 1) ? 0 : 1) | (g_tuning.affasm & 2) | (g_tuning.affasm & 12) | (g_tuning.affasm & 32);
     // the LUT weights (G space sub - 2 ge, X space sub - ge) must fit int8
     const int nge = -sc.gap_extend;
     const int ws[4] = {sc.match + 2 * nge, sc.mismatch + 2 * nge, sc.match + nge, sc.mismatch + nge};
@@ -720,6 +721,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.alpha = nullptr;
     fp.io_stage = g_tuning.io_stage;
     fp.io_skew = g_tuning.io_skew;
+    fp.io_poll2 = g_tuning.io_poll2;
     return fp;
 }
 
@@ -1159,9 +1161,13 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     int32_t* d_typ = d_status + nsv;
     int32_t* d_score = d_status + 2 * nsv;
     int32_t* h_status = (int32_t*)E.pin_down.get((2 * nsv + 4) * 4);
-    memcpy(h_status, sp.v.data(), nsv * 4);
-    memcpy(h_status + nsv, typ.data(), nsv * 4);
-    HIPCHECK(hipMemcpyAsync(d_status, h_status, 2 * nsv * 4, hipMemcpyHostToDevice, st));
+    // the initial split table: uploaded by the host-built levels below; the device-planned
+    // levels set its two ends in level 1's plan launch (the rest is written level by level)
+    auto upload_status = [&]() {
+        memcpy(h_status, sp.v.data(), nsv * 4);
+        memcpy(h_status + nsv, typ.data(), nsv * 4);
+        HIPCHECK(hipMemcpyAsync(d_status, h_status, 2 * nsv * 4, hipMemcpyHostToDevice, st));
+    };
     // level columns: view v's LH / LE / RH / RE at + v * nn
     const size_t nn = (size_t)std::max(n, 1);
     int32_t *LH0 = (int32_t*)E.L.get(nviews * nn * 4), *LE0 = (int32_t*)E.LE.get(nviews * nn * 4);
@@ -1315,7 +1321,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             register_static_range(rowbuf, max_rowbuf);
             register_static_range(rowpool, max_rowpool);
         }
-        HIPCHECK(hipMemsetAsync(d_tail, 0, tail_words * 4, st));
+        // (every level's header and error word are zeroed by level 1's plan launch; the
+        // final level's check word is written by aff_final_blocks_kernel)
         uint32_t* d_rchk = d_tail + 9 * (size_t)nlev;   // check words of level li at + 8 * li
         if (check_rows) HIPCHECK(hipMemsetD32Async(d_rchk, 0xffffffffu, 8 * (size_t)nlev, st));
         static std::atomic<int32_t> g_plan_epoch{0x40000};
@@ -1366,7 +1373,11 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         }
         // level 1: plan + prep; every level: fill, then one tail launch (join, next level's
         // sentinel rows, counters, best cells and plan)
+        if (nlev == 0) upload_status();   // (no level: the table's ends come from the host)
         if (nlev > 0) {
+            plans[0].zero_init = d_tail;
+            plans[0].nzero_init = 9 * nlev;
+            plans[0].init_ends = 1;
             HIPCHECK(anyseq_launch_aff_level_plan(&plans[0], st));
             HIPCHECK(anyseq_launch_fill_prep_planned(ctr, 32 + lv[0].slots, pbest, 2 * lv[0].parts, kAffNegH, rowbuf,
                                                      0, 0x80808080u, d_hdr, st));
@@ -1495,7 +1506,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         }
         planned = true;   // (the host loop below has nothing left)
     }
-    if (!planned) HIPCHECK(hipStreamSynchronize(st));   // h_status: its upload before the first download
+    if (!planned) {
+        upload_status();
+        HIPCHECK(hipStreamSynchronize(st));   // h_status: its upload before the first download
+    }
     for (int parts = 1; !planned && parts < sp.nb; parts *= 2) {
         ++g_stage_level;
         // free-end best cells, 2 per part, per view
@@ -2075,6 +2089,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "slack") g_tuning.slack = value;
     else if (n == "io_stage") g_tuning.io_stage = value;
     else if (n == "io_skew") g_tuning.io_skew = value;
+    else if (n == "io_poll2") g_tuning.io_poll2 = value;
     else if (n == "virtual_best") g_tuning.virtbest = value;
     else if (n == "affine_device_plan") g_tuning.devplan = value;
     else if (n == "affine_device_final") g_tuning.devfinal = value;

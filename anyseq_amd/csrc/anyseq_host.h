@@ -84,7 +84,8 @@ struct Tuning {
     int fronts = 2;
     int NWa = 0;     // affine fill: compute waves per workgroup (3, 4 or 7; 0 = chosen per launch)
     int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
-    int affasm = 1;  // affine fill: bit 0 asm steady state; bit 1 no asm epilogue; bits 2/3 none for best-all / other
+    int affasm = 1;  // affine fill: bit 0 asm steady state; bit 1 no asm epilogue; bits 2/3 none for best-all / other;
+                     // bit 5 the epilogue always captures column w-1 (the round-3 epilogue; A/B)
     int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
     int afft = 1;        // affine construct: run Hirschberg halves taller than wide transposed
     int prio = -1;       // 1: compute waves at s_setprio 3; 2: the I/O wave at 3; 3: its hand-off step at 3;
@@ -94,6 +95,7 @@ struct Tuning {
     int slack = 0;       // affine fill: half chunks a band starts behind the structural minimum
     int io_stage = 3;    // affine fill: the I/O wave's subject staging mode (io_wave; 0..3, r04o A/B)
     int io_skew = 0;     // affine fill: the I/O wave's skewed blocks per pass while a poll is out (0: 8)
+    int io_poll2 = 0;    // affine fill: the I/O wave keeps two hand-off polls in flight
     int devplan = 1;     // affine construct: Hirschberg levels planned on the device (one download)
     int devfinal = 1;    // affine construct, device-planned: the final level's blocks built on the device too
     int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe

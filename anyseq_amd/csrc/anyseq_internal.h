@@ -136,6 +136,7 @@ struct FillParams {
     int32_t slack;                    // affine: blocks a band starts behind the structural minimum (>= 0)
     int32_t io_stage;                 // affine I/O wave: subject staging mode (io_wave)
     int32_t io_skew;                  // affine I/O wave: skewed blocks per pass while a poll is out (0: 8)
+    int32_t io_poll2;                 // affine I/O wave: two hand-off polls in flight
 };
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).
@@ -235,6 +236,10 @@ struct AffLevelPlan {
     GroupRef* groups;             // 2 * parts * bound, k-major
     RowToCol* jobs;               // per half (n = 0: not transposed)
     uint32_t* hdr;                // [0] sentinel uint4s of rowbuf, [2..3] cells (u64)
+    // level 1's own launch (aff_level_plan_kernel) only: words to zero first (every
+    // level's header and error word), and the split table's two ends to set
+    uint32_t* zero_init;
+    int32_t nzero_init, init_ends;
 };
 
 // The tail of a device-planned level, one launch: the join of level L

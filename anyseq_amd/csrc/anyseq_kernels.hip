@@ -805,7 +805,7 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                         uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
                         uint32_t* cons0, uint32_t* err, bool reset_in = false, int ext = 0, int pscale = 1,
                         bool hprio = false, unsigned long long* evp = nullptr, int io_stage = 3,
-                        int io_skew = kIoSkewPolling) {
+                        int io_skew = kIoSkewPolling, bool io_poll2 = false) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
     constexpr int GR = 16;             // hand-off poll granule (columns)
@@ -821,6 +821,11 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
     int s_next = 0, sk_next = 0, in_gran = 0;
     int st_lim = 0;   // subject chunks whose loads are issued (s_next: stored in the ring)
     uint8_t sv[4];    // the loaded, not yet stored subject bytes (4 x 64 columns)
+    T qv[2] = {HandOff<T>::zero(), HandOff<T>::zero()};   // io_poll2: the poll in flight
+    int q_lim = 0, q_base = 0;
+#ifdef ANYSEQ_STAMPS
+    uint64_t q_t = 0;
+#endif
     uint32_t idle = 0;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     while (s_next < nchunks || (SKEW && sk_next < nskew) || (need_in && in_gran < ngran)) {
@@ -830,18 +835,42 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
         // load's round trip overlaps it.  The previous group's last band stores its
         // bottom row straight into g_in (sc1), which the host filled with the sentinel
         // (never a kernel value): a granule is in when none of its columns < w holds it.
+        // io_poll2: two polls in flight -- a pass issues one and consumes the one the
+        // previous pass issued (half the cadence of a poll's round trip); the consumed
+        // poll's granules start at pbase <= in_gran (those before in_gran came in through
+        // the other poll)
         T pv[2];
-        int plim = 0;
+        int plim = 0, pbase = in_gran;
 #ifdef ANYSEQ_STAMPS
-        const uint64_t t_poll = evp ? __builtin_amdgcn_s_memrealtime() : 0;   // diagnostic build
+        uint64_t t_poll = evp ? __builtin_amdgcn_s_memrealtime() : 0;   // diagnostic build
 #endif
         if (need_in && in_gran < ngran) {
-            plim = min(((int)lds_ld(cons0) + kSlots) * GPC, ngran);   // ring space
-            plim = min(plim, in_gran + 8);
+            int lim = min(((int)lds_ld(cons0) + kSlots) * GPC, ngran);   // ring space
+            lim = min(lim, in_gran + 8);
+            T nv[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int col = in_gran * GR + i * 64 + lane;
-                pv[i] = col < plim * GR && col < w ? HandOff<T>::load(g_in + col) : HandOff<T>::zero();
+                nv[i] = col < lim * GR && col < w ? HandOff<T>::load(g_in + col) : HandOff<T>::zero();
+            }
+            if (io_poll2) {
+                pv[0] = qv[0];
+                pv[1] = qv[1];
+                plim = q_lim;
+                pbase = q_base;
+                qv[0] = nv[0];
+                qv[1] = nv[1];
+                q_lim = lim;
+                q_base = in_gran;
+#ifdef ANYSEQ_STAMPS
+                const uint64_t tq = q_t;
+                q_t = t_poll;
+                t_poll = tq;
+#endif
+            } else {
+                pv[0] = nv[0];
+                pv[1] = nv[1];
+                plim = lim;
             }
         }
         // Subject staging (io_stage, FillParams::io_stage):
@@ -949,7 +978,7 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
             // with a compute wave, which otherwise wins every VALU slot); staging and skew
             // stay at the bottom, in the compute wave's bubbles
             if (hprio) __builtin_amdgcn_s_setprio(3);
-            // leading run of complete granules (16 lanes each)
+            // leading run of complete granules (16 lanes each) from in_gran
             int ready = 0;
             bool stop = false;
 #pragma unroll
@@ -957,7 +986,9 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                 const uint64_t bad = __ballot(HandOff<T>::pending(pv[i]));
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    if (!stop && in_gran + 4 * i + g < plim && ((bad >> (16 * g)) & 0xffffu) == 0u) ++ready;
+                    const int gi = pbase + 4 * i + g;
+                    if (gi < in_gran) continue;   // (came in through the other poll)
+                    if (!stop && gi < plim && ((bad >> (16 * g)) & 0xffffu) == 0u) ++ready;
                     else stop = true;
                 }
             }
@@ -972,8 +1003,8 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                 const int c0 = in_gran * GR, c2 = (in_gran + ready) * GR;
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const int col = c0 + i * 64 + lane;
-                    if (col < c2) ring0[col & IRM] = pv[i];
+                    const int col = pbase * GR + i * 64 + lane;
+                    if (col >= c0 && col < c2) ring0[col & IRM] = pv[i];
                 }
                 // ring of hand-off rows (DPProblem::nslots < ngroups - 1): put the sentinel
                 // back, so the group that reuses this slot 2*grid+2 groups later is polled
@@ -986,8 +1017,8 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                     T* gw = const_cast<T*>(g_in);
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
-                        const int col = c0 + i * 64 + lane;
-                        if (col < c2) HandOff<T>::store(gw + col, HandOff<T>::sentinel());
+                        const int col = pbase * GR + i * 64 + lane;
+                        if (col >= c0 && col < c2) HandOff<T>::store(gw + col, HandOff<T>::sentinel());
                     }
                 }
                 in_gran += ready;
@@ -1372,7 +1403,7 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
 // half of block b's top row is already in the TOP registers (never on entry from
 // C++: 0).  Returns 0, or 1 on a spin timeout.
 struct Aff2Args {
-    uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs;
+    uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs, thr;
     uint64_t gp;
     int q, wm, wx, ll, lh, zlp;
 };
@@ -1393,7 +1424,7 @@ struct Aff2Args {
                    [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
                    [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
-                   [hm] "s"(hm), [gp] "s"(gp)                                                                  \
+                   [hm] "s"(hm), [gp] "s"(gp), [thr] "s"(thr)                                                  \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
 // the band's last blocks (gen_aff2 epi): + the column-(w-1) capture and the poll clamp
 #define AF2E_ASM(NAME)                                                                                          \
@@ -1406,9 +1437,23 @@ struct Aff2Args {
                    [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
                    [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
-                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch)                                                  \
+                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr)                                  \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
-template <bool L, bool BORDER, int PUB, bool LUT, bool EPI = false>
+// the band's last blocks without the column-(w-1) capture (gen_aff2 cap=False)
+#define AF2F_ASM(NAME)                                                                                          \
+    asm volatile(NAME                                                                                          \
+                 : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
+                   [hg] "+v"(hg), [best] "+v"(bx), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf), [sc] "+s"(sc),     \
+                   [pf] "+s"(pf), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3), \
+                   [x4] "=&s"(x4) AF2_TS_OUT                                                                   \
+                 : [be] "s"(be), [q] "v"(a.q), [wm] "v"(a.wm), [wx] "v"(a.wx), [ll] "v"(a.ll), [lh] "v"(a.lh),   \
+                   [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
+                   [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
+                   [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
+                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr)                                  \
+                 : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
+// EPI: 0 the steady state, 1 the band's last blocks with the capture, 2 without it
+template <bool L, bool BORDER, int PUB, bool LUT, int EPI = 0>
 __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                   const Aff2Args& a, int go, int nge, int& g, int& fdn, int& dg,
                                                   int2& tf, int& e, int& hg, int& bx, uint64_t& ts_v, uint64_t& te_v,
@@ -1422,7 +1467,7 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
     sf = RFL(sf);
     sc = RFL(sc);
     be = RFL(be);
-    const uint32_t rb = RFL(a.rb), nb = RFL(a.nb), bvs = RFL(a.bvs);
+    const uint32_t rb = RFL(a.rb), nb = RFL(a.nb), bvs = RFL(a.bvs), thr = RFL(a.thr);
     const int ge = RFL(-nge);
     const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(a.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)a.gp);
 #ifdef ANYSEQ_STAMPS
@@ -1443,7 +1488,7 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
     if constexpr (!BORDER && PUB == 0) A(AF2_NAME(ANYSEQ_##V##_##K##_B0_NONE_U##U));         \
     if constexpr (!BORDER && PUB == 1) A(AF2_NAME(ANYSEQ_##V##_##K##_B0_LDS_U##U));          \
     if constexpr (!BORDER && PUB == 2) A(AF2_NAME(ANYSEQ_##V##_##K##_B0_GLOB_U##U));
-    if constexpr (EPI) {
+    if constexpr (EPI == 1) {
         nch = __builtin_amdgcn_readfirstlane(nch);
         int cnt = cap[0], gc = cap[1], ec = cap[2], fc = cap[3];
         if constexpr (L && LUT) { AF2_SEL(AF2E_ASM, AF2E, L, 1) }
@@ -1451,6 +1496,13 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
         if constexpr (!L && LUT) { AF2_SEL(AF2E_ASM, AF2E, G, 1) }
         if constexpr (!L && !LUT) { AF2_SEL(AF2E_ASM, AF2E, G, 0) }
         cap[0] = cnt, cap[1] = gc, cap[2] = ec, cap[3] = fc;
+    } else if constexpr (EPI == 2) {
+        nch = __builtin_amdgcn_readfirstlane(nch);
+        (void)cap;
+        if constexpr (L && LUT) { AF2_SEL(AF2F_ASM, AF2F, L, 1) }
+        if constexpr (L && !LUT) { AF2_SEL(AF2F_ASM, AF2F, L, 0) }
+        if constexpr (!L && LUT) { AF2_SEL(AF2F_ASM, AF2F, G, 1) }
+        if constexpr (!L && !LUT) { AF2_SEL(AF2F_ASM, AF2F, G, 0) }
     } else {
         (void)nch, (void)cap;
         if constexpr (L && LUT) { AF2_SEL(AF2_ASM, AF2, L, 1) }
@@ -1464,6 +1516,7 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
 }
 #undef AF2_ASM
 #undef AF2E_ASM
+#undef AF2F_ASM
 
 template <bool PARTIAL>
 __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k,
@@ -1578,6 +1631,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         la.skb = lds_addr(io.skew) + 4u * lane;
         la.lo = 8u * (lane - 48);   // publishing lanes 48..63: 16 columns each half block
         la.lid8 = 8u * lane;
+        la.thr = (uint32_t)max(k.thr, 0);   // band 0's pace (FillParams::throttle)
         // band 0's top border (value, value + go) in the loop's space
         la.bvb = (uint32_t)(xs ? to_x(B.top(lane, nge), lane) : B.top(lane, nge));
         la.bvs = (uint32_t)(B.top(1, nge) - B.top(0, nge) - (xs ? nge : 0));
@@ -1604,7 +1658,10 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 // one block of slack: block b starts once chunk b+1 is published, so in the
                 // steady state the loop's poll (step 16) already sees the next chunk and
                 // prefetches its top row -- no wait on the band chain's critical path
-                if (!io.in_border) {
+                // (without slack the loop's own block-start poll waits for the same half
+                // 2b: entering it right away overlaps the conversions and the loop's
+                // prologue with that wait -- round 4)
+                if (!io.in_border && k.slack > 0) {
                     const uint32_t need = (uint32_t)min(2 * b + 1 + k.slack, 2 * nchunks);
                     if (seen_prod < need && !(seen_prod = spin_lds_ge(io.my_prod, need, err))) return;
                 }
@@ -1622,9 +1679,6 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 uint32_t bb = (uint32_t)b;
                 const int role = (io.in_border ? 3 : 0) + (io.out_lds ? 1 : (io.gout ? 2 : 0));
                 uint32_t st = 0;
-#define AF2_CALL(LV, BD, PB, LU)                                                                               \
-    st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, fdn, \
-                                       dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, nullptr, dbp)
 #define AF2_ROLES(LV, LU)                          \
     switch (role) {                                \
         case 0: AF2_CALL(LV, false, 0, LU); break; \
@@ -1634,6 +1688,34 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         case 4: AF2_CALL(LV, true, 1, LU); break;  \
         default: AF2_CALL(LV, true, 2, LU); break; \
     }
+                // A band whose column-(w-1) state nobody reads (no out_col / out_col_e,
+                // last-row F or last-column best: the transposed Hirschberg halves, the
+                // score fronts) runs its last blocks in the same loop as the rest -- the
+                // capture-free epilogue variant (gen_aff2 cap=False), whose polls stop at
+                // the last half -- so there is no transition between two loops, and no
+                // capture work, on the band chain at the band's end (round 4)
+                const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || bestmode == 3 || (k.flags & 32);
+                if (epi && !need_cap) {
+#define AF2_CALL(LV, BD, PB, LU)                                                                                  \
+    st = aff2_loop_asm<LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
+                                          fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), \
+                                          nullptr, dbp)
+                    if (xs) {
+                        if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
+                    } else {
+                        if (k.lut) { AF2_ROLES(false, true) } else { AF2_ROLES(false, false) }
+                    }
+#undef AF2_CALL
+                    if (st) {
+                        atomicOr(err, ERR_SPIN_TIMEOUT);
+                        return;
+                    }
+                    if (xs) best = max(best, bx - (row + 2) * nge);
+                    break;   // band done (g / e / fdn: nobody reads them)
+                }
+#define AF2_CALL(LV, BD, PB, LU)                                                                               \
+    st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, fdn, \
+                                       dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, nullptr, dbp)
                 if (xs) {
                     if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
                 } else {
@@ -1648,9 +1730,9 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                     ev_store(8, __builtin_amdgcn_s_memrealtime());   // epilogue entry
 #endif
                     int cap[4] = {w + lane - (int)bb * CH, g, e, fdn};   // steps until column w-1
-#define AF2_CALL(LV, BD, PB, LU)                                                                                     \
-    st = aff2_loop_asm<LV, BD, PB, LU, true>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
-                                             fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), cap, dbp)
+#define AF2_CALL(LV, BD, PB, LU)                                                                               \
+    st = aff2_loop_asm<LV, BD, PB, LU, 1>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
+                                          fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), cap, dbp)
                     if (xs) {
                         if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
                     } else {
@@ -1887,7 +1969,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                                     P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc, 2, 2, fp.prio == 3,
                                     fp.dbg && first < 2048 ? fp.dbg + 16 + 4 * 4096 + 16 * (first + (P.q_step < 0 ? 2048 : 0))
                                                            : nullptr,
-                                    fp.io_stage, fp.io_skew > 0 ? fp.io_skew : kIoSkewPolling);
+                                    fp.io_stage, fp.io_skew > 0 ? fp.io_skew : kIoSkewPolling, fp.io_poll2 != 0);
         } else {
             const int band = first + wave;
             if (band <= last) {
@@ -2750,7 +2832,23 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
     }
 }
 
-__global__ __launch_bounds__(1024) void aff_level_plan_kernel(const AffLevelPlan a) { aff_level_plan_body(a); }
+__global__ __launch_bounds__(1024) void aff_level_plan_kernel(const AffLevelPlan a) {
+    // (level 1: what a memset and an upload did before -- two launches fewer)
+    if (a.nzero_init > 0 || a.init_ends) {
+        for (int i = threadIdx.x; i < a.nzero_init; i += blockDim.x) a.zero_init[i] = 0u;
+        if (a.init_ends && threadIdx.x == 0) {
+            int32_t* spl = const_cast<int32_t*>(a.spl);
+            int32_t* typ = const_cast<int32_t*>(a.typ);
+            spl[0] = 0;
+            spl[a.nb] = a.n;
+            typ[0] = a.kind != KIND_GLOBAL ? T_AFTER : T_H;
+            typ[a.nb] = a.kind != KIND_GLOBAL ? T_BEFORE : T_H;
+        }
+        __threadfence();
+        __syncthreads();
+    }
+    aff_level_plan_body(a);
+}
 
 constexpr int kTailStage = 8192;   // partials staged in LDS per chunk of parts (64 KiB)
 constexpr int kTailThreads = 1024;   // (16 waves: a join thread loads at most 4 rows of a 4096-row slice)
@@ -3459,7 +3557,7 @@ __global__ __launch_bounds__(1024) void aff_final_blocks_kernel(const AffFinalPl
         if (!ok) atomicOr(&bad, 1);
     }
     __syncthreads();
-    if (bad && threadIdx.x == 0) *a.err = 1u;
+    if (threadIdx.x == 0) *a.err = bad ? 1u : 0u;
     const bool stop = bad || (a.kind != KIND_GLOBAL && *a.score <= 0);
     for (int b = threadIdx.x; b < a.nb; b += blockDim.x) {
         BlockInfo bi{};

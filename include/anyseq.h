@@ -117,8 +117,9 @@ void anyseq_last_fill_timing(double* ms, int* launches);
 void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells);
 /* Plan of the calling thread's most recent sharded construct (anyseq_shard_construct,
  * anyseq_construct_local_sharded): the number of leading Hirschberg levels whose
- * halves were column-blocked over all ranks (0: every level dealt round-robin, e.g.
- * when GPU_MAX_HW_QUEUES is too small for the concurrent shard streams).  Resets it. */
+ * halves were column-blocked over rank subgroups (level 1 over all ranks; 0: every
+ * level dealt round-robin, e.g. when GPU_MAX_HW_QUEUES is too small for the concurrent
+ * shard streams).  Resets it. */
 int anyseq_last_shard_plan(void);
 
 /* ---- column-block sharded score (build-defined) ----
@@ -142,12 +143,14 @@ int anyseq_shard_finalize(void);
 /* Sharded affine construct (align.impala:237-311 distributed by level):
  * every rank calls it with the whole pair after anyseq_shard_init.  Level 1's two
  * halves are column-blocked over ALL ranks (rank g fills query columns
- * [g*lenq/N, (g+1)*lenq/N) of both, boundary columns over RCCL send/recv); the half
- * fills of the later levels and the final 128-column blocks are dealt round-robin; the
- * level columns are all-reduced over RCCL, and every rank returns the same score and
- * strings (sparse i+j+1 layout, lenq+lens bytes each).  When GPU_MAX_HW_QUEUES leaves
- * too few hardware queues for level 1's concurrent transport streams, level 1 is dealt
- * round-robin too (same result; anyseq_last_shard_plan reports which plan ran). */
+ * [g*lenq/N, (g+1)*lenq/N) of both, boundary columns over RCCL send/recv); every later
+ * level with P parts and N >= 2P ranks is column-blocked the same way, part p over the
+ * rank subgroup [p*N/P, (p+1)*N/P); the half fills of the remaining levels and the final
+ * 128-column blocks are dealt round-robin; the level columns are all-reduced over RCCL,
+ * and every rank returns the same score and strings (sparse i+j+1 layout, lenq+lens
+ * bytes each).  When GPU_MAX_HW_QUEUES leaves too few hardware queues for the concurrent
+ * transport streams, those levels are dealt round-robin too (same result;
+ * anyseq_last_shard_plan reports which plan ran). */
 int anyseq_shard_construct(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
                            int lens, char* alQuery, char* alSubject, int64_t* score);
 /* The same plan with `nshards` virtual ranks in this process on one device (one fill

@@ -109,6 +109,33 @@ def test_affine_waves_per_group(anyseq, oracle, nw):
         anyseq.set_option("affine_waves_per_group", 0)
 
 
+@pytest.mark.parametrize("option,value,default", [
+    ("io_stage", 0, 3), ("io_stage", 1, 3), ("io_stage", 2, 3),   # the I/O wave's subject staging
+    ("io_poll2", 1, 0),                                           # two hand-off polls in flight
+    ("io_skew", 2, 0),                                            # skewed blocks per polling pass
+    ("priority", 0, -1), ("priority", 3, -1),                     # issue priority
+    ("affine_asm", 33, 1),                                        # the capturing band epilogue
+])
+def test_affine_io_modes(anyseq, oracle, option, value, default):
+    """The affine fill's I/O-wave and epilogue variants give the
+    same scores and constructs: multi-group halves (HBM hand-offs through the I/O wave),
+    a long subject (several staging batches) and both epilogues (the fused capture-free
+    loop of bands nobody reads the last column of, the capturing one of the others)."""
+    rng = random.Random(28)
+    anyseq.set_option(option, value)
+    try:
+        for kind in KINDS:
+            q, s = rnd(rng, 2600), rnd(rng, 1900)
+            sc = (2, -1, -3, -1)
+            assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, option, value)
+            assert anyseq.construct(kind, q, s, *sc) == oracle.affine_construct(kind, q, s, *sc), (kind, option)
+        q, s = rnd(rng, 700), rnd(rng, 9000)
+        for kind in KINDS:
+            assert gpu(anyseq, kind, q, s, (2, -1, -2, -1)) == ora(oracle, kind, q, s, (2, -1, -2, -1)), (kind, option)
+    finally:
+        anyseq.set_option(option, default)
+
+
 def test_affine_rejects_bad_scoring(anyseq):
     with pytest.raises(anyseq.AnySeqError):
         anyseq.score("global", "ACGT", "ACGT", gap_open=1, gap_extend=-1)

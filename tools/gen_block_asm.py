@@ -326,7 +326,7 @@ SLIM = int(os.environ.get("ANYSEQ_GEN_SLIM", "1"))
 AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
-def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
+def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     """Affine steady-state loop, round 3: full blocks b .. be-1.
     kind G: G space (X_G = X + (r+c+2)|ge|), no clamp, no best (amode 0).
     kind L: X space (X = H + (r+2)|ge|, a per-ROW shift): the local clamp H >= 0 is
@@ -348,7 +348,16 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
     epi: the band's last blocks (some lanes past the last column w-1): every lane keeps
     computing past w (subject code 0xFF; those cells feed no real cell), polls stop at
     the last half (nch = 2 x chunks), the best takes real cells only, and each lane
-    captures its state at column w-1 (per-lane countdown cnt) into gc / ec / fc."""
+    captures its state at column w-1 (per-lane countdown cnt) into gc / ec / fc.
+    cap False (round 4, the AF2F variants): an epilogue for bands whose column-(w-1)
+    state nobody reads (no out_col / out_col_e / last-row F / last-column best: the
+    transposed Hirschberg halves and the score fronts): no capture, and the best over
+    every cell as in the main loop -- a cell right of column w-1 (subject code 0xFF,
+    weight -1) never exceeds some real cell (its diagonal, E and F terms are each below
+    a real cell's H; the clamp's 0 is a real cell's floor too), so the maximum is the
+    same.  The capture made the epilogue ~1.6x slower per step, and every band's
+    epilogue sits on the band chain (a consumer's last main-loop block waits for its
+    producer's last publish, at the producer's epilogue end)."""
     L = kind == "L"
     trailing = pub != "lds"
     out = []
@@ -466,6 +475,8 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
     def body(k):
         cs, ns = sets[k], sets[1 - k]
         e("s_add_u32 %[x1], %[b], 1")
+        if border:
+            throttle(e, k)            # band 0 paces the chain (%[thr] s_sleep-1 units per block)
         event(k, 0, EVB + 2)          # producer: block EVB+2 starts
         event(k, 3, EVB)              # consumer: block EVB starts
         # ---- first half of this block's top row (half 2b)
@@ -560,7 +571,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
                 if sr:
                     e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
-                if L and u % 2 == 1 and not epi:
+                if L and u % 2 == 1 and not (epi and cap):
                     e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
                 if sr:
                     e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
@@ -576,7 +587,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
                 e(f"v_max3_i32 {OG_(u)}, v{B_AA}, %[e], {tf}")
                 e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
                 e(f"v_max_i32_e32 {OF_(u)}, {tf}, %[hg]")
-            if epi:
+            if epi and cap:
                 if L:
                     # best over real cells only (cnt >= 0: column <= w-1)
                     e(f"v_max_i32_e32 v{B_AT}, %[best], {OG_(u)}")
@@ -589,7 +600,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False):
                 e(f"v_cndmask_b32_e32 %[fc], %[fc], {OF_(u)}, vcc")
                 e("v_add_u32_e32 %[cnt], -1, %[cnt]")
             if not REORDER:
-                if L and u % 2 == 1 and not epi:
+                if L and u % 2 == 1 and not (epi and cap):
                     e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
                 if sr:
                     e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
@@ -698,11 +709,11 @@ def main():
             for pub in ("none", "lds", "glob"):
                 for lut in (0, 1):
                     for ts in (False, True):
-                        for epi in (False, True):
-                            name = (f"ANYSEQ_AF2{'E' if epi else ''}_{kind}_B{border}_{pub.upper()}_U{lut}"
+                        for epi, cap, tag in ((False, True, ""), (True, True, "E"), (True, False, "F")):
+                            name = (f"ANYSEQ_AF2{tag}_{kind}_B{border}_{pub.upper()}_U{lut}"
                                     + ("_TS" if ts else ""))
                             lines.append(f"#define {name} \\")
-                            for ln in gen_aff2(kind, border, pub, lut, ts, epi):
+                            for ln in gen_aff2(kind, border, pub, lut, ts, epi, cap):
                                 lines.append(f'    "{ln}\\n" \\')
                             lines.append("")
     sclob = ", ".join(f'"s{n}"' for n in range(TA, TB + 2))
