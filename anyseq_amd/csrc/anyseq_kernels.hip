@@ -1661,7 +1661,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 // (without slack the loop's own block-start poll waits for the same half
                 // 2b: entering it right away overlaps the conversions and the loop's
                 // prologue with that wait -- round 4)
-                if (!io.in_border && k.slack > 0) {
+                if (!io.in_border && (k.slack > 0 || (k.flags & 32))) {
                     const uint32_t need = (uint32_t)min(2 * b + 1 + k.slack, 2 * nchunks);
                     if (seen_prod < need && !(seen_prod = spin_lds_ge(io.my_prod, need, err))) return;
                 }
