@@ -708,7 +708,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.affine = sc.gap_open != 0;
     fp.dbg = nullptr;
     // affine_asm bit 0: asm steady state, bit 1: scalar row stores (diagnostics)
-    fp.pad = ((g_tuning.affasm & 1) ? 0 : 1) | (g_tuning.affasm & 2) | (g_tuning.affasm & 12) | (g_tuning.affasm & 32);
+    fp.pad = ((g_tuning.affasm & 1) ? 0 : 1) | (g_tuning.affasm & 2) | (g_tuning.affasm & 12) | (g_tuning.affasm & 96);
     // the LUT weights (G space sub - 2 ge, X space sub - ge) must fit int8
     const int nge = -sc.gap_extend;
     const int ws[4] = {sc.match + 2 * nge, sc.mismatch + 2 * nge, sc.match + nge, sc.mismatch + nge};

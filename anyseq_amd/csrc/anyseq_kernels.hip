@@ -1661,7 +1661,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 // (without slack the loop's own block-start poll waits for the same half
                 // 2b: entering it right away overlaps the conversions and the loop's
                 // prologue with that wait -- round 4)
-                if (!io.in_border && (k.slack > 0 || (k.flags & 32))) {
+                if (!io.in_border && (k.slack > 0 || (k.flags & 64))) {
                     const uint32_t need = (uint32_t)min(2 * b + 1 + k.slack, 2 * nchunks);
                     if (seen_prod < need && !(seen_prod = spin_lds_ge(io.my_prod, need, err))) return;
                 }
@@ -1694,7 +1694,10 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 // capture-free epilogue variant (gen_aff2 cap=False), whose polls stop at
                 // the last half -- so there is no transition between two loops, and no
                 // capture work, on the band chain at the band's end (round 4)
-                const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || bestmode == 3 || (k.flags & 32);
+                // (bands with a best of their cells keep the masked epilogue too: with the
+                // best over the cells past w the local construct went wrong -- r04v, cause
+                // not found yet)
+                const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || bestmode != 0 || (k.flags & 32);
                 if (epi && !need_cap) {
 #define AF2_CALL(LV, BD, PB, LU)                                                                                  \
     st = aff2_loop_asm<LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \

@@ -114,7 +114,7 @@ def test_affine_waves_per_group(anyseq, oracle, nw):
     ("io_poll2", 1, 0),                                           # two hand-off polls in flight
     ("io_skew", 2, 0),                                            # skewed blocks per polling pass
     ("priority", 0, -1), ("priority", 3, -1),                     # issue priority
-    ("affine_asm", 1, 33), ("affine_asm", 33, 33),                # fused capture-free band ends / round 3's
+    ("affine_asm", 1, 97), ("affine_asm", 33, 97),                # fused band end + spin-free start / the start only
 ])
 def test_affine_io_modes(anyseq, oracle, option, value, default):
     """The affine fill's I/O-wave and epilogue variants give the

@@ -12,4 +12,4 @@ for rep in 1 2; do
     ANYSEQ_AFFINE_ASM=$a timeout -k 10 120 $B --config 1 --kind local --gap-open -2 --steps 10 --warmup 3 > $O/afl_a${a}_r$rep.json 2> $O/afl_a${a}_r$rep.err || exit 1
   done
 done
-timeout -k 10 120 python -u tools/probes/_aff_timeline.py $O/tl > $O/timeline.txt 2>&1 || exit 1
+ANYSEQ_AFFINE_ASM=1 timeout -k 10 120 python -u tools/probes/_aff_timeline.py $O/tl > $O/timeline.txt 2>&1 || exit 1
