@@ -56,10 +56,11 @@ VALU_DESIGN_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
 # VALU instructions per wave step (64 cells) of the steady-state asm loops
 # (tools/gen_block_asm.py): linear 5 (+1 publishing shift); affine
 # round 3: 9.25 counted in G space, 10.75 in X space (clamp + best), and the PMC
-# measurement of the X-space fill with its block overheads, 12.9 per wave step
-# (profiles/r03a_pmc.json: SQ_INSTS_VALU / (cells / 64)); G space = 9.25 + the same
-# 2.15 of block overhead.
-VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.4, "affine_local": 12.9}
+# measurement of the X-space fill with its block overheads and I/O waves, 12.9 per
+# wave step (profiles/r03a_pmc.json: SQ_INSTS_VALU / (cells / 64)), 12.8 in round 4
+# (profiles/r04z_pmc.json: 859.2 M per 65536^2 local score launch); G space = 9.25 +
+# the same 2.15 of block overhead.
+VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.4, "affine_local": 12.8}
 
 AFFINE = dict(match=2, mismatch=-1, gap_open=-2, gap_extend=-1)
 METRIC = "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; % of HBM roofline"
