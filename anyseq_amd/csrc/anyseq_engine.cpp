@@ -311,9 +311,15 @@ void init_tuning_locked() {
     g_tuning_init = true;
 }
 
+int process_hw_queues() {
+    static const int q = env_int("GPU_MAX_HW_QUEUES", 4);
+    return q;
+}
+
 Engine& engine() {
     std::lock_guard<std::mutex> lk(g_engines_mu);
     init_tuning_locked();
+    (void)process_hw_queues();   // (the snapshot, before this library's first HIP call)
     if (g_device < 0) g_device = env_int("ANYSEQ_DEVICE", 0);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) fail("no HIP device available (hipGetDeviceCount)");
@@ -1446,7 +1452,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             AffFinalPlan F{};
             F.spl = d_spl;
             F.typ = d_typ;
-            F.score = d_score;
+            // (no level, m <= 128: nothing writes d_score; the caller checked score > 0)
+            F.score = nlev > 0 ? d_score : nullptr;
             F.blocks = d_fblocks;
             F.tall = d_tall;
             F.err = d_ferr;
@@ -2093,6 +2100,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "virtual_best") g_tuning.virtbest = value;
     else if (n == "affine_device_plan") g_tuning.devplan = value;
     else if (n == "affine_device_final") g_tuning.devfinal = value;
+    else if (n == "plan_hw_queues") g_tuning.plan_queues = value;
     else return -1;
     return 0;
 }

@@ -99,8 +99,14 @@ struct Tuning {
     int devplan = 1;     // affine construct: Hirschberg levels planned on the device (one download)
     int devfinal = 1;    // affine construct, device-planned: the final level's blocks built on the device too
     int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe
+    int plan_queues = 0; // sharded construct plan: hardware queues to plan for (0 = the process's, below)
 };
 extern Tuning g_tuning;
+
+// GPU_MAX_HW_QUEUES as HIP read it: snapshot once, at the first engine use (before the
+// first HIP call of this library), so a later change of the variable cannot make the
+// plan disagree with the real queue count.
+int process_hw_queues();
 
 // Buffers and events of one in-flight fill launch (one per concurrently running
 // fill: the engine has one, each local shard of the sharded driver its own).

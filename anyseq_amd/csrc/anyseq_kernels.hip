@@ -3561,7 +3561,8 @@ __global__ __launch_bounds__(1024) void aff_final_blocks_kernel(const AffFinalPl
     }
     __syncthreads();
     if (threadIdx.x == 0) *a.err = bad ? 1u : 0u;
-    const bool stop = bad || (a.kind != KIND_GLOBAL && *a.score <= 0);
+    // (score null: no Hirschberg level ran, the host has already checked the score)
+    const bool stop = bad || (a.score && a.kind != KIND_GLOBAL && *a.score <= 0);
     for (int b = threadIdx.x; b < a.nb; b += blockDim.x) {
         BlockInfo bi{};
         const int ts = a.typ[b], te = a.typ[b + 1];

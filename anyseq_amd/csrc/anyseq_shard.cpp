@@ -143,7 +143,7 @@ hipStream_t lazy_stream(hipStream_t& s) {
 void check_hw_queues(int streams) {
     // this process's streams: the engine's, torch's null stream, the shards' fill and transport streams
     const int need = streams + 2;
-    const int have = env_int("GPU_MAX_HW_QUEUES", 4);
+    const int have = process_hw_queues();
     if (have < need)
         fail("the sharded fill runs %d concurrent streams: set GPU_MAX_HW_QUEUES >= %d (<= 32) in the environment "
              "before the first HIP call (it is %d); streams sharing a hardware queue would deadlock behind the "
@@ -833,13 +833,19 @@ void place_shard(Shard& S, const ShardPart& T, int rank) {
 // one rank per GPU needs its fill and up to 4 transport streams.  When the process
 // cannot give it that, the construct deals every level round-robin instead of failing
 // (same result, bit for bit).
-int hw_queues_available() { return env_int("GPU_MAX_HW_QUEUES", 4) - 2; }   // less the engine's and torch's
+// (the process's queues as HIP read them, or the plan_hw_queues option's; less the
+// engine's and torch's)
+int hw_queues_available() {
+    return (g_tuning.plan_queues > 0 ? std::min(g_tuning.plan_queues, process_hw_queues()) : process_hw_queues()) - 2;
+}
 int max_local_level1(int num_cus) { return std::max(1, num_cus / 8 - 8); }
 bool level1_local_possible(int N, int num_cus) {
     return N >= 2 && N <= max_local_level1(num_cus) && 3 * N - 2 <= hw_queues_available();
 }
-bool level1_rccl_possible(int rank, int world) {
-    return world >= 2 && 1 + 2 * ((rank > 0) + (rank < world - 1)) <= hw_queues_available();
+// The same answer on every rank (the ranks must agree on the collectives a level runs):
+// the worst case, an interior rank's fill + 2 transport streams per neighbour.
+bool level1_rccl_possible(int world) {
+    return world >= 2 && 1 + 2 * std::min(2, world - 1) <= hw_queues_available();
 }
 
 // Emulated ranks (anyseq_construct_local_sharded): N in-process shards, view g = rank g;
@@ -1159,7 +1165,7 @@ int anyseq_shard_construct(int kind, const anyseq_scoring* sc, const char* query
         cs.max_u8 = [comm](uint8_t* p, size_t n, hipStream_t st) {
             NCCLCHECK(ncclAllReduce(p, p, n, ncclUint8, ncclMax, comm, st));
         };
-        if (level1_rccl_possible(cs.rank, cs.world)) cs.blocked = [](const ShardLevel& J) { blocked_rccl(J); };
+        if (level1_rccl_possible(cs.world)) cs.blocked = [](const ShardLevel& J) { blocked_rccl(J); };
         const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
                                             lens, alQuery, alSubject, cs);
         if (score) *score = v;

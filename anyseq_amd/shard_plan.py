@@ -143,6 +143,15 @@ def blocked_level(parts: int, world: int) -> bool:
     return world >= 2 * parts
 
 
+def level1_blocked(n: int, m: int, world: int) -> bool:
+    """Whether the engine column-blocks level 1 of an n x m affine construct over `world`
+    ranks (anyseq_engine.cpp aff_construct_hb, with transposed halves and enough hardware
+    queues): a level exists (m > 128, two 128-column blocks), world >= 2 (the one part over
+    all ranks) and the part's query rows -- all n of them at level 1 -- give every rank
+    at least one column (len >= G)."""
+    return m > 128 and blocked_level(1, world) and n >= world
+
+
 def part_subgroup(p: int, parts: int, world: int):
     """(first rank, ranks) of part p's subgroup."""
     r0 = p * world // parts

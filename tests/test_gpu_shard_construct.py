@@ -135,7 +135,7 @@ def test_sharded_construct_level1_path_taken(anyseq, monkeypatch):
     assert launches["1"] - launches["0"] >= (8 - 2) + (8 - 4) - 2, launches
 
 
-def test_sharded_construct_level1_queue_fallback(anyseq, monkeypatch):
+def test_sharded_construct_level1_queue_fallback(anyseq):
     """Advisor round 3: the column-blocked level 1 needs 3N-2 concurrent shard streams.
     Under the box default of 4 hardware queues it must fall back to the round-robin
     level 1 (same result, anyseq_last_shard_plan() == 0) instead of failing; with enough
@@ -145,12 +145,17 @@ def test_sharded_construct_level1_queue_fallback(anyseq, monkeypatch):
     s = related(rng, q, 2200)
     want = anyseq.construct("local", q, s, 2, -1, -2, -1)
     plans = {}
-    for queues in ("4", "24"):
-        monkeypatch.setenv("GPU_MAX_HW_QUEUES", queues)   # (this process has 24; the check reads the variable)
-        anyseq.last_shard_plan()
-        assert anyseq.construct_local_sharded("local", q, s, 2, 2, -1, -2, -1) == want, queues
-        plans[queues] = anyseq.last_shard_plan()
-    assert plans == {"4": 0, "24": 1}, plans
+    try:
+        # (this process has 24 queues, snapshot at the first engine use; the plan option
+        # caps what the plan may assume, advisor round 4)
+        for queues in (4, 0):
+            anyseq.set_option("plan_hw_queues", queues)
+            anyseq.last_shard_plan()
+            assert anyseq.construct_local_sharded("local", q, s, 2, 2, -1, -2, -1) == want, queues
+            plans[queues] = anyseq.last_shard_plan()
+    finally:
+        anyseq.set_option("plan_hw_queues", 0)
+    assert plans == {4: 0, 0: 1}, plans
 
 
 def test_sharded_construct_nonpow2_fixture(anyseq):
@@ -166,3 +171,26 @@ def test_sharded_construct_nonpow2_fixture(anyseq):
     assert anyseq.last_shard_plan() == 2
     assert v == g["score"]
     assert (hashlib.sha256(aq).hexdigest(), hashlib.sha256(as_).hexdigest()) == (g["sha_alq"], g["sha_als"])
+
+
+def test_level1_blocked_matches_engine(anyseq):
+    """shard_plan.level1_blocked (what tools/rccl_ranks.py asserts on every RCCL construct
+    case) is the engine's own choice of a column-blocked level 1 (advisor round 4): the
+    worker's cases at 2 emulated ranks, scaled to a quarter, plus edge shapes (no level;
+    a query shorter than the rank count)."""
+    from anyseq_amd.shard_plan import level1_blocked
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "rccl_ranks.py")
+    spec = importlib.util.spec_from_file_location("rccl_ranks", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rng = random.Random(96)
+    shapes = [(k, max(1, n // 4), max(1, m // 4), 2) for k, n, m in mod.CONSTRUCT_CASES]
+    shapes += [("local", 1, 900, 2), ("local", 2, 900, 3), ("semiglobal", 3, 900, 3), ("global", 500, 128, 2)]
+    for kind, n, m, ns in shapes:
+        q = rnd(rng, n)
+        s = related(rng, q, m) if n > 50 else rnd(rng, m)
+        want = anyseq.construct(kind, q, s, 2, -1, -2, -1)
+        anyseq.last_shard_plan()
+        assert anyseq.construct_local_sharded(kind, q, s, ns, 2, -1, -2, -1) == want, (kind, n, m, ns)
+        assert (anyseq.last_shard_plan() >= 1) == level1_blocked(n, m, ns), (kind, n, m, ns)

@@ -301,18 +301,22 @@ def test_sharded_level1_column_blocks(world):
 
 def test_rccl_worker_cases_cover_column_blocked_level1():
     """tools/rccl_ranks.py (the 2-GPU RCCL parity worker) must include constructs whose
-    level 1 is column-blocked over the ranks (level1_rccl) as well as round-robin ones,
-    and say which it expects (checked there through anyseq_last_shard_plan)."""
+    level 1 is column-blocked over the ranks (blocked_rccl) as well as ones with no
+    blocked level, judged by the one definition the worker asserts with
+    (shard_plan.level1_blocked; checked against the engine's own choice in
+    tests/test_gpu_shard_construct.py::test_level1_blocked_matches_engine)."""
     import importlib.util
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "rccl_ranks.py")
     spec = importlib.util.spec_from_file_location("rccl_ranks", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    blocked = [c for c in mod.CONSTRUCT_CASES if c[3]]
-    assert blocked and any(not c[3] for c in mod.CONSTRUCT_CASES)
-    for kind, n, m, exp in mod.CONSTRUCT_CASES:
-        assert mod.level1_expected(n, m, 2) == exp, (kind, n, m)
+    blocked = [c for c in mod.CONSTRUCT_CASES if SP.level1_blocked(c[1], c[2], 2)]
+    assert blocked and any(not SP.level1_blocked(c[1], c[2], 2) for c in mod.CONSTRUCT_CASES)
     assert {c[0] for c in blocked} >= {"local", "semiglobal"}
+    # the engine's condition: a level (m > 128), world >= 2, n >= world
+    assert SP.level1_blocked(8000, 16384, 2) and not SP.level1_blocked(100, 120, 2)
+    assert not SP.level1_blocked(3, 4000, 4) and SP.level1_blocked(4, 4000, 4)
+    assert not SP.level1_blocked(5000, 5000, 1)
 
 
 # ------------------------- column-blocked levels >= 2 over rank subgroups (§6.2) --

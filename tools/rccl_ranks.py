@@ -10,10 +10,10 @@ anyseq_shard_score / anyseq_shard_construct, whose boundary columns and level
 columns travel over RCCL; rank 0 prints one JSON line per case and
 ALL_MATCH / MISMATCH; the exit status is 0 only if every case matches.
 
-Construct cases (CONSTRUCT_CASES): a subject longer than the query (n < m: level 1's
-transposed halves are shorter than the query, so level 1 is dealt round-robin) and
-square pairs, where level 1 is column-blocked over the ranks (level1_rccl, the
-boundary columns over RCCL send/recv); every case asserts through
+Construct cases (CONSTRUCT_CASES): subjects longer than the query and square or wide
+pairs; level 1 (and, at world >= 4, level 2) is column-blocked over the ranks whenever
+the query gives every rank a column (shard_plan.level1_blocked, the engine's own test:
+blocked_rccl, the boundary columns over RCCL send/recv); every case asserts through
 anyseq_last_shard_plan which plan ran.  RCCL_FIXTURE=1 adds the configs[2] fixture
 (tests/golden/config2_65536.json, SW affine 65536^2: score and SHA-256 of both strings).
 
@@ -30,22 +30,9 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SCORE_CASES = [("global", 0), ("semiglobal", 0), ("local", 0), ("global", -2), ("semiglobal", -2), ("local", -2)]
-# (kind, n, m, level 1 column-blocked?)  The column-blocked level 1 needs the halves
-# transposed and the query longer than the level's split row (anyseq_engine.cpp).
-CONSTRUCT_CASES = [("semiglobal", 8000, 16384, False), ("local", 8000, 16500, False),
-                   ("local", 16384, 16384, True), ("semiglobal", 16384, 16384, True),
-                   ("global", 12000, 9000, True)]
-
-
-def level1_expected(n: int, m: int, world: int) -> bool:
-    """Whether the engine column-blocks level 1 of an n x m construct over `world` ranks
-    (the same test as anyseq_engine.cpp: one part, transposed halves, len > the left
-    half's width; level 1 splits at the middle 128-column block, aff_part_geo)."""
-    if world < 2 or n < world or m <= 128:
-        return False
-    nb = (m + 127) // 128
-    half = 128 * (nb // 2)
-    return n > half
+# (kind, n, m): level 1 column-blocked iff shard_plan.level1_blocked(n, m, world)
+CONSTRUCT_CASES = [("semiglobal", 8000, 16384), ("local", 8000, 16500), ("local", 16384, 16384),
+                   ("semiglobal", 16384, 16384), ("global", 12000, 9000), ("local", 100, 120)]
 
 
 def main():
@@ -54,6 +41,7 @@ def main():
     import torch.distributed as dist
     import anyseq_amd as A
     from anyseq_amd import sharded
+    from anyseq_amd.shard_plan import level1_blocked
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
@@ -79,7 +67,7 @@ def main():
             print(json.dumps({"op": "score", "kind": c[0], "gap_open": c[1], "n": n, "m": m, "world": world,
                               "single": ref[c], "rccl": got, "match": good, "s": round(dt, 4)}), flush=True)
     for c in CONSTRUCT_CASES:
-        k, cn, cm, blocked = c
+        k, cn, cm = c
         t = time.time()
         A.last_shard_plan()
         got = sharded.construct(k, Q[:cn], S[:cm], gap_open=-2)
@@ -87,7 +75,7 @@ def main():
         dt = time.time() - t
         exp = ref_c[c]
         good = got[0] == exp[0] and got[1] == exp[1] and got[2] == exp[2]
-        plan_ok = (plan >= 1) == blocked == level1_expected(cn, cm, world)
+        plan_ok = (plan >= 1) == level1_blocked(cn, cm, world)
         ok &= good and plan_ok
         if rank == 0:
             print(json.dumps({"op": "construct", "kind": k, "n": cn, "m": cm, "gap_open": -2, "world": world,
