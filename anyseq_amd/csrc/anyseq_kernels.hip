@@ -774,6 +774,7 @@ struct HandOff<int32_t> {
     __device__ static bool pending(int32_t v) { return v == -1; }
     __device__ static int32_t zero() { return 0; }
     __device__ static int32_t sentinel() { return -1; }
+    __device__ static int32_t neg() { return -(1 << 29); }
 };
 template <>
 struct HandOff<int2> {
@@ -789,6 +790,7 @@ struct HandOff<int2> {
     __device__ static bool pending(int2 v) { return v.x == (int)0x80808080; }
     __device__ static int2 zero() { return make_int2(0, 0); }
     __device__ static int2 sentinel() { return make_int2((int)0x80808080, (int)0x80808080); }
+    __device__ static int2 neg() { return make_int2(-(1 << 29), -(1 << 29)); }   // (kAffNeg, kAffNeg)
 };
 
 #ifndef ANYSEQ_IO_SKEW_POLLING
@@ -1022,6 +1024,14 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                     }
                 }
                 in_gran += ready;
+                // ext: the consumer's blocks run past w to the end of the last chunk, whose
+                // columns past the last granule (16 when ceil(w/16) is odd) no poll brings
+                // in: "minus infinity" there, not whatever an earlier workgroup left in
+                // this LDS (those cells' best counts in the capture-free band end, round 5)
+                if (ext && in_gran >= ngran) {
+                    const int c = ngran * GR + lane;
+                    if (c < nchunks * CH) ring0[c & IRM] = HandOff<T>::neg();
+                }
                 // the counter: granules (pscale 2, CH 32), else whole chunks
                 lds_st(prod0, in_gran >= ngran ? (uint32_t)(nchunks * pscale) : (uint32_t)(in_gran * pscale / GPC));
                 progress = true;
@@ -1335,6 +1345,7 @@ struct AffShared {
     uint32_t prod[NW + 1];
     uint32_t cons[NW + 1];
     uint32_t skew[kSkewBlocks][8][64];   // pre-skewed subject, as FillShared::skew
+    int2 neg[32];   // "minus infinity" top row: the capture-free epilogue's blocks past the last chunk
     uint32_t s_filled;
     uint32_t tail;
     int32_t group;
@@ -1350,6 +1361,7 @@ struct AffIO {
     uint32_t* next_cons;
     const uint8_t* s_ring;
     const uint32_t* skew;
+    const int2* neg;
     uint32_t* s_filled;
     uint32_t* tail;
     int2* gout;   // last band of a group: HBM destination of the bottom row (G, F)
@@ -1403,7 +1415,7 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
 // half of block b's top row is already in the TOP registers (never on entry from
 // C++: 0).  Returns 0, or 1 on a spin timeout.
 struct Aff2Args {
-    uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs, thr;
+    uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs, thr, neg;
     uint64_t gp;
     int q, wm, wx, ll, lh, zlp;
 };
@@ -1450,7 +1462,7 @@ struct Aff2Args {
                    [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
                    [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
-                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr)                                  \
+                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr), [neg] "s"(negp)                 \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
 // EPI: 0 the steady state, 1 the band's last blocks with the capture, 2 without it
 template <bool L, bool BORDER, int PUB, bool LUT, int EPI = 0>
@@ -1498,6 +1510,7 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
         cap[0] = cnt, cap[1] = gc, cap[2] = ec, cap[3] = fc;
     } else if constexpr (EPI == 2) {
         nch = __builtin_amdgcn_readfirstlane(nch);
+        const uint32_t negp = __builtin_amdgcn_readfirstlane(a.neg);
         (void)cap;
         if constexpr (L && LUT) { AF2_SEL(AF2F_ASM, AF2F, L, 1) }
         if constexpr (L && !LUT) { AF2_SEL(AF2F_ASM, AF2F, L, 0) }
@@ -1632,6 +1645,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         la.lo = 8u * (lane - 48);   // publishing lanes 48..63: 16 columns each half block
         la.lid8 = 8u * lane;
         la.thr = (uint32_t)max(k.thr, 0);   // band 0's pace (FillParams::throttle)
+        la.neg = lds_addr(io.neg);
         // band 0's top border (value, value + go) in the loop's space
         la.bvb = (uint32_t)(xs ? to_x(B.top(lane, nge), lane) : B.top(lane, nge));
         la.bvs = (uint32_t)(B.top(1, nge) - B.top(0, nge) - (xs ? nge : 0));
@@ -1694,10 +1708,17 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 // capture-free epilogue variant (gen_aff2 cap=False), whose polls stop at
                 // the last half -- so there is no transition between two loops, and no
                 // capture work, on the band chain at the band's end (round 4)
-                // (bands with a best of their cells keep the masked epilogue too: with the
-                // best over the cells past w the local construct went wrong -- r04v, cause
-                // not found yet)
-                const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || bestmode != 0 || (k.flags & 32);
+                // A best of every cell takes the cells past w too.
+                // They never exceed the best real cell when (1) a diagonal step past w never
+                // gains -- the LUT's weight of code 0xFF is -1 in X space (H - 1 - |ge|),
+                // the compare's is the mismatch -- (2) the top row past w is cells of the
+                // band above, or "minus infinity" (the I/O wave's pad past the last granule,
+                // the masked top row past the last chunk), and (3) band 0's top border past
+                // w cannot seed a winner: -inf, or the free border under the clamp (H = 0,
+                // every real cell >= 0).  Else the capturing end (best over real cells).
+                const bool top_safe = !io.in_border || (B.tfree ? clamp : B.tg == kAffNeg);
+                const bool best_safe = bestmode == 0 || (bestmode == 1 && (k.lut || k.wx <= 2 * nge) && top_safe);
+                const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || !best_safe || (k.flags & 32);
                 if (epi && !need_cap) {
 #define AF2_CALL(LV, BD, PB, LU)                                                                                  \
     st = aff2_loop_asm<LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
@@ -1942,6 +1963,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
             sh.prod[threadIdx.x] = 0;
             sh.cons[threadIdx.x] = 0;
         }
+        if (threadIdx.x < 32) sh.neg[threadIdx.x] = make_int2(kAffNeg, kAffNeg);
         __syncthreads();
         const int gi = __builtin_amdgcn_readfirstlane(sh.group);
         if (gi >= ngroups_total || err_set(err)) break;
@@ -1984,6 +2006,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                 io.my_cons = &sh.cons[wave];
                 io.s_ring = sh.s_ring;
                 io.skew = &sh.skew[0][0][0];
+                io.neg = sh.neg;
                 io.s_filled = &sh.s_filled;
                 io.tail = &sh.tail;
                 io.out_lds = band < last;

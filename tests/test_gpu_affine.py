@@ -136,6 +136,42 @@ def test_affine_io_modes(anyseq, oracle, option, value, default):
         anyseq.set_option(option, default)
 
 
+@pytest.mark.parametrize("nw", [3, 4, 7])
+@pytest.mark.parametrize("asm", [1, 65])
+def test_affine_fused_end_every_cell_best(anyseq, oracle, nw, asm):
+    """Round 5 (verdict round 4, item 1): the capture-free band end with a best of every
+    cell (local scores and local constructs).  Round 4 saw local scores like 0x04000DB5
+    at shapes 511x33, 1000x200 and 700x100 -- exactly those whose first band of a later
+    workgroup (fed through the I/O wave) runs the asm end over a last chunk whose second
+    half no hand-off poll covers (ceil(w/16) odd): a stale LDS word of an earlier
+    workgroup there became the top row of cells past w, and their best won.  Shapes with
+    and without that gap, three wave counts, the fused end with both band starts, and
+    schemes where band 0's finite top border could seed a winner past w (mismatch far
+    below the gap costs; > 8 symbols, the compare weights, with a positive mismatch):
+    those keep the capturing end."""
+    rng = random.Random(29)
+    anyseq.set_option("affine_waves_per_group", nw)
+    anyseq.set_option("affine_asm", asm)
+    try:
+        shapes = [(511, 33), (1000, 200), (700, 100), (1500, 64), (640, 47), (900, 81), (2600, 1900)]
+        schemes = [(2, -1, -2, -1), (1, -6, -2, -1), (3, -2, -1, -3)]
+        for i, (n, m) in enumerate(shapes):
+            sc = schemes[i % len(schemes)]
+            for alph in ("ACGT", "ACGTNRYKMSWB"):
+                q, s = rnd(rng, n, alph), rnd(rng, m, alph)
+                assert gpu(anyseq, "local", q, s, sc) == ora(oracle, "local", q, s, sc), (n, m, sc, alph)
+                if n <= 1000:
+                    assert anyseq.construct("local", q, s, *sc) == oracle.affine_construct("local", q, s, *sc), \
+                        (n, m, sc, alph)
+        q, s = rnd(rng, 700, "ACGTNRYKMSWB"), rnd(rng, 300, "ACGTNRYKMSWB")
+        for sc in [(4, 1, -6, -1), (3, 0, -2, -2)]:   # a mismatch that does not lose
+            assert gpu(anyseq, "local", q, s, sc) == ora(oracle, "local", q, s, sc), sc
+            assert anyseq.construct("local", q, s, *sc) == oracle.affine_construct("local", q, s, *sc), sc
+    finally:
+        anyseq.set_option("affine_waves_per_group", 0)
+        anyseq.set_option("affine_asm", 97)
+
+
 def test_affine_rejects_bad_scoring(anyseq):
     with pytest.raises(anyseq.AnySeqError):
         anyseq.score("global", "ACGT", "ACGT", gap_open=1, gap_extend=-1)

@@ -375,6 +375,13 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
         e(f"s_lshl_b32 %[x2], {breg}, 8")
         e("s_and_b32 %[x2], %[x2], 4095")
         e("s_add_u32 %[x2], %[x2], %[rb]")
+        if epi and not cap:
+            # blocks past the last chunk (2b >= nch; the polls stop at the last half):
+            # the top row from the "minus infinity" area, not a ring slot nobody
+            # published for them
+            e(f"s_lshl_b32 %[x4], {breg}, 1")
+            e("s_cmp_ge_u32 %[x4], %[nch]")
+            e("s_cselect_b32 %[x2], %[neg], %[x2]")
         e(f"v_mov_b32_e32 v{B_VB}, %[x2]")
 
     def border_write(breg):
