@@ -256,7 +256,11 @@ __device__ __forceinline__ void band_block(int t0, int lane, int w, int top_firs
     }
 }
 
+#ifdef ANYSEQ_ASM_INC   // (experimental builds: another generated loop, Makefile `lean`)
+#include ANYSEQ_ASM_INC
+#else
 #include "anyseq_block_asm.inc"
+#endif
 
 // A full 32-step block (all 64 lanes inside [0, w) or on virtual columns, no dead
 // rows) as ONE asm statement (tools/gen_block_asm.py): ra = LDS byte address of
@@ -1383,9 +1387,12 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
         const int2 top = u == 0 ? tf : rv[u - 1];
         const int upg = wave_shr1(top.x, g);
         const int fin = wave_shr1(top.y, fdn);
-        // virtual columns (< 0) hold a code that matches no query code
-        const int sb = (VIRT && c0 + u < 0) ? 0x1ff : (int)((sw[u >> 2] >> (8 * (u & 3))) & 0xffu);
-        const int wgt = q == sb ? k.wm : k.wx;
+        // virtual columns (< 0): no diagonal gain (the asm LUT gives their code 0xFF
+        // -1 in X space; the mismatch could be positive, which under the clamp would
+        // lift column -1 above the local border -- round 5); they only shape column -1
+        const bool vcol = VIRT && c0 + u < 0;
+        const int sb = (int)((sw[u >> 2] >> (8 * (u & 3))) & 0xffu);
+        const int wgt = vcol ? kAffNeg : (q == sb ? k.wm : k.wx);
         const int en = max(e, hg);
         int v = max(max(dg + wgt, en), fin);
         v = max(v, zc + u * k.nge);
@@ -1570,8 +1577,13 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     // left border is -inf, nor under NORMAL when min(match, mismatch) >= go + ge (flags
     // bit 4, set by the host): then cell (0,0) >= the largest border cell go + ge.
     const bool best_border_ok = !(bestmode == 1 && !clamp) || !finite_left || (bm == BM_NORMAL && (k.flags & 16));
+    // Under the clamp the virtual cells are clamped to H = 0, so a diagonal step into
+    // them must not gain: code 0xFF's weight is -1 (X space) in the LUT, but the compare
+    // weights give it the mismatch -- a positive mismatch would lift column -1 above the
+    // local left border (round 5: local scores too high with > 8 symbols and mismatch > 0)
+    const bool ff_loses = k.lut || k.wx <= 2 * nge;
     const bool virt = ASM_OK && !shard_left && !zero_open && !(bestmode == 2 && finite_left) && best_border_ok &&
-                      (!clamp || k.codes) && !(k.flags & 1);
+                      (!clamp || (k.codes && ff_loses)) && !(k.flags & 1);
     const int rb = band * 64;
     const int row = rb + lane;
     const bool dead = row >= h;
@@ -1717,7 +1729,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 // w cannot seed a winner: -inf, or the free border under the clamp (H = 0,
                 // every real cell >= 0).  Else the capturing end (best over real cells).
                 const bool top_safe = !io.in_border || (B.tfree ? clamp : B.tg == kAffNeg);
-                const bool best_safe = bestmode == 0 || (bestmode == 1 && (k.lut || k.wx <= 2 * nge) && top_safe);
+                const bool best_safe = bestmode == 0 || (bestmode == 1 && ff_loses && top_safe);
                 const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || !best_safe || (k.flags & 32);
                 if (epi && !need_cap) {
 #define AF2_CALL(LV, BD, PB, LU)                                                                                  \

@@ -172,6 +172,31 @@ def test_affine_fused_end_every_cell_best(anyseq, oracle, nw, asm):
         anyseq.set_option("affine_asm", 97)
 
 
+@pytest.mark.parametrize("asm", [97, 3, 1, 0])
+def test_affine_positive_mismatch(anyseq, oracle, asm):
+    """Round 5: a mismatch that does not lose (> 0, or 0).  Under the local clamp the
+    virtual prologue's cells are clamped to H = 0, so a diagonal step into them must not
+    gain: the compare weights (> 8 symbols) gave code 0xFF the positive mismatch, and so
+    did the C++ blocks' virtual columns (the asm LUT's -1 was right) -- local scores came
+    out too high (468 vs 427; 89 vs 81).  Every kind, both weight paths, the asm / C++
+    band ends and starts (affine_asm 97, 3: C++ epilogue, 1: fused end, 0: no asm)."""
+    rng = random.Random(30)
+    anyseq.set_option("affine_asm", asm)
+    try:
+        for it in range(24):
+            sc = [(4, 1, -6, -1), (3, 0, -2, -2), (5, 2, -3, -1)][it % 3]
+            alph = ("ACGT", "ACGTNRYKMSWB")[(it // 3) % 2]
+            n, m = rng.randint(20, 400), rng.randint(20, 400)
+            q, s = rnd(rng, n, alph), rnd(rng, m, alph)
+            for kind in KINDS:
+                assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, n, m, sc, alph, asm)
+            if it % 4 == 0:
+                assert anyseq.construct("local", q, s, *sc) == oracle.affine_construct("local", q, s, *sc), \
+                    (n, m, sc, alph, asm)
+    finally:
+        anyseq.set_option("affine_asm", 97)
+
+
 def test_affine_rejects_bad_scoring(anyseq):
     with pytest.raises(anyseq.AnySeqError):
         anyseq.score("global", "ACGT", "ACGT", gap_open=1, gap_extend=-1)

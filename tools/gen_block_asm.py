@@ -24,6 +24,7 @@ store from a single lane would cost ~29 issue cycles per ds_write_b128 plus exec
 switches; the shift costs one VALU per step off the critical path.
 """
 import os
+import sys
 
 T0, O0, W, A = 64, 96, 128, 129   # fixed VGPRs: T 64..95, O 96..127, w, a (<= 170 VGPRs: 3 waves/SIMD)
 
@@ -114,13 +115,14 @@ SK0, VT, VT2, VA, VB = 130, 138, 139, 140, 141   # subject words, temps, LDS add
 TA, TB = 96, 98                                   # fixed SGPR pairs for s_memrealtime
 
 
-def wait(e, name, seen, target, addr, count=None, tmp=None):
+def wait(e, name, seen, target, addr, count=None, tmp=None, signed=False):
     """Spin until seen >= target, refreshing `seen` from the LDS word at `addr`
     (wave-uniform), with s_sleep between polls.  The 10 s s_memrealtime limit
     starts at the 256th poll and is checked every 256 polls (-> L_timeout): the
     common case (ready within a few polls) issues no SMEM read, whose latency the
     poll's lgkmcnt(0) would otherwise wait for on the hand-off's critical path."""
-    e(f"s_cmp_ge_u32 {seen}, {target}")
+    cmp = "s_cmp_ge_i32" if signed else "s_cmp_ge_u32"
+    e(f"{cmp} {seen}, {target}")
     e(f"s_cbranch_scc1 L_{name}_ok_%=")
     e("s_mov_b32 %[x3], 0")
     e(f"L_{name}_loop_%=:")
@@ -128,7 +130,7 @@ def wait(e, name, seen, target, addr, count=None, tmp=None):
     e(f"ds_read_b32 v{tmp}, {addr}")
     e("s_waitcnt lgkmcnt(0)")
     e(f"v_readfirstlane_b32 {seen}, v{tmp}")
-    e(f"s_cmp_ge_u32 {seen}, {target}")
+    e(f"{cmp} {seen}, {target}")
     e(f"s_cbranch_scc1 L_{name}_ok_%=")
     if count:
         e(f"s_add_u32 {count}, {count}, 1")
@@ -323,6 +325,13 @@ NEG_INF = -(1 << 29)   # kAffNeg
 REORDER = int(os.environ.get("ANYSEQ_GEN_REORDER", "1"))
 # gen_aff2 LDS publish (round 4): 1 = the slot address once per block, counter inside the exec window
 SLIM = int(os.environ.get("ANYSEQ_GEN_SLIM", "1"))
+# gen_aff2 issue slots (round 5): a wave alone on its SIMD issues about one instruction
+# per 4-5 cycles whatever its kind, so every SALU, s_waitcnt and LDS instruction of the
+# block costs a step's worth of VALU slots.  1 = the lean block: loop-carried diagonal /
+# top-row state in the rotation's own registers (no block-end moves), 4 counted LDS waits
+# per block instead of 16, the ring-slot check every other block, 2b kept in an SGPR, the
+# consumption counters every other block.
+LEAN = int(os.environ.get("ANYSEQ_GEN_LEAN", "0"))
 AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
@@ -396,12 +405,27 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
         e(f"v_add_u32_e32 v{B_VA}, %[rb], v{B_VA}")
         e(f"ds_write_b64 v{B_VA}, v[{B_VT}:{B_VT2}]")
 
+    # lean (non-border variants, where x0 is free): 2b in x0, set at the block start
+    b2 = LEAN and not border
+
     def half_target(add):
         # x4 = 2b + add (clamped to the last half in the epilogue)
-        e("s_lshl_b32 %[x4], %[b], 1")
-        e(f"s_add_u32 %[x4], %[x4], {add}")
+        if b2:
+            e(f"s_add_u32 %[x4], %[x0], {add}")
+        else:
+            e("s_lshl_b32 %[x4], %[b], 1")
+            e(f"s_add_u32 %[x4], %[x4], {add}")
         if epi:
             e("s_min_u32 %[x4], %[x4], %[nch]")
+
+    def pub_counter(half):
+        # x2 = 2(b-2) + half + 1 halves published (0 while b < 2)
+        if b2:
+            e(f"s_sub_u32 %[x2], %[x0], {3 - half}")
+        else:
+            e("s_lshl_b32 %[x2], %[b], 1")
+            e(f"s_sub_u32 %[x2], %[x2], {3 - half}")
+        e("s_max_i32 %[x2], %[x2], 0")
 
     EVB = 1000   # diagnostic build: the block whose hand-off events are recorded
 
@@ -443,10 +467,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
                 e("s_and_b32 %[x2], %[x2], 4095")
                 e("s_add_u32 %[x2], %[x2], %[nb]")
                 e(f"v_add_u32_e32 v{B_VT}, %[x2], %[lo]")
-            # counter: 2(b-2) + half + 1 halves published (0 while b < 2)
-            e("s_lshl_b32 %[x2], %[b], 1")
-            e(f"s_sub_u32 %[x2], %[x2], {3 - half}")
-            e("s_max_i32 %[x2], %[x2], 0")
+            pub_counter(half)
             e(f"v_mov_b32_e32 v{B_VT2}, %[x2]")
             e("s_mov_b64 exec, %[hm]")
             e(f"ds_write_b64 v{B_VT}, v[{reg}:{reg + 1}] offset:{128 * half}")
@@ -470,10 +491,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
             e(f"global_store_dwordx2 v{B_VT}, v[{reg}:{reg + 1}], %[gp] offset:{128 * half} sc1")
         e("s_mov_b64 exec, s[%d:%d]" % (TA, TA + 1))
         if pub == "lds":
-            # counter: 2(b-2) + half + 1 halves published (0 while b < 2)
-            e("s_lshl_b32 %[x2], %[b], 1")
-            e(f"s_sub_u32 %[x2], %[x2], {3 - half}")
-            e("s_max_i32 %[x2], %[x2], 0")
+            pub_counter(half)
             e(f"v_mov_b32_e32 v{B_VT2}, %[x2]")
             e(f"ds_write_b32 %[anp], v{B_VT2}")
         if pub == "glob":
@@ -482,6 +500,8 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     def body(k):
         cs, ns = sets[k], sets[1 - k]
         e("s_add_u32 %[x1], %[b], 1")
+        if b2:
+            e("s_lshl_b32 %[x0], %[b], 1")
         if border:
             throttle(e, k)            # band 0 paces the chain (%[thr] s_sleep-1 units per block)
         event(k, 0, EVB + 2)          # producer: block EVB+2 starts
@@ -501,14 +521,26 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
             e("s_waitcnt lgkmcnt(0)")
             e("s_mov_b32 %[tsf], 1")
             e(f"L_nots{k}_%=:")
-        if pub == "lds":
+        if pub == "lds" and not LEAN:
             # the next band's ring slot of chunk b-2 is free once it consumed chunk b-17
             e("s_cmp_lt_u32 %[b], 17")
             e(f"s_cbranch_scc1 L_nobp{k}_%=")
             e("s_sub_u32 %[x4], %[b], 17")
             wait(e, f"bp{k}", "%[sc]", "%[x4]", "%[anc]", tmp=B_VT2)
             e(f"L_nobp{k}_%=:")
+        elif pub == "lds" and k == 1:
+            # lean: every other block, for this block and the next (chunks b-2 and b-1:
+            # consumed through chunk b-16); the loop's first block is checked at entry
+            e("s_sub_u32 %[x4], %[b], 16")
+            wait(e, f"bp{k}", "%[sc]", "%[x4]", "%[anc]", tmp=B_VT2, signed=True)
         g, f, dg = "%[cur]", "%[fd]", "%[dg]"
+        if LEAN:
+            # the diagonal and lane 0's top values of step 0 stay in the rotation's own
+            # registers from the previous block (TG_30, TG_31 / TF_31); without the
+            # publishing shift register the cell pair of step 31 does too
+            dg = TG_(30)
+            if pub == "none":
+                g, f = OG_(31), OF_(31)
         nsub = 5 if border else 4   # subject reads (+ the border write) at step 8
         for u in range(32):
             if u == 8:
@@ -540,17 +572,31 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
                     wait(e, f"pb{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
                     event(k, 5, EVB)      # consumer: second half seen
                 top_reads(1)
-            if u in (1, 3, 5, 7, 9, 11, 13):
+            if LEAN:
+                # lean: reads 0-3 of the first half by step 1, 4-7 by step 9 (the subject
+                # reads and band 0's border write of step 8 may be in flight), the second
+                # half (issued at step 14, ~3 steps earlier) by step 17 (the half-0 publish
+                # of step 16 may be in flight)
+                if u == 1:
+                    e("s_waitcnt lgkmcnt(4)")
+                if u == 9:
+                    e(f"s_waitcnt lgkmcnt({nsub})")
+                if u == 17:
+                    e(f"s_waitcnt lgkmcnt({2 if pub == 'lds' else 0})")
+            elif u in (1, 3, 5, 7, 9, 11, 13):
                 i = (u - 1) // 2                   # first-half read holding T(u-1)
                 allowed = (7 - i) + (nsub if u > 8 else 0) + (1 if (u > 10 and not border) else 0)
                 e(f"s_waitcnt lgkmcnt({min(15, allowed)})")
-            if u >= 17 and u % 2 == 1:
+            elif u >= 17 and u % 2 == 1:
                 i = (u - 17) // 2                  # second-half read holding T(u-1)
                 allowed = (7 - i) + (2 if pub == "lds" else 0)
                 e(f"s_waitcnt lgkmcnt({min(15, allowed)})")
             sw = v(cs + u // 4)
-            tg = "%[tfg]" if u == 0 else TG_(u - 1)
-            tf = "%[tff]" if u == 0 else TF_(u - 1)
+            if LEAN:
+                tg, tf = TG_((u - 1) % 32), TF_((u - 1) % 32)
+            else:
+                tg = "%[tfg]" if u == 0 else TG_(u - 1)
+                tf = "%[tff]" if u == 0 else TF_(u - 1)
             # Instruction order (round 4): no VALU reads the result of the instruction
             # right before it -- E's max3 first, the DPP moves between the E pair, the
             # shift-register moves between OG -> hg -> F-down, the best after hg.
@@ -616,23 +662,29 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
                 publish(k, 0, AO0 + 6)             # cell pair of step 15: steps 0..15 in lanes 48..63
                 event(k, 1, EVB + 2)               # producer: first half of chunk EVB published
             g, f, dg = OG_(u), OF_(u), tg
-        e(f"v_mov_b32_e32 %[cur], {OG_(31)}")
-        e(f"v_mov_b32_e32 %[fd], {OF_(31)}")
-        e(f"v_mov_b32_e32 %[dg], {TG_(30)}")
+        if not LEAN or pub != "none":
+            e(f"v_mov_b32_e32 %[cur], {OG_(31)}")
+            e(f"v_mov_b32_e32 %[fd], {OF_(31)}")
+        if not LEAN:
+            e(f"v_mov_b32_e32 %[dg], {TG_(30)}")
         if pub != "none":
             e(f"v_mov_b32_dpp {OG_(31)}, {OG_(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
             e(f"v_mov_b32_dpp {OF_(31)}, {OF_(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-        e(f"v_mov_b32_e32 %[tfg], {TG_(31)}")
-        e(f"v_mov_b32_e32 %[tff], {TF_(31)}")
+        if not LEAN:
+            e(f"v_mov_b32_e32 %[tfg], {TG_(31)}")
+            e(f"v_mov_b32_e32 %[tff], {TF_(31)}")
         if pub != "none":
             publish(k, 1, AO0 + 6)                 # pair of step 31: steps 16..31 in lanes 48..63
             event(k, 2, EVB + 2)                   # producer: second half published
         event(k, 6, EVB)                           # consumer: block EVB ends
-        e(f"v_mov_b32_e32 v{B_VT2}, %[x1]")
-        if not border:
-            e(f"ds_write_b32 %[acn], v{B_VT2}")
-        if trailing:
-            e(f"ds_write_b32 %[atl], v{B_VT2}")
+        if not LEAN or k == 1:
+            # (lean: every other block -- a consumption counter one block behind only
+            # holds the producer and the I/O wave one ring slot further back)
+            e(f"v_mov_b32_e32 v{B_VT2}, %[x1]")
+            if not border:
+                e(f"ds_write_b32 %[acn], v{B_VT2}")
+            if trailing:
+                e(f"ds_write_b32 %[atl], v{B_VT2}")
         e("s_mov_b32 %[b], %[x1]")
 
     # the first block's subject codes into set 0 (band 0: and its border)
@@ -646,6 +698,18 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     if border:
         border_write("%[b]")
     e("s_waitcnt lgkmcnt(0)")
+    # lean: the loop-carried diagonal / top values (and without publishing, the cell
+    # pair) live in the rotation's registers; the ring slot of the first block's
+    # publish is checked here (the loop checks every other block)
+    lean_regs = [("%[dg]", TG_(30)), ("%[tfg]", TG_(31)), ("%[tff]", TF_(31))]
+    if pub == "none":
+        lean_regs += [("%[cur]", OG_(31)), ("%[fd]", OF_(31))]
+    if LEAN:
+        for named, reg in lean_regs:
+            e(f"v_mov_b32_e32 {reg}, {named}")
+        if pub == "lds":
+            e("s_sub_u32 %[x4], %[b], 17")
+            wait(e, "bpe", "%[sc]", "%[x4]", "%[anc]", tmp=B_VT2, signed=True)
     e("L_top_%=:")
     body(0)
     e("s_cmp_lt_u32 %[b], %[be]")
@@ -664,6 +728,9 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     e("s_waitcnt lgkmcnt(0)")
     e("s_mov_b32 %[st], 1")
     e("L_end_%=:")
+    if LEAN:
+        for named, reg in lean_regs:
+            e(f"v_mov_b32_e32 {named}, {reg}")
     return out
 
 
@@ -688,6 +755,8 @@ def OF_(u):
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
     dst = os.path.join(here, "..", "anyseq_amd", "csrc", "anyseq_block_asm.inc")
+    if len(sys.argv) > 1:   # (experimental builds: another file, e.g. ANYSEQ_GEN_LEAN=1)
+        dst = sys.argv[1]
     lines = ["// GENERATED by tools/gen_block_asm.py -- do not edit.", ""]
     variants = [("G", "G", {}), ("L", "L", {}),
                 # timing variants for tools/micro/block_micro.hip

@@ -11,7 +11,11 @@
 #include <cstdio>
 #include <vector>
 
+#ifdef ANYSEQ_ASM_INC
+#include ANYSEQ_ASM_INC
+#else
 #include "../../anyseq_amd/csrc/anyseq_block_asm.inc"
+#endif
 
 #define RFL(x) __builtin_amdgcn_readfirstlane(x)
 constexpr int kMaxW = 8;
