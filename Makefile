@@ -35,17 +35,17 @@ anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_stamps.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
-# experimental build: the lean affine loop (tools/gen_block_asm.py LEAN) as
-# anyseq_amd/libanyseq_lean.so, loaded with ANYSEQ_LIB for A/B runs
-lean: anyseq_amd/libanyseq_lean.so
-build/lean_asm.inc: tools/gen_block_asm.py
-	mkdir -p build && ANYSEQ_GEN_LEAN=1 python3 tools/gen_block_asm.py $@ > /dev/null
-anyseq_amd/libanyseq_lean.so: $(SRC)/anyseq_kernels.hip build/lean_asm.inc $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o $(SRC)/anyseq_internal.h
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_ASM_INC='"$(CURDIR)/build/lean_asm.inc"' -c $(SRC)/anyseq_kernels.hip -o build/anyseq_kernels_lean.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -Wl,-z,defs -o $@ build/anyseq_kernels_lean.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
+# experimental build for A/B runs: the affine loop generated under other generator knobs
+# (EXPGEN, e.g. `make exp EXPGEN="ANYSEQ_GEN_LEAN=0"`) as anyseq_amd/libanyseq_exp.so,
+# loaded with ANYSEQ_LIB
+EXPGEN ?= ANYSEQ_GEN_LEAN=1
+exp:
+	mkdir -p build && env $(EXPGEN) python3 tools/gen_block_asm.py build/exp_asm.inc > /dev/null
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_ASM_INC='"$(CURDIR)/build/exp_asm.inc"' -c $(SRC)/anyseq_kernels.hip -o build/anyseq_kernels_exp.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -Wl,-z,defs -o anyseq_amd/libanyseq_exp.so build/anyseq_kernels_exp.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
 clean:
 	rm -f $(SRC)/*.o $(LIB) anyseq_amd/libanyseq_*.so
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean stamps lean
+.PHONY: all oracle clean stamps exp

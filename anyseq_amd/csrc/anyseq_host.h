@@ -84,8 +84,9 @@ struct Tuning {
     int fronts = 2;
     int NWa = 0;     // affine fill: compute waves per workgroup (3, 4 or 7; 0 = chosen per launch)
     int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
-    int affasm = 97; // affine fill: bit 0 asm steady state; bit 1 no asm epilogue; bits 2/3 none for best-all / other;
-                     // bit 5 the round-3 band end (capturing epilogue), bit 6 its start (C++ spin) (A/B)
+    int affasm = 1;  // affine fill: bit 0 asm steady state; bit 1 no asm epilogue; bits 2/3 none for best-all / other;
+                     // bit 5 the round-3 band end (capturing epilogue), bit 6 its start (C++ spin) (A/B; round 5:
+                     // 1 = the fused band end, every-cell bests included, and the spin-free start: configs[2] +2 %)
     int ring_slots = 0;  // hand-off rows per problem (0 = 4*grid+4; never below 2*grid+2)
     int afft = 1;        // affine construct: run Hirschberg halves taller than wide transposed
     int prio = -1;       // 1: compute waves at s_setprio 3; 2: the I/O wave at 3; 3: its hand-off step at 3;

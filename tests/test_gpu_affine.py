@@ -114,7 +114,7 @@ def test_affine_waves_per_group(anyseq, oracle, nw):
     ("io_poll2", 1, 0),                                           # two hand-off polls in flight
     ("io_skew", 2, 0),                                            # skewed blocks per polling pass
     ("priority", 0, -1), ("priority", 3, -1),                     # issue priority
-    ("affine_asm", 1, 97), ("affine_asm", 33, 97),                # fused band end + spin-free start / the start only
+    ("affine_asm", 97, 1), ("affine_asm", 33, 1), ("affine_asm", 65, 1),   # round-3 ends / the start only / the end only
 ])
 def test_affine_io_modes(anyseq, oracle, option, value, default):
     """The affine fill's I/O-wave and epilogue variants give the
@@ -169,7 +169,7 @@ def test_affine_fused_end_every_cell_best(anyseq, oracle, nw, asm):
             assert anyseq.construct("local", q, s, *sc) == oracle.affine_construct("local", q, s, *sc), sc
     finally:
         anyseq.set_option("affine_waves_per_group", 0)
-        anyseq.set_option("affine_asm", 97)
+        anyseq.set_option("affine_asm", 1)
 
 
 @pytest.mark.parametrize("asm", [97, 3, 1, 0])
@@ -194,7 +194,7 @@ def test_affine_positive_mismatch(anyseq, oracle, asm):
                 assert anyseq.construct("local", q, s, *sc) == oracle.affine_construct("local", q, s, *sc), \
                     (n, m, sc, alph, asm)
     finally:
-        anyseq.set_option("affine_asm", 97)
+        anyseq.set_option("affine_asm", 1)
 
 
 def test_affine_rejects_bad_scoring(anyseq):

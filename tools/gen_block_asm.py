@@ -330,8 +330,9 @@ SLIM = int(os.environ.get("ANYSEQ_GEN_SLIM", "1"))
 # block costs a step's worth of VALU slots.  1 = the lean block: loop-carried diagonal /
 # top-row state in the rotation's own registers (no block-end moves), 4 counted LDS waits
 # per block instead of 16, the ring-slot check every other block, 2b kept in an SGPR, the
-# consumption counters every other block.
-LEAN = int(os.environ.get("ANYSEQ_GEN_LEAN", "0"))
+# consumption counters every other block.  A/B (gpurun_out/r05d, one box): the loop alone
+# 61.9 -> 58.1 cycles per step (X space, LDS publisher), configs[2] 517 -> 535 GCUPS.
+LEAN = int(os.environ.get("ANYSEQ_GEN_LEAN", "1"))
 AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
