@@ -308,6 +308,7 @@ void init_tuning_locked() {
     g_tuning.virtbest = env_int("ANYSEQ_VIRT_BEST", g_tuning.virtbest);
     g_tuning.devplan = env_int("ANYSEQ_AFF_DEVPLAN", g_tuning.devplan);
     g_tuning.devfinal = env_int("ANYSEQ_AFF_DEVFINAL", g_tuning.devfinal);
+    g_tuning.xcdq = env_int("ANYSEQ_XCD_GROUPS", g_tuning.xcdq);
     g_tuning_init = true;
 }
 
@@ -409,6 +410,16 @@ void audit_probs(const std::vector<DPProblem>& probs, bool aff) {
     }
 }
 
+// XCD-local groups (FillParams::xq): the affine fill of a single-GPU
+// launch (no concurrent shard fill it could wait on: a shard launch passes its own grid)
+// of a multiple of 8 workgroups, dealt grid / 8 per XCD, when the tuning asks for it;
+// returns the run of consecutive groups per XCD, or 0 (one queue).  A workgroup whose
+// XCD queue is empty takes from the others, so every group runs whatever the placement.
+int xcd_run(const Engine& E, int grid, bool aff, int grid_req = 0) {
+    if (!aff || !g_tuning.xcdq || grid_req > 0 || grid > E.num_cus || grid < kXcds || grid % kXcds != 0) return 0;
+    return grid / kXcds;
+}
+
 void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const FillParams& fp, hipStream_t st,
                   int grid_req, const void* extra, size_t extra_bytes, int32_t* init, int init_words,
                   int32_t init_value) {
@@ -460,11 +471,28 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     for (int k = 0; k < max_groups; ++k)
         for (size_t p = 0; p < probs.size(); ++p)
             if (k < probs[p].ngroups) groups.push_back(GroupRef{(int32_t)p, k, 0, 0});
+    // XCD-local groups (FillParams::xq; a launch over the whole chip only): the table
+    // stably partitioned by XCD, its 9 offsets uploaded right behind it
+    const int xrun = xcd_run(E, grid, aff, grid_req);
+    uint32_t xoff[kXcds + 1] = {0};
+    if (xrun > 0) {
+        std::vector<int64_t> first(probs.size(), 0);   // problem-major index of each problem's group 0
+        for (size_t p = 1; p < probs.size(); ++p) first[p] = first[p - 1] + probs[p - 1].ngroups;
+        std::vector<GroupRef> byx[kXcds];
+        for (const GroupRef& g : groups) byx[xcd_of_group(first[g.prob] + g.group, xrun)].push_back(g);
+        groups.clear();
+        for (int x = 0; x < kXcds; ++x) {
+            xoff[x] = (uint32_t)groups.size();
+            groups.insert(groups.end(), byx[x].begin(), byx[x].end());
+        }
+        xoff[kXcds] = (uint32_t)groups.size();
+    }
     // ONE device block per launch: [counters (32 words) | group flags | descriptors |
-    // group table | caller's extra payload], so the launch costs one upload and one
-    // memset besides the hand-off rows' sentinel fill
+    // group table (+ XCD offsets) | caller's extra payload], so the launch costs one
+    // upload and one memset besides the hand-off rows' sentinel fill
     const size_t zb = ((32 + flag_words) * 4 + 255) & ~(size_t)255;
-    const size_t pb = probs.size() * sizeof(DPProblem), gb = groups.size() * sizeof(GroupRef);
+    const size_t pb = probs.size() * sizeof(DPProblem),
+                 gb = groups.size() * sizeof(GroupRef) + (xrun > 0 ? sizeof xoff : 0);
     const size_t eoff = (pb + gb + 15) & ~(size_t)15;
     const size_t ub = eoff + extra_bytes;
     char* meta = (char*)C.probs.get(zb + ub);
@@ -503,7 +531,8 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     char* pin = (char*)C.pin.get(64 + ub + 16);
     C.err_host = (uint32_t*)pin;
     memcpy(pin + 64, C.h_probs.data(), pb);
-    memcpy(pin + 64 + pb, groups.data(), gb);
+    memcpy(pin + 64 + pb, groups.data(), groups.size() * sizeof(GroupRef));
+    if (xrun > 0) memcpy(pin + 64 + pb + groups.size() * sizeof(GroupRef), xoff, sizeof xoff);
     if (extra_bytes) memcpy(pin + 64 + eoff, extra, extra_bytes);
     if (groups.empty()) {
         if (ub) HIPCHECK(hipMemcpyAsync(meta + zb, pin + 64, ub, hipMemcpyHostToDevice, st));
@@ -522,6 +551,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
                                      rowbuf_ints * 4, aff ? 0x80808080u : 0xffffffffu, pin + 64, meta + zb, ub, st));
     FillParams fpl = fp;
     fpl.epoch = epoch;
+    fpl.xq = xrun > 0 ? reinterpret_cast<const uint32_t*>(d_groups + groups.size()) : nullptr;
     fpl.prio = fill_prio(aff);
     fpl.throttle = g_tuning.thr;
     fpl.slack = g_tuning.slack;
@@ -1271,7 +1301,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                                  64 * (int64_t)L.parts;
             L.rowbuf_bytes = (size_t)std::min(L.bound - 1, L.want) * 2 * (size_t)cols * 2 * 4;
             const size_t meta = (((32 + (size_t)L.slots) * 4 + 255) & ~(size_t)255) +
-                                (size_t)L.nh * sizeof(DPProblem) + (size_t)L.slots * sizeof(GroupRef);
+                                (size_t)L.nh * sizeof(DPProblem) + (size_t)L.slots * sizeof(GroupRef) +
+                                (kXcds + 1) * 4;   // (+ the XCD offsets of FillParams::xq)
             max_meta = std::max(max_meta, meta);
             max_rowbuf = std::max(max_rowbuf, L.rowbuf_bytes);
             max_rowpool = std::max(max_rowpool, (size_t)2 * ((size_t)n + 64 * (size_t)L.parts) * 2 * 4);
@@ -1376,6 +1407,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             A.groups = d_groups;
             A.jobs = d_jobs;
             A.hdr = d_hdr + 8 * li;
+            A.xrun = xcd_run(E, L.grid, true);
+            A.xq = reinterpret_cast<uint32_t*>(d_groups + L.slots);
         }
         // level 1: plan + prep; every level: fill, then one tail launch (join, next level's
         // sentinel rows, counters, best cells and plan)
@@ -1400,6 +1433,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             fpl.throttle = g_tuning.thr;
             fpl.slack = g_tuning.slack;
             fpl.dbg = nullptr;
+            fpl.xq = A.xrun > 0 ? A.xq : nullptr;
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li], st));
             HIPCHECK(anyseq_launch_fill_affine(L.nw, d_probs, d_groups, L.slots, ctr, d_err + li, &fpl, L.grid, st));
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li + 1], st));
@@ -2101,6 +2135,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_device_plan") g_tuning.devplan = value;
     else if (n == "affine_device_final") g_tuning.devfinal = value;
     else if (n == "plan_hw_queues") g_tuning.plan_queues = value;
+    else if (n == "xcd_groups") g_tuning.xcdq = value;
     else return -1;
     return 0;
 }

@@ -101,6 +101,7 @@ struct Tuning {
     int devfinal = 1;    // affine construct, device-planned: the final level's blocks built on the device too
     int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe
     int plan_queues = 0; // sharded construct plan: hardware queues to plan for (0 = the process's, below)
+    int xcdq = 0;        // affine fill: XCD-local groups on whole-chip launches (FillParams::xq)
 };
 extern Tuning g_tuning;
 

@@ -137,7 +137,21 @@ struct FillParams {
     int32_t io_stage;                 // affine I/O wave: subject staging mode (io_wave)
     int32_t io_skew;                  // affine I/O wave: skewed blocks per pass while a poll is out (0: 8)
     int32_t io_poll2;                 // affine I/O wave: two hand-off polls in flight
+    // XCD-local groups (round 5): null = one global queue in group-table
+    // order; else the table is partitioned by XCD (xcd_of_group), xq[x] .. xq[x+1] the
+    // groups of XCD x in k-major order, dequeued by that XCD's workgroups through the
+    // counter dq[kXcdCtr + x] (a workgroup whose queue is empty takes from the others)
+    const uint32_t* xq;
 };
+
+// XCD-local group placement: the workgroups of a launch of `grid` >= 8 are dealt to the 8
+// XCDs round-robin, grid / 8 each; a problem's groups go to the XCDs in runs of that many
+// consecutive groups (v = the problem's first group index in problem-major order + k), so
+// a hand-off between consecutive groups stays in one XCD's L2 but at run boundaries, and
+// any grid-wide window of consecutive groups spreads evenly over the XCDs.
+constexpr int kXcds = 8;
+constexpr int kXcdCtr = 16;   // dq[16 .. 23]: the per-XCD dequeue counters (zeroed with the launch's counters)
+__host__ __device__ inline int xcd_of_group(int64_t v, int run) { return (int)((v / (run > 0 ? run : 1)) % kXcds); }
 
 // Part table entry of one Hirschberg level (traceback_lintime.impala:44-135).
 struct PartInfo {
@@ -240,6 +254,10 @@ struct AffLevelPlan {
     // level's header and error word), and the split table's two ends to set
     uint32_t* zero_init;
     int32_t nzero_init, init_ends;
+    // XCD-local groups (FillParams::xq): run > 0 -> the group table in XCD order and its
+    // 9 offsets at xq (run: consecutive groups per XCD, the grid / 8)
+    int32_t xrun;
+    uint32_t* xq;
 };
 
 // The tail of a device-planned level, one launch: the join of level L

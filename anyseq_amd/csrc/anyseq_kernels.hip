@@ -1965,9 +1965,29 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
     // sleeps when idle; its hand-off polls sit on the band chain)
     if (fp.prio == 1 && wave < NW) __builtin_amdgcn_s_setprio(3);
     if (fp.prio == 2 && wave == NW) __builtin_amdgcn_s_setprio(3);
+    // XCD-local groups (FillParams::xq): this workgroup's XCD first, then the others
+    uint32_t xcc = 0;
+    if (fp.xq) asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= kXcds - 1;
     for (;;) {
         if (threadIdx.x == 0) {
-            sh.group = (int32_t)atomicAdd(dq, 1u);
+            if (fp.xq) {
+                int32_t g = ngroups_total;
+                for (uint32_t i = 0; i < (uint32_t)kXcds; ++i) {
+                    const uint32_t y = (xcc + i) & (kXcds - 1), lo = fp.xq[y], hi = fp.xq[y + 1];
+                    if (lo >= hi || __hip_atomic_load(dq + kXcdCtr + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                                        hi - lo)
+                        continue;
+                    const uint32_t j = atomicAdd(dq + kXcdCtr + y, 1u);
+                    if (j < hi - lo) {
+                        g = (int32_t)(lo + j);
+                        break;
+                    }
+                }
+                sh.group = g;
+            } else {
+                sh.group = (int32_t)atomicAdd(dq, 1u);
+            }
             sh.s_filled = 0;
             sh.tail = 0;
         }
@@ -2856,11 +2876,45 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
             }
         }
     }
-    // the group table, k-major over the half slots (a half's groups in increasing k)
+    // the group table, k-major over the half slots (a half's groups in increasing k);
+    // XCD-local groups (a.xrun > 0, FillParams::xq): stably partitioned by XCD
     const int nh = 2 * a.parts;
-    for (int i = (int)threadIdx.x; i < nh * a.bound; i += blockDim.x) {
-        const int k = i / nh, pr = i % nh;
-        a.groups[i] = GroupRef{pr, k, a.epoch, group_check(pr, k, a.epoch)};
+    const int T = nh * a.bound;
+    if (a.xrun <= 0) {
+        for (int i = (int)threadIdx.x; i < T; i += blockDim.x) {
+            const int k = i / nh, pr = i % nh;
+            a.groups[i] = GroupRef{pr, k, a.epoch, group_check(pr, k, a.epoch)};
+        }
+    } else {
+        __shared__ int32_t xcnt[kXcds], xoff[kXcds + 1];
+        if (threadIdx.x < kXcds) xcnt[threadIdx.x] = 0;
+        __syncthreads();
+        for (int i = (int)threadIdx.x; i < T; i += blockDim.x)
+            atomicAdd(&xcnt[xcd_of_group((int64_t)(i % nh) * a.bound + i / nh, a.xrun)], 1);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            xoff[0] = 0;
+            for (int x = 0; x < kXcds; ++x) xoff[x + 1] = xoff[x] + xcnt[x];
+        }
+        __syncthreads();
+        if (threadIdx.x <= kXcds) a.xq[threadIdx.x] = (uint32_t)xoff[threadIdx.x];
+        // rank within the XCD in k-major order: two block scans of four 16-bit counters
+        int32_t base[kXcds] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int t0 = 0; t0 < T; t0 += blockDim.x) {
+            const int i = t0 + (int)threadIdx.x;
+            const int k = i / nh, pr = i % nh;
+            const int x = i < T ? xcd_of_group((int64_t)pr * a.bound + k, a.xrun) : -1;
+            const int64_t lo = x >= 0 && x < 4 ? (int64_t)1 << (16 * x) : 0;
+            const int64_t hi = x >= 4 ? (int64_t)1 << (16 * (x - 4)) : 0;
+            int64_t tlo, thi;
+            const int64_t elo = block_scan_excl(lo, sh, &tlo);
+            const int64_t ehi = block_scan_excl(hi, sh, &thi);
+            if (x >= 0) {
+                const int rank = (int)(((x < 4 ? elo >> (16 * x) : ehi >> (16 * (x - 4)))) & 0xffff) + base[x];
+                a.groups[xoff[x] + rank] = GroupRef{pr, k, a.epoch, group_check(pr, k, a.epoch)};
+            }
+            for (int y = 0; y < kXcds; ++y) base[y] += (int)(((y < 4 ? tlo >> (16 * y) : thi >> (16 * (y - 4)))) & 0xffff);
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -202,3 +202,24 @@ def test_affine_rejects_bad_scoring(anyseq):
         anyseq.score("global", "ACGT", "ACGT", gap_open=1, gap_extend=-1)
     with pytest.raises(anyseq.AnySeqError):
         anyseq.score("global", "ACGT", "ACGT", gap_open=-1, gap_extend=0)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_affine_xcd_groups(anyseq, oracle, kind):
+    """XCD-local groups (round 5, FillParams::xq): the group table partitioned by XCD in
+    runs of grid/8 consecutive groups and dequeued per XCD (a workgroup whose queue is
+    empty takes from the others) gives the same scores and constructs: launches of 8..256
+    workgroups (affine_grid), host-built and device-planned levels, tall and wide halves."""
+    rng = random.Random(31)
+    anyseq.set_option("xcd_groups", 1)
+    try:
+        for grid in (0, 64, 8):
+            anyseq.set_option("affine_grid", grid)
+            for n, m in ((2600, 1900), (700, 5000), (9000, 3000)):
+                q, s = rnd(rng, n), rnd(rng, m)
+                sc = (2, -1, -3, -1)
+                assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, grid, n, m)
+                assert anyseq.construct(kind, q, s, *sc) == oracle.affine_construct(kind, q, s, *sc), (kind, grid, n, m)
+    finally:
+        anyseq.set_option("xcd_groups", 0)
+        anyseq.set_option("affine_grid", 0)

@@ -332,7 +332,8 @@ SLIM = int(os.environ.get("ANYSEQ_GEN_SLIM", "1"))
 # per block instead of 16, the ring-slot check every other block, 2b kept in an SGPR, the
 # consumption counters every other block.  A/B (gpurun_out/r05d, one box): the loop alone
 # 61.9 -> 58.1 cycles per step (X space, LDS publisher), configs[2] 517 -> 535 GCUPS.
-LEAN = int(os.environ.get("ANYSEQ_GEN_LEAN", "1"))
+# 2 = also the subject-prefetch wait every other block (r05f: configs[2] 544 -> 551 GCUPS).
+LEAN = int(os.environ.get("ANYSEQ_GEN_LEAN", "2"))
 AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
@@ -548,11 +549,18 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
                 # next block's subject codes (other register set) and, band 0, its border.
                 # Issued in every block (after the last one they read a stale slot, unused):
                 # the counted lgkmcnt waits assume they are in flight.
-                e("s_cmp_ge_u32 %[x1], %[be]")
-                e(f"s_cbranch_scc1 L_nopf{k}_%=")
-                e("s_add_u32 %[x4], %[b], 2")
-                wait(e, f"sf{k}", "%[sf]", "%[x4]", "%[asf]", tmp=B_VT2)
-                e(f"L_nopf{k}_%=:")
+                if LEAN < 2:
+                    e("s_cmp_ge_u32 %[x1], %[be]")
+                    e(f"s_cbranch_scc1 L_nopf{k}_%=")
+                    e("s_add_u32 %[x4], %[b], 2")
+                    wait(e, f"sf{k}", "%[sf]", "%[x4]", "%[asf]", tmp=B_VT2)
+                    e(f"L_nopf{k}_%=:")
+                elif k == 1:
+                    # lean: every other block, for this block's prefetch and the next's
+                    # (skewed blocks through b+2; the loop's first prefetch at entry)
+                    e("s_add_u32 %[x4], %[b], 3")
+                    e("s_min_u32 %[x4], %[x4], %[be]")
+                    wait(e, f"sf{k}", "%[sf]", "%[x4]", "%[asf]", tmp=B_VT2)
                 e("s_and_b32 %[x2], %[x1], 31")
                 e("s_lshl_b32 %[x2], %[x2], 11")
                 e(f"v_add_u32_e32 v{B_VA}, %[x2], %[skb]")
@@ -708,6 +716,10 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     if LEAN:
         for named, reg in lean_regs:
             e(f"v_mov_b32_e32 {reg}, {named}")
+        if LEAN >= 2:
+            e("s_add_u32 %[x4], %[b], 2")
+            e("s_min_u32 %[x4], %[x4], %[be]")
+            wait(e, "sfe", "%[sf]", "%[x4]", "%[asf]", tmp=B_VT2)
         if pub == "lds":
             e("s_sub_u32 %[x4], %[b], 17")
             wait(e, "bpe", "%[sc]", "%[x4]", "%[anc]", tmp=B_VT2, signed=True)
