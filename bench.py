@@ -209,6 +209,57 @@ def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: s
     }
 
 
+# Critical path of the affine construct ("what bounds configs[2]"): every
+# Hirschberg level is one band chain of its widest half, `cols + 1.28 rows` band steps
+# (a 64-row band trails the one above by 82 steps: 64 of skew, 16 of half-chunk
+# granularity, 2 of latency).  Clock and per-step costs measured on MI355X:
+CHAIN_CLOCK_GHZ = 2.18          # shader clock under a full-chip fill (loop micro: cycles / wall ns, r05d)
+CHAIN_LOOP_CYCLES = 57.0        # the production X-space loop alone, LDS publisher (aff_loop_micro, r05d/r05f)
+CHAIN_BARE_CYCLES = 42.0        # the bare X-space step, no publishing, no block overhead (aff_micro, r04)
+NORTH_STAR_GCUPS = 1400.0       # 70 % of the 2000 GCUPS HBM model (BASELINE.json north_star)
+
+
+def chain_steps(n: int, m: int) -> int:
+    """Band steps on the critical path of an n x m affine construct: sum over the levels
+    (P = 1, 2, 4, .. < nb parts of the 128-column blocks, aff_part_geo) of the widest
+    half's chain, run transposed when taller than wide (nominal parts of n / P rows)."""
+    nb = (m + 127) // 128
+    total, P = 0.0, 1
+    while P < nb:
+        half = 128 * ((-(-nb // P) + 1) // 2)
+        rows = -(-n // P)
+        w, h = (rows, half) if rows > half else (half, rows)
+        total += w + 1.28 * h
+        P *= 2
+    return int(total)
+
+
+def chain_model(n: int, m: int, fill_ms: float, step_ms: float):
+    """The reachable ceiling of the construct at the measured chain (verdict round 4, item
+    3): GCUPS if every chain step cost the loop's isolated step, or only the bare step."""
+    steps = chain_steps(n, m)
+    nonfill = max(step_ms - fill_ms, 0.0)
+    per_ns = fill_ms * 1e6 / steps if steps else None
+
+    def gcups_at(cycles):
+        t_ms = steps * cycles / (CHAIN_CLOCK_GHZ * 1e6) + nonfill
+        return round(n * m / (t_ms * 1e-3) / 1e9, 1)
+    need_ms = n * m / (NORTH_STAR_GCUPS * 1e9) * 1e3 - nonfill
+    return {
+        "chain_steps": steps, "fill_ms": round(fill_ms, 4), "nonfill_ms": round(nonfill, 4),
+        "ns_per_chain_step": round(per_ns, 2) if per_ns else None,
+        "cycles_per_chain_step": round(per_ns * CHAIN_CLOCK_GHZ, 1) if per_ns else None,
+        "clock_ghz": CHAIN_CLOCK_GHZ,
+        "ceiling_gcups_at_isolated_loop": gcups_at(CHAIN_LOOP_CYCLES), "isolated_loop_cycles": CHAIN_LOOP_CYCLES,
+        "ceiling_gcups_at_bare_step": gcups_at(CHAIN_BARE_CYCLES), "bare_step_cycles": CHAIN_BARE_CYCLES,
+        "north_star_gcups": NORTH_STAR_GCUPS,
+        "north_star_cycles_per_chain_step": round(need_ms * 1e6 / steps * CHAIN_CLOCK_GHZ, 1) if steps else None,
+        "reading": "the north star needs fewer cycles per chain step than the step's own VALU issue "
+                   "(~10.75 VALU x 4.4-5.4 cycles for one wave alone): out of reach for this "
+                   "column-split decomposition; DESIGN.md 5",
+    }
+
+
 def pair(A, n: int, m: int):
     """main.cpp's `-r L L` pair (L = max(n, m); exactly the reference inputs at 65536),
     cut to n x m."""
@@ -292,6 +343,12 @@ def construct_bench(args):
                              "affine_local" if kind == "local" else "affine",
                              f"fill_affine_kernel<{kind}> construct {n}x{m}"),
     }
+    if args.config == 2:
+        out["roofline"]["chain_model"] = chain_model(n, m, fill_ms / max(args.steps, 1), elapsed * 1e3 / args.steps)
+        out["roofline"]["binding"] = (
+            "band-chain latency: the construct's critical path is sum over the Hirschberg levels of "
+            "(cols + 1.28 rows) band steps (chain_model), each step one wave's instruction issue; "
+            "DESIGN.md 3.5 / 5")
     if not args.no_cpu_baseline:
         from oracle import oracle as O
         side = 16384 if args.config == 2 else 8192
