@@ -701,7 +701,7 @@ void fill_collect(FillCtx& C) {
                 for (size_t i = 0; i < ev.size(); i += 16) {
                     if (!ev[i + 3] && !ev[i]) continue;
                     fprintf(g, "%zu", i / 16);
-                    for (int k = 0; k < 13; ++k) fprintf(g, " %llu", ev[i + k]);
+                    for (int k = 0; k < 15; ++k) fprintf(g, " %llu", ev[i + k]);
                     fprintf(g, "\n");
                 }
                 fclose(g);

@@ -826,6 +826,16 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
     const GLOBAL_AS uint8_t* sg = gmem(s);
     int s_next = 0, sk_next = 0, in_gran = 0;
     int st_lim = 0;   // subject chunks whose loads are issued (s_next: stored in the ring)
+    // io_skew < 0: DIAGNOSTIC timing only -- no subject staging and no skewed copy (the
+    // compute waves read whatever the LDS holds: wrong scores), to time the hand-off path
+    // without the I/O wave's subject work (round 5)
+    if (io_skew < 0) {
+        s_next = st_lim = nchunks;
+        sk_next = SKEW ? nskew : 0;
+        lds_st(s_filled, (uint32_t)nskew);
+        io_skew = 8;
+    }
+
     uint8_t sv[4];    // the loaded, not yet stored subject bytes (4 x 64 columns)
     T qv[2] = {HandOff<T>::zero(), HandOff<T>::zero()};   // io_poll2: the poll in flight
     int q_lim = 0, q_base = 0;
@@ -2026,7 +2036,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                                     P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc, 2, 2, fp.prio == 3,
                                     fp.dbg && first < 2048 ? fp.dbg + 16 + 4 * 4096 + 16 * (first + (P.q_step < 0 ? 2048 : 0))
                                                            : nullptr,
-                                    fp.io_stage, fp.io_skew > 0 ? fp.io_skew : kIoSkewPolling, fp.io_poll2 != 0);
+                                    fp.io_stage, fp.io_skew != 0 ? fp.io_skew : kIoSkewPolling, fp.io_poll2 != 0);
         } else {
             const int band = first + wave;
             if (band <= last) {

@@ -448,6 +448,26 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
         e(f"global_store_dwordx2 v{B_VT2}, v[138:139], %[dbp] offset:{8 * slot}")
         e(f"L_ev{slot}{k}_%=:")
 
+    def event_last(k, slot, add):
+        """Diagnostic build, band-end variants: when 2b + add is the band's last half
+        (nch), store s_memrealtime to dbp[slot] (consumer: the last half seen, add 2;
+        producer: the last half published, add -2)."""
+        if not (ts and epi):
+            return
+        e("s_lshl_b32 %[x2], %[b], 1")
+        e(f"s_add_u32 %[x2], %[x2], {add & 0xffffffff}")
+        e("s_cmp_eq_u32 %[x2], %[nch]")
+        e(f"s_cbranch_scc0 L_evl{slot}{k}_%=")
+        e("s_cmp_lg_u64 %[dbp], 0")
+        e(f"s_cbranch_scc0 L_evl{slot}{k}_%=")
+        e(f"s_memrealtime s[{TB}:{TB + 1}]")
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"v_mov_b32_e32 v138, s{TB}")
+        e(f"v_mov_b32_e32 v139, s{TB + 1}")
+        e(f"v_mov_b32_e32 v{B_VT2}, 0")
+        e(f"global_store_dwordx2 v{B_VT2}, v[138:139], %[dbp] offset:{8 * slot}")
+        e(f"L_evl{slot}{k}_%=:")
+
     def count_miss(k, tag):
         if ts:   # diagnostic: hand-off waits (block start or step 14)
             e("s_cmp_ge_u32 %[sp], %[x4]")
@@ -580,6 +600,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
                     count_miss(k, "b")
                     wait(e, f"pb{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
                     event(k, 5, EVB)      # consumer: second half seen
+                    event_last(k, 13, 2)  # consumer: the band's last half seen
                 top_reads(1)
             if LEAN:
                 # lean: reads 0-3 of the first half by step 1, 4-7 by step 9 (the subject
@@ -685,6 +706,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
         if pub != "none":
             publish(k, 1, AO0 + 6)                 # pair of step 31: steps 16..31 in lanes 48..63
             event(k, 2, EVB + 2)                   # producer: second half published
+            event_last(k, 14, -2)                  # producer: the band's last half published
         event(k, 6, EVB)                           # consumer: block EVB ends
         if not LEAN or k == 1:
             # (lean: every other block -- a consumption counter one block behind only

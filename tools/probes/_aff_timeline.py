@@ -100,6 +100,21 @@ if os.path.exists(path + ".ev"):
         if tr:
             print(f"  {front}: main loop end -> epilogue entry median {np.median(tr):.3f} us; epilogue "
                   f"{np.median(ep):.3f} us; epilogue end -> band end {np.median(tl):.3f} us")
+        # the band end (round 5): producer publishes its last half (slot 14) -> consumer
+        # sees it (slot 13) -> consumer's loop end (steady end, the timeline file)
+        se_of = {}
+        for r in rows_:
+            se_of[int(float(r[0]))] = float(r[2])
+        lh = []
+        for k in range(1, 2048):
+            v, p = ev.get(off + k), ev.get(off + k - 1)
+            if v and p and len(v) > 14 and len(p) > 14 and v[13] and p[14] and v[13] > p[14]:
+                lh.append(((v[13] - p[14]) / 100.0, k % NW == 0))
+        if lh:
+            a = np.array([x[0] for x in lh]); hb = np.array([x[1] for x in lh])
+            print(f"  {front} band end: producer's last half published -> consumer sees it: LDS hop median "
+                  f"{np.median(a[~hb]):.3f} us, HBM hop median {np.median(a[hb]):.3f} us (n {len(a)})")
+            t13 = {k: ev[off + k][13] / 100.0 for k in range(2048) if ev.get(off + k) and len(ev[off + k]) > 14 and ev[off + k][13]}
         kinds = np.array(kinds)
         for name, sel in (("LDS", ~kinds), ("HBM", kinds)):
             if sel.sum() == 0:
