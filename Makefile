@@ -38,10 +38,12 @@ anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o
 # experimental build for A/B runs: the affine loop generated under other generator knobs
 # (EXPGEN, e.g. `make exp EXPGEN="ANYSEQ_GEN_LEAN=0"`) as anyseq_amd/libanyseq_exp.so,
 # loaded with ANYSEQ_LIB
+# (EXPDEF: extra -D flags of the kernels, e.g. EXPGEN="ANYSEQ_GEN_GS=0" EXPDEF=-DANYSEQ_AFF_GS=0)
 EXPGEN ?= ANYSEQ_GEN_LEAN=1
+EXPDEF ?=
 exp:
 	mkdir -p build && env $(EXPGEN) python3 tools/gen_block_asm.py build/exp_asm.inc > /dev/null
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_ASM_INC='"$(CURDIR)/build/exp_asm.inc"' -c $(SRC)/anyseq_kernels.hip -o build/anyseq_kernels_exp.o
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(EXPDEF) -DANYSEQ_ASM_INC='"$(CURDIR)/build/exp_asm.inc"' -c $(SRC)/anyseq_kernels.hip -o build/anyseq_kernels_exp.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -Wl,-z,defs -o anyseq_amd/libanyseq_exp.so build/anyseq_kernels_exp.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
 clean:

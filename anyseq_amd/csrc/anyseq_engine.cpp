@@ -72,6 +72,7 @@ hipError_t anyseq_launch_aff_final(const AffFinalPlan* plan, const uint8_t* Q, c
 hipError_t anyseq_launch_aff_level_tail(const void* tail, int fill_groups, hipStream_t st);
 hipError_t anyseq_launch_rows_check(const void* rows, size_t nwords, uint32_t sentinel, const void* probs, int nprobs,
                                     uint32_t* out, int inject, hipStream_t st);
+hipError_t anyseq_launch_aff_scode(const void* probs, int nprobs, int64_t max_w, hipStream_t st);
 hipError_t anyseq_launch_fill_prep_planned(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
                                            void* sent, size_t sent_max_bytes, uint32_t sent_value,
                                            const uint32_t* sent_n16, hipStream_t st);
@@ -407,6 +408,7 @@ void audit_probs(const std::vector<DPProblem>& probs, bool aff) {
         if (P.left_flag && P.left_chunk > 0)
             check_range(P.left_flag, (size_t)((P.h + P.left_chunk - 1) / P.left_chunk) * 4, "left_flag");
         check_range(P.progress, 4, "progress");
+        if (P.scode) check_range(P.scode, (size_t)(4 * scode_len(P.w)), "subject-code rows");
     }
 }
 
@@ -514,6 +516,23 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
         ro += (size_t)(P.ngroups > 1 ? P.nslots : 0) * P.wpad * vpc;
         fo += P.ngroups;
     }
+    // affine: every problem's subject-code rows (DPProblem::scode), built on the device
+    // right after the descriptors land (aff_scode_kernel)
+    int64_t scode_max_w = 0;
+    if (aff) {
+        size_t sb = 0;
+        for (const auto& P : probs)
+            if (P.h > 0 && P.w > 0) sb += (size_t)(4 * scode_len(P.w));
+        uint8_t* sc = (uint8_t*)C.scode.get(std::max<size_t>(sb, 16));
+        size_t so = 0;
+        for (auto& P : probs) {
+            P.scode = nullptr;
+            if (P.h <= 0 || P.w <= 0) continue;
+            P.scode = sc + so;
+            so += (size_t)(4 * scode_len(P.w));
+            scode_max_w = std::max<int64_t>(scode_max_w, P.w);
+        }
+    }
     // the digest covers every word of the final descriptor (pointers included)
     for (size_t i = 0; i < probs.size(); ++i) {
         probs[i].pad_ = 0;
@@ -549,6 +568,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     // (the kernel also copies the descriptors in from the pinned staging area)
     HIPCHECK(anyseq_launch_fill_prep(ctr, (int)(32 + flag_words), init, init_words, init_value, rowbuf,
                                      rowbuf_ints * 4, aff ? 0x80808080u : 0xffffffffu, pin + 64, meta + zb, ub, st));
+    if (aff) HIPCHECK(anyseq_launch_aff_scode(d_probs, (int)probs.size(), scode_max_w, st));
     FillParams fpl = fp;
     fpl.epoch = epoch;
     fpl.xq = xrun > 0 ? reinterpret_cast<const uint32_t*>(d_groups + groups.size()) : nullptr;
@@ -1322,6 +1342,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             HIPCHECK(hipMemsetD32Async(rowbuf, 0x80808080, E.pl_rowbuf.cap / 4, st));
         E.pl_dirty = true;   // until this call has checked its error words
         int32_t* rowpool = (int32_t*)E.outrow.get(std::max<size_t>(max_rowpool, 16));
+        // subject-code rows of a level's halves: sum of 4 scode_len(w) <= 4 (2n + m + 192 halves)
+        // (a half's w is its part's rows or its width; the parts' rows and widths are disjoint)
+        const size_t scode_cap = 4 * ((size_t)2 * n + (size_t)m + 192 * (size_t)(2 * max_parts)) + 16;
+        uint8_t* scode_rows = (uint8_t*)E.pl_scode.get(scode_cap);
         PartInfo* d_parts = (PartInfo*)E.pl_parts.get((size_t)max_parts * sizeof(PartInfo));
         RowToCol* d_jobs = (RowToCol*)E.pl_jobs.get((size_t)2 * max_parts * sizeof(RowToCol));
         int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * max_parts * 4);
@@ -1409,6 +1433,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             A.hdr = d_hdr + 8 * li;
             A.xrun = xcd_run(E, L.grid, true);
             A.xq = reinterpret_cast<uint32_t*>(d_groups + L.slots);
+            A.scode = scode_rows;
+            A.scode_cap = (int64_t)scode_cap;
         }
         // level 1: plan + prep; every level: fill, then one tail launch (join, next level's
         // sentinel rows, counters, best cells and plan)
@@ -1434,6 +1460,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             fpl.slack = g_tuning.slack;
             fpl.dbg = nullptr;
             fpl.xq = A.xrun > 0 ? A.xq : nullptr;
+            // the level's subject-code rows, from the descriptors its plan just wrote
+            HIPCHECK(anyseq_launch_aff_scode(d_probs, L.nh, std::max(n, m), st));
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li], st));
             HIPCHECK(anyseq_launch_fill_affine(L.nw, d_probs, d_groups, L.slots, ctr, d_err + li, &fpl, L.grid, st));
             HIPCHECK(hipEventRecord(E.pl_ev[2 * li + 1], st));

@@ -115,6 +115,7 @@ int process_hw_queues();
 struct FillCtx {
     DevBuf probs;                           // launch block: counters | flags | descriptors | groups | extra
     DevBuf groups, rowbuf, flags, ctr;      // (groups, flags: unused since the launch block; ctr: result words)
+    DevBuf scode;                           // affine: the problems' subject-code rows (DPProblem::scode)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int R = 1, NW = 4;
     unsigned long long* stamps = nullptr;   // diagnostic build only
@@ -161,6 +162,7 @@ struct Engine {
     // affine construct, device-planned levels: launch block, hand-off rows, part table,
     // row-to-column jobs, per-level header and error words (+ their pinned download)
     DevBuf pl_meta, pl_rowbuf, pl_parts, pl_jobs, pl_hdr;
+    DevBuf pl_scode;           // the planned levels' subject-code rows (DPProblem::scode)
     PinBuf pl_pin;
     std::vector<hipEvent_t> pl_ev;
     bool pl_dirty = true;      // pl_rowbuf may hold non-sentinel words (fresh, or a failed call)

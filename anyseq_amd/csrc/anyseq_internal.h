@@ -61,12 +61,19 @@ struct DPProblem {
     int32_t amode;
     uint32_t* progress;
     uint32_t* stage;       // diagnostics (ANYSEQ_SHARD_DEBUG): per-band stage reached
+    // Affine fill (round 5): the problem's subject codes as the compute waves read them
+    // from HBM -- column c at byte c + 64 of a padded row (code 0xFF left of column 0 and
+    // from column w on), in four copies shifted by 0..3 bytes (scode_len(w) bytes each), so
+    // a lane's 32 codes of a block are two dword-aligned 16-byte loads (aff_scode_kernel).
+    const uint8_t* scode;
     // kProbMagic ^ (index in the launch's problem table) ^ (epoch << 12), set by
     // fill_prepare: a fill group checks it before it uses any pointer of the descriptor
     int32_t magic;
     int32_t pad_;
 };
 constexpr int32_t kProbMagic = 0x5eb1a700;
+// bytes of one shifted copy of DPProblem::scode (columns -64 .. 32 ceil(w/32) + 95)
+__host__ __device__ inline int64_t scode_len(int w) { return 32 * (int64_t)((w + 31) / 32) + 160; }
 
 // Digest of a descriptor's words before `magic` (FNV-1a over 32-bit words).  magic =
 // kProbMagic ^ index ^ (epoch << 12) ^ digest: a fill group recomputes it from the
@@ -258,6 +265,8 @@ struct AffLevelPlan {
     // 9 offsets at xq (run: consecutive groups per XCD, the grid / 8)
     int32_t xrun;
     uint32_t* xq;
+    uint8_t* scode;   // the level's subject-code rows (DPProblem::scode), packed by the plan
+    int64_t scode_cap;   // their bytes (a plan that needs more fails the level's bound check)
 };
 
 // The tail of a device-planned level, one launch: the join of level L

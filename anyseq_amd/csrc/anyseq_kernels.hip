@@ -811,7 +811,7 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
                         uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
                         uint32_t* cons0, uint32_t* err, bool reset_in = false, int ext = 0, int pscale = 1,
                         bool hprio = false, unsigned long long* evp = nullptr, int io_stage = 3,
-                        int io_skew = kIoSkewPolling, bool io_poll2 = false) {
+                        int io_skew = kIoSkewPolling, bool io_poll2 = false, bool no_subject = false) {
     constexpr int IRM = kSlots * CH - 1;
     constexpr int SCH = kSRing / CH;   // chunks held by the subject ring
     constexpr int GR = 16;             // hand-off poll granule (columns)
@@ -826,10 +826,11 @@ __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step
     const GLOBAL_AS uint8_t* sg = gmem(s);
     int s_next = 0, sk_next = 0, in_gran = 0;
     int st_lim = 0;   // subject chunks whose loads are issued (s_next: stored in the ring)
-    // io_skew < 0: DIAGNOSTIC timing only -- no subject staging and no skewed copy (the
-    // compute waves read whatever the LDS holds: wrong scores), to time the hand-off path
-    // without the I/O wave's subject work (round 5)
-    if (io_skew < 0) {
+    // no_subject: the compute waves read their codes from HBM (DPProblem::scode, round 5):
+    // no subject staging and no skewed copy, only the hand-off rows.  (io_skew < 0 on the
+    // LDS path: the same, as a DIAGNOSTIC that times the hand-off without the subject work
+    // -- the compute waves then read stale LDS: wrong scores.)
+    if (no_subject || io_skew < 0) {
         s_next = st_lim = nchunks;
         sk_next = SKEW ? nskew : 0;
         lds_st(s_filled, (uint32_t)nskew);
@@ -1321,6 +1322,14 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_kernel(const DPProblem* __
 // Problems with amode 0 run the plain steady-state loop (11 VALU per step), the
 // others the clamp + best loop (14).
 constexpr int kAffNeg = -(1 << 29);   // "minus infinity" of the E/F states (the oracle's AFF_NEG_INF)
+// Round 5: the compute waves read their subject codes from the problem's code rows in
+// HBM (DPProblem::scode, two 16-byte loads per lane and block) instead of the I/O wave's
+// pre-skewed LDS copy, so the I/O wave only forwards the hand-off rows.
+// 0: the round-4 LDS path (A/B builds, tools/gen_block_asm.py GS=0).
+#ifndef ANYSEQ_AFF_GS
+#define ANYSEQ_AFF_GS 1
+#endif
+constexpr bool kAffGS = ANYSEQ_AFF_GS != 0;
 
 struct AffK {
     int wm, wx;   // diagonal weight sub - 2 ge
@@ -1434,6 +1443,7 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
 struct Aff2Args {
     uint32_t rb, nb, apr, acn, anp, anc, asf, atl, skb, lo, lid8, bvb, bvs, thr, neg;
     uint64_t gp;
+    uint64_t sg;   // GS: the problem's subject-code rows (skb: the lane's byte offset at block 0)
     int q, wm, wx, ll, lh, zlp;
 };
 #ifdef ANYSEQ_STAMPS
@@ -1453,7 +1463,7 @@ struct Aff2Args {
                    [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
                    [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
-                   [hm] "s"(hm), [gp] "s"(gp), [thr] "s"(thr)                                                  \
+                   [hm] "s"(hm), [gp] "s"(gp), [thr] "s"(thr), [sg] "s"(sg)                                    \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
 // the band's last blocks (gen_aff2 epi): + the column-(w-1) capture and the poll clamp
 #define AF2E_ASM(NAME)                                                                                          \
@@ -1466,7 +1476,7 @@ struct Aff2Args {
                    [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
                    [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
-                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr)                                  \
+                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr), [sg] "s"(sg)                    \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
 // the band's last blocks without the column-(w-1) capture (gen_aff2 cap=False)
 #define AF2F_ASM(NAME)                                                                                          \
@@ -1479,7 +1489,7 @@ struct Aff2Args {
                    [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
                    [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
-                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr), [neg] "s"(negp)                 \
+                   [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr), [neg] "s"(negp), [sg] "s"(sg)    \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
 // EPI: 0 the steady state, 1 the band's last blocks with the capture, 2 without it
 template <bool L, bool BORDER, int PUB, bool LUT, int EPI = 0>
@@ -1499,6 +1509,7 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
     const uint32_t rb = RFL(a.rb), nb = RFL(a.nb), bvs = RFL(a.bvs), thr = RFL(a.thr);
     const int ge = RFL(-nge);
     const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(a.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)a.gp);
+    const uint64_t sg = ((uint64_t)(uint32_t)RFL((uint32_t)(a.sg >> 32)) << 32) | (uint32_t)RFL((uint32_t)a.sg);
 #ifdef ANYSEQ_STAMPS
     ts_f = RFL(ts_f);
     nmiss = RFL(nmiss);
@@ -1602,6 +1613,10 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     // settle the query load here: a vmcnt wait inside the step loop would also wait
     // for lane 63's HBM row stores
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(q)::"memory");
+    if (kAffGS && !P.scode) {   // (a planned level whose code rows did not fit: its bound check fails too)
+        if (lane == 0) atomicOr(err, ERR_BAD_DESC);
+        return;
+    }
     int g, e = kAffNeg, hg, fdn = kAffNeg, dg;
     int2 tf;
     if (shard_left) {
@@ -1668,6 +1683,15 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         la.lid8 = 8u * lane;
         la.thr = (uint32_t)max(k.thr, 0);   // band 0's pace (FillParams::throttle)
         la.neg = lds_addr(io.neg);
+        if constexpr (kAffGS) {
+            // the lane's 32 codes of block b: columns 32b-1-lane .. 32b+30-lane, i.e. row
+            // bytes i .. i+31 with i = 32b + 63 - lane, from the copy shifted by i & 3
+            const int i0 = 63 - lane, r = i0 & 3;
+            la.skb = (uint32_t)(r * scode_len(w) + (i0 - r));
+            la.sg = (uint64_t)(size_t)P.scode;
+        } else {
+            la.sg = 0;
+        }
         // band 0's top border (value, value + go) in the loop's space
         la.bvb = (uint32_t)(xs ? to_x(B.top(lane, nge), lane) : B.top(lane, nge));
         la.bvs = (uint32_t)(B.top(1, nge) - B.top(0, nge) - (xs ? nge : 0));
@@ -1823,11 +1847,19 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 continue;
             }
         }
-        if (b < nchunks && seen_sfill < (uint32_t)(b + 1)) {
-            if (!(seen_sfill = spin_lds_ge(io.s_filled, (uint32_t)(b + 1), err))) return;
-        }
         uint32_t sw[8];
-        load_sbytes<CH>(io.s_ring, (t0 - 1 - lane) & (kSRing - 1), sw);
+        if constexpr (kAffGS) {
+            const int i0 = t0 + 63 - lane, r = i0 & 3;
+            const GLOBAL_AS uint32_t* src =
+                reinterpret_cast<const GLOBAL_AS uint32_t*>(gmem(P.scode) + r * scode_len(w) + (i0 - r));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sw[i] = src[i];
+        } else {
+            if (b < nchunks && seen_sfill < (uint32_t)(b + 1)) {
+                if (!(seen_sfill = spin_lds_ge(io.s_filled, (uint32_t)(b + 1), err))) return;
+            }
+            load_sbytes<CH>(io.s_ring, (t0 - 1 - lane) & (kSRing - 1), sw);
+        }
         int2 rv[CH];
         if (b < nchunks) {
             if (io.in_border) {
@@ -2036,7 +2068,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                                     P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc, 2, 2, fp.prio == 3,
                                     fp.dbg && first < 2048 ? fp.dbg + 16 + 4 * 4096 + 16 * (first + (P.q_step < 0 ? 2048 : 0))
                                                            : nullptr,
-                                    fp.io_stage, fp.io_skew != 0 ? fp.io_skew : kIoSkewPolling, fp.io_poll2 != 0);
+                                    fp.io_stage, fp.io_skew != 0 ? fp.io_skew : kIoSkewPolling, fp.io_poll2 != 0,
+                                    kAffGS);
         } else {
             const int band = first + wave;
             if (band <= last) {
@@ -2721,6 +2754,7 @@ struct AffHalfGeo {
     int32_t tr, ngroups, nslots, wpad;
     int64_t rowbuf;        // hand-off ring ints
     int64_t rowpool;       // transposed bottom row ints
+    int64_t scode;         // subject-code row bytes (DPProblem::scode)
 };
 __device__ AffHalfGeo aff_half_geo(const AffLevelPlan& a, int len, int width) {
     AffHalfGeo g{};
@@ -2734,6 +2768,7 @@ __device__ AffHalfGeo aff_half_geo(const AffLevelPlan& a, int len, int width) {
     g.nslots = max(1, min(g.ngroups - 1, a.want_slots));
     g.rowbuf = g.ngroups > 1 ? (int64_t)g.nslots * g.wpad * 2 : 0;
     g.rowpool = g.tr ? (int64_t)((len + 63) & ~63) * 2 : 0;
+    g.scode = 4 * scode_len(g.w);
     return g;
 }
 
@@ -2777,7 +2812,7 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
     // kind != global with a level-1 value <= 0: the empty alignment, no halves
     const bool stop = a.score && a.kind != KIND_GLOBAL && *a.score <= 0;
     RowToCol* jobs = a.jobs;
-    int64_t rb_base = 0, rp_base = 0;
+    int64_t rb_base = 0, rp_base = 0, sc_base = 0;
     for (int t0 = 0; t0 < a.parts; t0 += blockDim.x) {
         const int p = t0 + (int)threadIdx.x;
         PartInfo pi{};
@@ -2816,11 +2851,13 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
             a.parts_out[p] = pi;
             if (gl.ngroups > a.bound || gr.ngroups > a.bound) atomicOr(&bad, 1);
         }
-        int64_t tot_rb, tot_rp;
+        int64_t tot_rb, tot_rp, tot_sc;
         const int64_t rb = rb_base + block_scan_excl(gl.rowbuf + gr.rowbuf, sh, &tot_rb);
         const int64_t rp = rp_base + block_scan_excl(gl.rowpool + gr.rowpool, sh, &tot_rp);
+        const int64_t sco = sc_base + block_scan_excl(gl.scode + gr.scode, sh, &tot_sc);
         rb_base += tot_rb;
         rp_base += tot_rp;
+        sc_base += tot_sc;
         if (p < a.parts) {
             for (int side = 0; side < 2; ++side) {
                 const AffHalfGeo& g = side ? gr : gl;
@@ -2874,6 +2911,8 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
                     P.wpad = g.wpad;
                     P.nslots = g.nslots;
                     P.rowbuf = a.rowbuf + rb + (side ? gl.rowbuf : 0);
+                    const int64_t so = sco + (side ? gl.scode : 0);
+                    P.scode = a.scode && so + g.scode <= a.scode_cap ? a.scode + so : nullptr;
                     atomicAdd(&cells, (unsigned long long)((int64_t)g.h * g.w));
                 } else {
                     P.nslots = 1;
@@ -2929,7 +2968,7 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
     __syncthreads();
     if (threadIdx.x == 0) {
         a.hdr[0] = (uint32_t)(rb_base / 4);   // sentinel uint4s (every ring is a multiple of 128 ints)
-        a.hdr[1] = (uint32_t)bad;
+        a.hdr[1] = (uint32_t)(bad || sc_base > a.scode_cap);
         reinterpret_cast<unsigned long long*>(a.hdr)[1] = cells;
     }
 }
@@ -3901,6 +3940,42 @@ hipError_t anyseq_launch_fill_prep(uint32_t* zero, int nzero, int32_t* init, int
     const int blocks = (int)std::max<size_t>(1, std::min<size_t>(2048, (work + 255) / 256));
     hipLaunchKernelGGL(anyseq::fill_prep_kernel, dim3(blocks), dim3(256), 0, st, zero, nzero, init, ninit, init_value,
                        (uint4*)sent, n16, sent_value, (const uint4*)up_src, (uint4*)up_dst, nup, (const uint32_t*)nullptr);
+    return hipGetLastError();
+}
+
+// The subject-code rows of an affine launch's problems (DPProblem::scode): problem
+// blockIdx.y, grid-stride over its 4 shifted copies in dwords.  Column c sits at byte
+// c + 64 of copy 0; copy r holds the row shifted left by r bytes.  Codes 0xFF outside
+// [0, w): the virtual prologue's columns and the asm band end's columns past w.
+namespace anyseq {
+__global__ __launch_bounds__(256) void aff_scode_kernel(const DPProblem* __restrict__ probs, int nprobs) {
+    const DPProblem& P = probs[blockIdx.y];
+    if ((int)blockIdx.y >= nprobs || P.h <= 0 || P.w <= 0 || !P.scode) return;
+    const int64_t L = scode_len(P.w);
+    const int64_t nd = L / 4;   // dwords per copy (L is a multiple of 16)
+    const GLOBAL_AS uint8_t* s = gmem(P.s);
+    uint32_t* out = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(P.scode));
+    for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < 4 * nd; d += (int64_t)gridDim.x * blockDim.x) {
+        const int r = (int)(d / nd);
+        const int64_t c0 = (d % nd) * 4 - 64 + r;   // column of the dword's first byte
+        uint32_t v = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t c = c0 + t;
+            const uint32_t b = (c >= 0 && c < P.w) ? s[P.s_off + (int64_t)P.s_step * c] : 0xffu;
+            v |= b << (8 * t);
+        }
+        out[d] = v;
+    }
+}
+}  // namespace anyseq
+
+hipError_t anyseq_launch_aff_scode(const void* probs, int nprobs, int64_t max_w, hipStream_t st) {
+    if (nprobs <= 0) return hipSuccess;
+    const int64_t per = (4 * anyseq::scode_len((int)std::min<int64_t>(max_w, INT32_MAX - 256)) / 4 + 255) / 256;
+    const int bx = (int)std::max<int64_t>(1, std::min<int64_t>(per, std::max(1, 2048 / nprobs)));
+    hipLaunchKernelGGL(anyseq::aff_scode_kernel, dim3(bx, nprobs), dim3(256), 0, st,
+                       (const anyseq::DPProblem*)probs, nprobs);
     return hipGetLastError();
 }
 

@@ -334,6 +334,10 @@ SLIM = int(os.environ.get("ANYSEQ_GEN_SLIM", "1"))
 # 61.9 -> 58.1 cycles per step (X space, LDS publisher), configs[2] 517 -> 535 GCUPS.
 # 2 = also the subject-prefetch wait every other block (r05f: configs[2] 544 -> 551 GCUPS).
 LEAN = int(os.environ.get("ANYSEQ_GEN_LEAN", "2"))
+# gen_aff2 subject codes (round 5): 1 = two 16-byte loads per lane and block from the
+# problem's code rows in HBM (DPProblem::scode; kernel ANYSEQ_AFF_GS 1), issued one block
+# ahead; 0 = the I/O wave's pre-skewed LDS copy (ds_read2st64 at step 8, an s_filled wait)
+GS = int(os.environ.get("ANYSEQ_GEN_GS", "1"))
 AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
@@ -374,6 +378,19 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     out = []
     e = out.append
     sets = (B_SK0, B_SK1)
+
+    def code_loads(breg, dst):
+        """GS: the lane's 32 subject codes of block `breg` into v[dst .. dst+7]: row bytes
+        %[skb] + 32 breg (two dword-aligned 16-byte loads from the code rows %[sg])."""
+        e(f"s_lshl_b32 %[x2], {breg}, 5")
+        e(f"v_add_u32_e32 v{B_VA}, %[x2], %[skb]")
+        e(f"global_load_dwordx4 v[{dst}:{dst + 3}], v{B_VA}, %[sg]")
+        e(f"global_load_dwordx4 v[{dst + 4}:{dst + 7}], v{B_VA}, %[sg] offset:16")
+
+    # GS: VMEM operations a block issues after its code loads (the vmcnt a block waits
+    # with for its own codes): the glob publisher's two half stores; the diagnostic
+    # build's event stores are not counted (it waits for all)
+    code_wait = 0 if ts else (2 if pub == "glob" else 0)
 
     def top_reads(half):
         """8 ds_read_b128 of top-row pairs [16*half, 16*half+16) (chunk address in VB)."""
@@ -536,6 +553,20 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
         event(k, 4, EVB)              # consumer: first half of chunk EVB seen
         ring_addr("%[b]")
         top_reads(0)
+        if GS:
+            # this block's codes (loaded one block ago), then the next block's.  The glob
+            # publisher stores its halves from block 2 on: blocks 0..2 wait for all.
+            if code_wait:
+                e("s_cmp_lt_u32 %[b], 3")
+                e(f"s_cbranch_scc1 L_cw0{k}_%=")
+                e(f"s_waitcnt vmcnt({code_wait})")
+                e(f"s_branch L_cwd{k}_%=")
+                e(f"L_cw0{k}_%=:")
+                e("s_waitcnt vmcnt(0)")
+                e(f"L_cwd{k}_%=:")
+            else:
+                e("s_waitcnt vmcnt(0)")
+            code_loads("%[x1]", ns)
         if ts:
             e("s_cmp_lg_u32 %[tsf], 0")
             e(f"s_cbranch_scc1 L_nots{k}_%=")
@@ -563,9 +594,12 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
             dg = TG_(30)
             if pub == "none":
                 g, f = OG_(31), OF_(31)
-        nsub = 5 if border else 4   # subject reads (+ the border write) at step 8
+        nsub = (0 if GS else 4) + (1 if border else 0)   # subject reads (+ the border write) at step 8
         for u in range(32):
-            if u == 8:
+            if u == 8 and GS:
+                if border:
+                    border_write("%[x1]")
+            elif u == 8:
                 # next block's subject codes (other register set) and, band 0, its border.
                 # Issued in every block (after the last one they read a stale slot, unused):
                 # the counted lgkmcnt waits assume they are in flight.
@@ -720,15 +754,20 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
 
     # the first block's subject codes into set 0 (band 0: and its border)
     e("s_add_u32 %[x1], %[b], 1")
-    wait(e, "sfp", "%[sf]", "%[x1]", "%[asf]", tmp=B_VT2)
-    e("s_and_b32 %[x2], %[b], 31")
-    e("s_lshl_b32 %[x2], %[x2], 11")
-    e(f"v_add_u32_e32 v{B_VA}, %[x2], %[skb]")
-    for i in range(4):
-        e(f"ds_read2st64_b32 v[{B_SK0 + 2 * i}:{B_SK0 + 2 * i + 1}], v{B_VA} offset0:{2 * i} offset1:{2 * i + 1}")
+    if GS:
+        code_loads("%[b]", B_SK0)
+    else:
+        wait(e, "sfp", "%[sf]", "%[x1]", "%[asf]", tmp=B_VT2)
+        e("s_and_b32 %[x2], %[b], 31")
+        e("s_lshl_b32 %[x2], %[x2], 11")
+        e(f"v_add_u32_e32 v{B_VA}, %[x2], %[skb]")
+        for i in range(4):
+            e(f"ds_read2st64_b32 v[{B_SK0 + 2 * i}:{B_SK0 + 2 * i + 1}], v{B_VA} offset0:{2 * i} offset1:{2 * i + 1}")
     if border:
         border_write("%[b]")
     e("s_waitcnt lgkmcnt(0)")
+    if GS:
+        e("s_waitcnt vmcnt(0)")
     # lean: the loop-carried diagonal / top values (and without publishing, the cell
     # pair) live in the rotation's registers; the ring slot of the first block's
     # publish is checked here (the loop checks every other block)
@@ -738,7 +777,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     if LEAN:
         for named, reg in lean_regs:
             e(f"v_mov_b32_e32 {reg}, {named}")
-        if LEAN >= 2:
+        if LEAN >= 2 and not GS:
             e("s_add_u32 %[x4], %[b], 2")
             e("s_min_u32 %[x4], %[x4], %[be]")
             wait(e, "sfe", "%[sf]", "%[x4]", "%[asf]", tmp=B_VT2)
