@@ -306,6 +306,7 @@ void init_tuning_locked() {
     g_tuning.io_stage = env_int("ANYSEQ_IO_STAGE", g_tuning.io_stage);
     g_tuning.io_skew = env_int("ANYSEQ_IO_SKEW", g_tuning.io_skew);
     g_tuning.io_poll2 = env_int("ANYSEQ_IO_POLL2", g_tuning.io_poll2);
+    g_tuning.io_fwd = env_int("ANYSEQ_IO_FWD", g_tuning.io_fwd);
     g_tuning.virtbest = env_int("ANYSEQ_VIRT_BEST", g_tuning.virtbest);
     g_tuning.devplan = env_int("ANYSEQ_AFF_DEVPLAN", g_tuning.devplan);
     g_tuning.devfinal = env_int("ANYSEQ_AFF_DEVFINAL", g_tuning.devfinal);
@@ -778,6 +779,7 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     fp.io_stage = g_tuning.io_stage;
     fp.io_skew = g_tuning.io_skew;
     fp.io_poll2 = g_tuning.io_poll2;
+    fp.io_fwd = g_tuning.io_fwd;
     return fp;
 }
 
@@ -2159,6 +2161,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "io_stage") g_tuning.io_stage = value;
     else if (n == "io_skew") g_tuning.io_skew = value;
     else if (n == "io_poll2") g_tuning.io_poll2 = value;
+    else if (n == "io_forward") g_tuning.io_fwd = value;
     else if (n == "virtual_best") g_tuning.virtbest = value;
     else if (n == "affine_device_plan") g_tuning.devplan = value;
     else if (n == "affine_device_final") g_tuning.devfinal = value;

@@ -97,6 +97,7 @@ struct Tuning {
     int io_stage = 3;    // affine fill: the I/O wave's subject staging mode (io_wave; 0..3, r04o A/B)
     int io_skew = 0;     // affine fill: the I/O wave's skewed blocks per pass while a poll is out (0: 8)
     int io_poll2 = 0;    // affine fill: the I/O wave keeps two hand-off polls in flight
+    int io_fwd = 1;      // affine fill with code rows: the I/O wave as the plain forwarder (io_forward)
     int devplan = 1;     // affine construct: Hirschberg levels planned on the device (one download)
     int devfinal = 1;    // affine construct, device-planned: the final level's blocks built on the device too
     int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe

@@ -806,6 +806,101 @@ constexpr int kIoSkewPolling = ANYSEQ_IO_SKEW_POLLING;   // skewed blocks per I/
 #endif
 constexpr int kIoSleep = ANYSEQ_IO_SLEEP;   // s_sleep units of an affine I/O pass without progress
 
+// The affine I/O wave when the compute waves read their own subject codes (GS, round 5):
+// it only forwards the previous group's bottom row from the HBM hand-off row into wave
+// 0's LDS ring.  One poll of 128 columns (8 granules of 16, 2 loads per lane) is always
+// in flight; after a poll is consumed the next one goes out BEFORE the consumed granules
+// get their sentinel back, so the next poll's wait never covers those stores.  Same data
+// protocol as io_wave: a granule is in when none of its columns < w holds the sentinel;
+// ext: "minus infinity" past the last granule; pscale: ring counter units per chunk.
+template <typename T>
+__device__ void io_forward(int lane, int w, const T* g_in, T* ring0, uint32_t* prod0, uint32_t* cons0, uint32_t* err,
+                           bool reset_in, int ext, int pscale, bool hprio, unsigned long long* evp) {
+    constexpr int CH = 32, GR = 16, GPC = CH / GR, IRM = kSlots * CH - 1;
+    const int nchunks = (w + CH - 1) / CH, ngran = (w + GR - 1) / GR;
+    if (!g_in) return;
+    int in_gran = 0, plim = 0;
+    T pv[2];
+    uint32_t idle = 0;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#ifdef ANYSEQ_STAMPS
+    uint64_t t_poll = 0;
+#endif
+    auto issue = [&]() {
+        int lim = min(((int)lds_ld(cons0) + kSlots) * GPC, ngran);   // ring space
+        plim = min(lim, in_gran + 8);
+#ifdef ANYSEQ_STAMPS
+        t_poll = evp ? __builtin_amdgcn_s_memrealtime() : 0;
+#endif
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int col = in_gran * GR + i * 64 + lane;
+            pv[i] = col < plim * GR && col < w ? HandOff<T>::load(g_in + col) : HandOff<T>::zero();
+        }
+    };
+    issue();
+    while (in_gran < ngran) {
+        if (hprio) __builtin_amdgcn_s_setprio(3);
+        int ready = 0;
+        bool stop = false;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint64_t bad = __ballot(HandOff<T>::pending(pv[i]));
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int gi = in_gran + 4 * i + g;
+                if (!stop && gi < plim && ((bad >> (16 * g)) & 0xffffu) == 0u) ++ready;
+                else stop = true;
+            }
+        }
+        if (ready > 0) {
+#ifdef ANYSEQ_STAMPS
+            if (evp && lane == 0 && in_gran <= 2000 && in_gran + ready > 2000) {
+                evp[11] = __builtin_amdgcn_s_memrealtime();
+                evp[12] = t_poll;
+            }
+#endif
+            const int base = in_gran, c0 = in_gran * GR, c2 = (in_gran + ready) * GR;
+            const T done0 = pv[0], done1 = pv[1];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int col = base * GR + i * 64 + lane;
+                if (col >= c0 && col < c2) ring0[col & IRM] = i ? done1 : done0;
+            }
+            in_gran += ready;
+            if (ext && in_gran >= ngran) {   // (as io_wave: the last chunk's unpolled columns)
+                const int c = ngran * GR + lane;
+                if (c < nchunks * CH) ring0[c & IRM] = HandOff<T>::neg();
+            }
+            lds_st(prod0, in_gran >= ngran ? (uint32_t)(nchunks * pscale) : (uint32_t)(in_gran * pscale / GPC));
+            if (hprio) __builtin_amdgcn_s_setprio(0);
+            if (in_gran < ngran) issue();
+            if (reset_in) {   // whole granules, also past w (io_wave)
+                T* gw = const_cast<T*>(g_in);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int col = base * GR + i * 64 + lane;
+                    if (col >= c0 && col < c2) HandOff<T>::store(gw + col, HandOff<T>::sentinel());
+                }
+            }
+            idle = 0;
+        } else {
+            if (hprio) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_sleep(kIoSleep);
+            if ((++idle & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t_start > SPIN_TICKS || err_set(err))) {
+                atomicOr(err, ERR_SPIN_TIMEOUT | 8u);
+                lds_st(prod0, (uint32_t)(nchunks * pscale));
+                return;
+            }
+            issue();
+        }
+    }
+    if (reset_in) {   // (as io_wave: the producer's last chunk past w)
+        T* gw = const_cast<T*>(g_in);
+        for (int c = ngran * GR + lane; c < nchunks * CH; c += 64) HandOff<T>::store(gw + c, HandOff<T>::sentinel());
+    }
+}
+
 template <int CH, bool SKEW, typename T = int32_t>
 __device__ void io_wave(int lane, int w, const uint8_t* s, int s_off, int s_step, uint8_t* s_ring, uint32_t* skew,
                         uint32_t* s_filled, uint32_t* tail, const T* g_in, T* ring0, uint32_t* prod0,
@@ -2061,7 +2156,13 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
             g_out = rows + (size_t)(gr.group % P.nslots) * P.wpad;
         else if (P.out_row)
             g_out = reinterpret_cast<int2*>(P.out_row);
-        if (wave == NW) {
+        if (wave == NW && kAffGS && fp.io_fwd) {
+            const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
+            io_forward<int2>(lane, P.w, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
+                             P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc, 2, 2, fp.prio == 3,
+                             fp.dbg && first < 2048 ? fp.dbg + 16 + 4 * 4096 + 16 * (first + (P.q_step < 0 ? 2048 : 0))
+                                                    : nullptr);
+        } else if (wave == NW) {
             const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
             io_wave<32, true, int2>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0], &sh.s_filled,
                                     &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
