@@ -605,6 +605,26 @@ void fill_launch(FillCtx& C) {
         HIPCHECK(anyseq_launch_fill(C.R, g_tuning.CH, C.NW, C.d_probs, C.d_groups, C.ngroups, ctr, ctr + 1, &C.fp,
                                     C.grid, C.st));
     HIPCHECK(hipEventRecord(C.ev1, C.st));
+    // ANYSEQ_CHECK_ROWS (host-built affine launches, round 5): every ring that is reused
+    // within the launch (nslots < ngroups - 1: each reader puts the sentinel back) must
+    // be all sentinel again afterwards, as the device-planned levels' rows;
+    // 2 plants one stale word past w in the first such ring (the check's own test)
+    C.rows_checked = false;
+    const int check_rows = C.aff ? env_int("ANYSEQ_CHECK_ROWS", 0) : 0;
+    if (check_rows) {
+        uint32_t* w = (uint32_t*)C.rcheck.get(64);
+        HIPCHECK(hipMemsetAsync(w, 0, 64, C.st));
+        bool injected = false;
+        for (size_t i = 0; i < C.h_probs.size(); ++i) {
+            const DPProblem& P = C.h_probs[i];
+            if (P.ngroups <= 1 || P.nslots >= P.ngroups - 1) continue;
+            const bool inject = check_rows == 2 && !injected;
+            injected |= inject;
+            HIPCHECK(anyseq_launch_rows_check(P.rowbuf, (size_t)P.nslots * P.wpad * 2, 0x80808080u, C.d_probs + i, 1,
+                                              w, inject, C.st));
+            C.rows_checked = true;
+        }
+    }
     HIPCHECK(hipMemcpyAsync(C.err_host, ctr + 1, 4, hipMemcpyDeviceToHost, C.st));
     HIPCHECK(hipEventRecord(C.ev2, C.st));
 }
@@ -689,6 +709,13 @@ void fill_collect(FillCtx& C) {
     g_fill_launches += 1;
     g_fill_cells += C.cells;
     const uint32_t err = C.err_host ? *(volatile uint32_t*)C.err_host : 0u;
+    if (C.rows_checked && !err) {
+        uint32_t c[8];
+        HIPCHECK(hipMemcpy(c, C.rcheck.p, sizeof c, hipMemcpyDeviceToHost));
+        if (c[0])
+            fail("hand-off row invariant broken after a host-built fill: %u non-sentinel word(s), the first in a ring "
+                 "at word %u = ring slot %d, column %d (width %d)", c[0], c[1], (int)c[3], (int)c[4], (int)c[5]);
+    }
     if (dbg) {
         unsigned long long h[16];
         HIPCHECK(hipMemcpy(h, dbg, sizeof h, hipMemcpyDeviceToHost));

@@ -117,6 +117,8 @@ struct FillCtx {
     DevBuf probs;                           // launch block: counters | flags | descriptors | groups | extra
     DevBuf groups, rowbuf, flags, ctr;      // (groups, flags: unused since the launch block; ctr: result words)
     DevBuf scode;                           // affine: the problems' subject-code rows (DPProblem::scode)
+    DevBuf rcheck;                          // ANYSEQ_CHECK_ROWS: the hand-off row check's result words
+    bool rows_checked = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int R = 1, NW = 4;
     unsigned long long* stamps = nullptr;   // diagnostic build only

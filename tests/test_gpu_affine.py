@@ -224,3 +224,30 @@ def test_affine_xcd_groups(anyseq, oracle, kind):
     finally:
         anyseq.set_option("xcd_groups", 0)
         anyseq.set_option("affine_grid", 0)
+
+
+def test_affine_host_built_row_check(anyseq, oracle, monkeypatch):
+    """Verdict round 4, item 7: the hand-off row check also covers host-built affine
+    launches (score fronts, genome-length and sharded construct levels): with
+    ANYSEQ_CHECK_ROWS every ring reused within a launch (nslots < ngroups - 1, here forced
+    by an 8-workgroup grid) must be all sentinel again afterwards; =2 plants a stale word
+    past w in the first such ring and the call must fail naming it, and the next call must
+    be right."""
+    rng = random.Random(32)
+    q, s = rnd(rng, 20000), rnd(rng, 500)
+    sc = (2, -1, -2, -1)
+    want = ora(oracle, "local", q, s, sc)
+    anyseq.set_option("affine_grid", 8)
+    try:
+        monkeypatch.setenv("ANYSEQ_CHECK_ROWS", "1")
+        assert gpu(anyseq, "local", q, s, sc) == want
+        monkeypatch.setenv("ANYSEQ_CHECK_ROWS", "2")
+        with pytest.raises(anyseq.AnySeqError, match=r"hand-off row invariant broken after a host-built fill: 1 "
+                                                     r"non-sentinel word\(s\)"):
+            gpu(anyseq, "local", q, s, sc)
+        monkeypatch.setenv("ANYSEQ_CHECK_ROWS", "1")
+        assert gpu(anyseq, "local", q, s, sc) == want
+        q2, s2 = rnd(rng, 6000), rnd(rng, 3000)
+        assert anyseq.construct_local_sharded("local", q2, s2, 2, *sc) == anyseq.construct("local", q2, s2, *sc)
+    finally:
+        anyseq.set_option("affine_grid", 0)
