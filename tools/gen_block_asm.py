@@ -388,9 +388,9 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
         e(f"global_load_dwordx4 v[{dst + 4}:{dst + 7}], v{B_VA}, %[sg] offset:16")
 
     # GS: VMEM operations a block issues after its code loads (the vmcnt a block waits
-    # with for its own codes): the glob publisher's two half stores; the diagnostic
-    # build's event stores are not counted (it waits for all)
-    code_wait = 0 if ts else (2 if pub == "glob" else 0)
+    # with for its own codes): the glob publisher's two half stores (the diagnostic
+    # build's event stores only add younger operations: the wait then covers a few more)
+    code_wait = 2 if pub == "glob" else 0
 
     def top_reads(half):
         """8 ds_read_b128 of top-row pairs [16*half, 16*half+16) (chunk address in VB)."""
