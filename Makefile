@@ -46,8 +46,14 @@ exp:
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(EXPDEF) -DANYSEQ_ASM_INC='"$(CURDIR)/build/exp_asm.inc"' -c $(SRC)/anyseq_kernels.hip -o build/anyseq_kernels_exp.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -Wl,-z,defs -o anyseq_amd/libanyseq_exp.so build/anyseq_kernels_exp.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
+# diagnostic build with only the steady-state stamps (band lags at a product-like step)
+stamps_light:
+	mkdir -p build && ANYSEQ_GEN_TSLIGHT=1 python3 tools/gen_block_asm.py build/light_asm.inc > /dev/null
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -DANYSEQ_ASM_INC='"$(CURDIR)/build/light_asm.inc"' -c $(SRC)/anyseq_kernels.hip -o build/anyseq_kernels_light.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o anyseq_amd/libanyseq_stamps_light.so build/anyseq_kernels_light.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
+
 clean:
 	rm -f $(SRC)/*.o $(LIB) anyseq_amd/libanyseq_*.so
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean stamps exp
+.PHONY: all oracle clean stamps exp stamps_light

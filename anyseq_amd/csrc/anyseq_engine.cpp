@@ -579,8 +579,9 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     unsigned long long* dbg = nullptr;
     static DevBuf stamp_buf;
     if (getenv("ANYSEQ_STAMPS")) {
-        dbg = (unsigned long long*)stamp_buf.get(8 * (16 + 20 * 4096));
-        HIPCHECK(hipMemsetAsync(dbg, 0, 8 * (16 + 20 * 4096), st));
+        // [header 16 | timeline 4/band | hand-off events 16/band | clock 4/band] x 4096 bands
+        dbg = (unsigned long long*)stamp_buf.get(8 * (16 + 24 * 4096));
+        HIPCHECK(hipMemsetAsync(dbg, 0, 8 * (16 + 24 * 4096), st));
         fpl.dbg = dbg;
     }
     C.stamps = dbg;
@@ -734,6 +735,16 @@ void fill_collect(FillCtx& C) {
                 fprintf(f, "# launch %.3f ms R=%d NW=%d\n", ms, R, NW);
                 unsigned long long t0 = ~0ull;
                 for (size_t i = 0; i < t.size(); i += 4) if (t[i] && t[i] < t0) t0 = t[i];
+                // clock per band (round 5): shader cycles / 100 MHz ticks over the band's loop
+                std::vector<unsigned long long> ck(4 * 4096);
+                HIPCHECK(hipMemcpy(ck.data(), dbg + 16 + 20 * 4096, ck.size() * 8, hipMemcpyDeviceToHost));
+                if (FILE* g = fopen((std::string(tl) + ".clk").c_str(), "a")) {
+                    fprintf(g, "# launch: band shader_cycles ticks_100MHz\n");
+                    for (size_t i = 0; i < ck.size(); i += 4)
+                        if (ck[i] && ck[i + 2] > ck[i] && ck[i + 3] > ck[i + 1])
+                            fprintf(g, "%zu %llu %llu\n", i / 4, ck[i + 2] - ck[i], ck[i + 3] - ck[i + 1]);
+                    fclose(g);
+                }
                 for (size_t i = 0; i < t.size(); i += 4)
                     if (t[i]) fprintf(f, "%zu %.2f %.2f %.2f %.2f\n", i / 4, (t[i] - t0) / 100.0,
                                       t[i + 1] ? (t[i + 1] - t0) / 100.0 : -1.0, (t[i + 2] - t0) / 100.0,

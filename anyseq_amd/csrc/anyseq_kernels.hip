@@ -1756,6 +1756,8 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
 #endif
 #ifdef ANYSEQ_STAMPS
     uint64_t t_b0 = 0;             // diagnostic build: C++ block 0 start
+    // diagnostic build: shader clock and 100 MHz time at the band's start and end (clock per band)
+    const uint64_t ck_mt0 = __builtin_amdgcn_s_memtime(), ck_rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     // clamp bound far below any cell when the problem does not clamp
     const int zoff = clamp ? 0 : 2 * kAffNeg;
@@ -2059,6 +2061,13 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         dbg[slot + 3] = t_b0 ? t_b0 : (uint64_t)nmiss;   // (asm path: prefetch misses)
     }
     ev_store(10, __builtin_amdgcn_s_memrealtime());   // band end
+    if (dbg && lane == 0 && band < 2048) {
+        unsigned long long* ck = dbg + 16 + 20 * 4096 + 4 * (band + (P.q_step < 0 ? 2048 : 0));
+        ck[0] = ck_mt0;
+        ck[1] = ck_rt0;
+        ck[2] = __builtin_amdgcn_s_memtime();
+        ck[3] = __builtin_amdgcn_s_memrealtime();
+    }
 #endif
     if (!dead) {
         if (P.out_col) gmem(P.out_col)[row] = aff_to_h(g, row, w - 1, nge);

@@ -338,6 +338,9 @@ LEAN = int(os.environ.get("ANYSEQ_GEN_LEAN", "2"))
 # problem's code rows in HBM (DPProblem::scode; kernel ANYSEQ_AFF_GS 1), issued one block
 # ahead; 0 = the I/O wave's pre-skewed LDS copy (ds_read2st64 at step 8, an s_filled wait)
 GS = int(os.environ.get("ANYSEQ_GEN_GS", "1"))
+# diagnostic build (ts variants): 1 = only the steady-state start / end stamps, no per-block
+# event checks (a step close to the product's: band lags in product steps)
+TSLIGHT = int(os.environ.get("ANYSEQ_GEN_TSLIGHT", "0"))
 AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
@@ -451,7 +454,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     def event(k, slot, bval):
         """Diagnostic build: at block `bval` (b + const), store s_memrealtime to
         dbp[slot] (vector store from v138:139; the record pointer is 0 when off)."""
-        if not ts:
+        if not ts or TSLIGHT:
             return
         e(f"s_cmp_eq_u32 %[b], {bval}")
         e(f"s_cbranch_scc0 L_ev{slot}{k}_%=")
@@ -469,7 +472,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
         """Diagnostic build, band-end variants: when 2b + add is the band's last half
         (nch), store s_memrealtime to dbp[slot] (consumer: the last half seen, add 2;
         producer: the last half published, add -2)."""
-        if not (ts and epi):
+        if not (ts and epi) or TSLIGHT:
             return
         e("s_lshl_b32 %[x2], %[b], 1")
         e(f"s_add_u32 %[x2], %[x2], {add & 0xffffffff}")
@@ -486,7 +489,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
         e(f"L_evl{slot}{k}_%=:")
 
     def count_miss(k, tag):
-        if ts:   # diagnostic: hand-off waits (block start or step 14)
+        if ts and not TSLIGHT:   # diagnostic: hand-off waits (block start or step 14)
             e("s_cmp_ge_u32 %[sp], %[x4]")
             e(f"s_cbranch_scc1 L_nm{tag}{k}_%=")
             e("s_add_u32 %[nmiss], %[nmiss], 1")

@@ -20,7 +20,7 @@ q = q[:rows]
 path = out + ".txt"
 os.environ["ANYSEQ_TIMELINE"] = ""
 A.score(kind, q, s, gap_open=-2, gap_extend=-1)
-for f_ in (path, path + ".ev"):
+for f_ in (path, path + ".ev", path + ".clk"):
     if os.path.exists(f_):
         os.remove(f_)
 os.environ["ANYSEQ_TIMELINE"] = path
@@ -63,6 +63,20 @@ for front, sel in (("fwd", a[:, 0] < 2048), ("rev", a[:, 0] >= 2048)):
               f"slot-{k} steady duration median {np.median(dur[mk]):.2f} us")
     q4 = len(d) // 4
     print("  start lag by chain quarter:", " ".join(f"{np.mean(d[i*q4:(i+1)*q4]):.3f}" for i in range(4)))
+
+# clock per band (shader cycles / 100 MHz ticks over the band, from its start to its end)
+if os.path.exists(path + ".clk"):
+    ck = [ln.split() for ln in open(path + ".clk") if not ln.startswith("#")]
+    if ck:
+        c = np.array([[float(x) for x in r] for r in ck])
+        for front, sel in (("fwd", c[:, 0] < 2048), ("rev", c[:, 0] >= 2048)):
+            b = c[sel]
+            b = b[np.argsort(b[:, 0])]
+            ghz = b[:, 1] / (b[:, 2] * 10.0)
+            q4 = max(1, len(ghz) // 4)
+            print(f"  {front} clock per band (GHz): band0 {ghz[0]:.3f}, by chain quarter "
+                  + " ".join(f"{np.median(ghz[i*q4:(i+1)*q4]):.3f}" for i in range(4))
+                  + f"; cycles per band: band0 {b[0, 1]:.0f}, median {np.median(b[:, 1]):.0f}")
 
 # hand-off events of block 1000 (producer: its block 1002) per band, 10 ns ticks
 if os.path.exists(path + ".ev"):
