@@ -1326,11 +1326,17 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         return mx;
     };
     bool planned = false, dev_final = false;
-    if (!sharded && g_tuning.devplan && plan_rowbuf_bytes() <= ((size_t)8 << 30) && n < 8192 * 4096 - 1) {
-        // Device-planned levels: every level is enqueued up front -- plan
-        // (aff_level_plan_kernel builds the level from the splits on the device), prep,
-        // fill, row-to-column, join -- and the splits come back in ONE download after the
-        // last level, instead of a download and a host rebuild per level.
+    const bool plan_ok = g_tuning.devplan && plan_rowbuf_bytes() <= ((size_t)8 << 30) && n < 8192 * 4096 - 1;
+    // Device-planned levels: every level from the one with P0 parts on is
+    // enqueued up front -- plan (aff_level_plan_kernel builds the level from the splits on
+    // the device), prep, fill, row-to-column, join -- and the splits come back in ONE
+    // download after the last level, instead of a download and a host rebuild per level.
+    // Sharded (round 5): the levels the host loop does not column-block (the halves dealt
+    // round-robin) go the same way, each rank's fill running only its own halves (emulated
+    // ranks: every half, into its owner's view), the level's columns, transposed bottom
+    // rows and best cells reduced over the ranks between the fill and the tail.
+    auto run_planned = [&](int P0) {
+        const int lev0 = [&] { int k = 0; while ((1 << k) < P0) ++k; return k; }();   // levels before P0
         struct Lev {
             int half, parts, bound, nh, slots, grid, want, nw;   // half: the level's widest half
             size_t rowbuf_bytes;
@@ -1339,7 +1345,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         size_t max_meta = 0, max_rowbuf = 0, max_rowpool = 0, max_joinbuf = 0;
         int max_parts = 1;
         const int nsl = std::max(1, (n + 1 + 4095) / 4096);   // join slices of the longest possible part
-        for (int P = 1; P < sp.nb; P *= 2) {
+        for (int P = P0; P < sp.nb; P *= 2) {
             Lev L;
             L.half = level_half(P);
             L.parts = P;
@@ -1388,7 +1394,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         uint8_t* scode_rows = (uint8_t*)E.pl_scode.get(scode_cap);
         PartInfo* d_parts = (PartInfo*)E.pl_parts.get((size_t)max_parts * sizeof(PartInfo));
         RowToCol* d_jobs = (RowToCol*)E.pl_jobs.get((size_t)2 * max_parts * sizeof(RowToCol));
-        int32_t* pbest = (int32_t*)E.bmax.get((size_t)2 * max_parts * 4);
+        // best cells: 2 per part and view (view v at + v * pstride)
+        const int64_t pstride = 2 * (int64_t)max_parts;
+        int32_t* pbest = (int32_t*)E.bmax.get((size_t)nviews * pstride * 4);
+        const int ninit_best = (int)(nviews * pstride);
         void* partial = E.joinbuf.get(std::max<size_t>(max_joinbuf, 16));
         // per level: header (8 words: sentinel uint4s, bound check, cells (u64), tail counter)
         // then one error word per level
@@ -1407,9 +1416,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         BlockInfo* d_fblocks = nullptr;
         int32_t* d_tall = nullptr;
         uint8_t* d_fpred = nullptr;
-        if (dev_final) {
-            d_fblocks = (BlockInfo*)E.blocks.get((size_t)sp.nb * sizeof(BlockInfo));
-            d_tall = (int32_t*)E.tall.get(((size_t)sp.nb + 1) * 4);
+        if (dev_final) {   // (a block table and tall list per view)
+            d_fblocks = (BlockInfo*)E.blocks.get((size_t)nviews * sp.nb * sizeof(BlockInfo));
+            d_tall = (int32_t*)E.tall.get((size_t)nviews * ((size_t)sp.nb + 1) * 4);
             d_fpred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(slab_bound, 16));
         }
         while ((int)E.pl_ev.size() < 2 * nlev) {
@@ -1465,7 +1474,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             A.flags = ctr + 32;
             A.spl = d_spl;
             A.typ = d_typ;
-            A.score = li == 0 ? nullptr : d_score;
+            A.score = li == 0 && P0 == 1 ? nullptr : d_score;   // (level 1's own value: its tail)
             A.parts_out = d_parts;
             A.probs = d_probs;
             A.groups = d_groups;
@@ -1475,6 +1484,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             A.xq = reinterpret_cast<uint32_t*>(d_groups + L.slots);
             A.scode = scode_rows;
             A.scode_cap = (int64_t)scode_cap;
+            A.world = sharded ? world : 1;
+            A.rank = emulate ? -1 : my_rank;
+            A.vstride = (int64_t)nn;
+            A.pstride = pstride;
         }
         // level 1: plan + prep; every level: fill, then one tail launch (join, next level's
         // sentinel rows, counters, best cells and plan)
@@ -1484,13 +1497,17 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             plans[0].nzero_init = 9 * nlev;
             plans[0].init_ends = 1;
             HIPCHECK(anyseq_launch_aff_level_plan(&plans[0], st));
-            HIPCHECK(anyseq_launch_fill_prep_planned(ctr, 32 + lv[0].slots, pbest, 2 * lv[0].parts, kAffNegH, rowbuf,
+            HIPCHECK(anyseq_launch_fill_prep_planned(ctr, 32 + lv[0].slots, pbest, ninit_best, kAffNegH, rowbuf,
                                                      0, 0x80808080u, d_hdr, st));
         }
         for (int li = 0; li < nlev; ++li) {
             const Lev& L = lv[li];
             const AffLevelPlan& A = plans[li];
-            g_stage_level = li + 1;
+            g_stage_level = lev0 + li + 1;
+            if (sharded) {   // rows and best cells a rank does not fill are zero / -inf in the reductions
+                for (int32_t* b : {LH0, LE0, RH0, RE0}) HIPCHECK(hipMemsetAsync(b, 0, nviews * nn * 4, st));
+                if (!emulate) HIPCHECK(hipMemsetAsync(rowpool, 0, max_rowpool, st));
+            }
             DPProblem* d_probs = A.probs;
             GroupRef* d_groups = A.groups;
             FillParams fpl = fp;
@@ -1515,6 +1532,18 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                 const int inject = check_rows == 2 && li == 0;
                 HIPCHECK(anyseq_launch_rows_check(rowbuf, max_rowbuf / 4, 0x80808080u, d_probs, L.nh, w, inject, st));
             }
+            if (sharded) {   // every rank gets every half's columns, bottom rows and best cells
+                if (emulate) {
+                    for (int32_t* b : {LH0, LE0, RH0, RE0})
+                        HIPCHECK(anyseq_launch_view_reduce_i32(b, nn, nviews, nn, 0, st));
+                    HIPCHECK(anyseq_launch_view_reduce_i32(pbest, (size_t)pstride, nviews, (size_t)2 * L.parts, 1, st));
+                } else {
+                    for (int32_t* b : {LH0, LE0, RH0, RE0}) shards->sum_i32(b, (size_t)n, st);
+                    shards->sum_i32(rowpool, max_rowpool / 4, st);
+                    shards->max_i32(pbest, (size_t)2 * L.parts, st);
+                }
+                stage_check(st, "sharded level reductions (device plan)");
+            }
             AffLevelTail T{};
             T.parts = d_parts;
             T.jobs = d_jobs;
@@ -1533,7 +1562,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             T.partial = partial;
             T.splits = d_spl;
             T.types = d_typ;
-            T.score = li == 0 ? d_score : nullptr;
+            T.score = li == 0 && P0 == 1 ? d_score : nullptr;
             T.done = d_hdr + 8 * li + 4;
             T.has_next = li + 1 < nlev;
             if (T.has_next) {
@@ -1543,7 +1572,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                 T.zero = ctr;
                 T.nzero = 32 + N.slots;
                 T.init = pbest;
-                T.ninit = 2 * N.parts;
+                T.ninit = ninit_best;
                 T.next = plans[li + 1];
             }
             HIPCHECK(anyseq_launch_aff_level_tail(&T, T.has_next && T.nsent16 ? 1024 : 1, st));
@@ -1551,23 +1580,40 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         }
         uint32_t* d_ferr = d_tail + tail_words - 1;
         if (dev_final) {
-            AffFinalPlan F{};
-            F.spl = d_spl;
-            F.typ = d_typ;
-            // (no level, m <= 128: nothing writes d_score; the caller checked score > 0)
-            F.score = nlev > 0 ? d_score : nullptr;
-            F.blocks = d_fblocks;
-            F.tall = d_tall;
-            F.err = d_ferr;
-            F.nb = sp.nb;
-            F.n = n;
-            F.m = m;
-            F.kind = kind;
-            F.small_rows = kPredSmallRows;
-            g_stage_level = nlev + 1;
-            HIPCHECK(anyseq_launch_aff_final(&F, dq, ds, d_fpred, sc.match, sc.mismatch, sc.gap_open, sc.gap_extend,
-                                             d_alq, d_als, st));
-            stage_check(st, "aff_final (device plan)");
+            // sharded: each view walks its blocks (b % world == rank) into its own strings,
+            // which merge by the byte-wise MAX of the host-built final level
+            for (int v = 0; v < nviews; ++v) {
+                AffFinalPlan F{};
+                F.spl = d_spl;
+                F.typ = d_typ;
+                // (no level, m <= 128: nothing writes d_score; the caller checked score > 0)
+                F.score = lev0 + nlev > 0 ? d_score : nullptr;
+                F.blocks = d_fblocks + (size_t)v * sp.nb;
+                F.tall = d_tall + (size_t)v * (sp.nb + 1);
+                F.err = d_ferr;
+                F.nb = sp.nb;
+                F.n = n;
+                F.m = m;
+                F.kind = kind;
+                F.small_rows = kPredSmallRows;
+                F.world = sharded ? world : 1;
+                F.rank = view_rank(v);
+                g_stage_level = lev0 + nlev + 1;
+                uint8_t *aq, *as;
+                view_str(v, aq, as);
+                HIPCHECK(anyseq_launch_aff_final(&F, dq, ds, d_fpred, sc.match, sc.mismatch, sc.gap_open,
+                                                 sc.gap_extend, aq, as, st));
+                stage_check(st, "aff_final (device plan)");
+            }
+            if (sharded) {
+                if (emulate) {
+                    HIPCHECK(anyseq_launch_view_max_u8(d_alq, vstr, 2 * L, nviews - 1, L, st));
+                    HIPCHECK(anyseq_launch_view_max_u8(d_als, vstr + L, 2 * L, nviews - 1, L, st));
+                } else {
+                    shards->max_u8(d_alq, L, st);
+                    shards->max_u8(d_als, L, st);
+                }
+            }
         }
         HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + 1) * 4, hipMemcpyDeviceToHost, st));
         HIPCHECK(hipMemcpyAsync(h_tail, d_tail, tail_words * 4, hipMemcpyDeviceToHost, st));
@@ -1588,7 +1634,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         }
         for (int li = 0; li < nlev; ++li) {
             const uint32_t err = h_tail[8 * nlev + li];
-            g_stage_level = li + 1;
+            g_stage_level = lev0 + li + 1;
             if (err & ERR_BAD_DESC) fail("fill kernel read a corrupt problem descriptor (error %u; planned level %d)", err, li + 1);
             if (err) fail("fill kernel reported error %u (spin timeout; planned level %d)", err, li + 1);
             if (h_tail[8 * li + 1]) fail("internal: planned level %d: a half exceeds its group slots", li + 1);
@@ -1608,17 +1654,19 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                 fail("internal: planned levels left split %zu = %d (type %d)", i - 1, sp.v[i], typ[i]);
         if (dev_final && h_tail[tail_words - 1])
             fail("internal: the device final level found a bad split table (the host check passed)");
-        if (nlev > 0) {
+        if (nlev > 0 && P0 == 1) {   // (P0 > 1: the host's level 1 set it)
             const int32_t s32 = h_status[2 * nsv];
             score = kind == KIND_SEMIGLOBAL ? std::max(s32, 0) : s32;
-            if (kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
         }
-        planned = true;   // (the host loop below has nothing left)
-    }
+        planned = true;   // (the host loop has nothing left)
+    };
+    if (!sharded && plan_ok) run_planned(1);
+    if (planned && kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
     if (!planned) {
         upload_status();
         HIPCHECK(hipStreamSynchronize(st));   // h_status: its upload before the first download
     }
+    int handover = 0;
     for (int parts = 1; !planned && parts < sp.nb; parts *= 2) {
         ++g_stage_level;
         // free-end best cells, 2 per part, per view
@@ -1673,6 +1721,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                 const int r0 = (int)((int64_t)p * world / parts), G = (int)((int64_t)(p + 1) * world / parts) - r0;
                 if ((pi.flags & 12) == 0 && pi.len > 0 && pi.len < G) blocked = false;
             }
+        }
+        if (sharded && plan_ok && !blocked && env_int("ANYSEQ_SHARD_DEVPLAN", 1) != 0) {
+            handover = parts;   // this level and the rest: device-planned
+            break;
         }
         if (blocked) {
             auto tam = [](int am) {
@@ -1834,6 +1886,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             level1 = false;
             if (kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
         }
+    }
+    if (handover > 0) {
+        run_planned(handover);
+        if (kind != KIND_GLOBAL && score <= 0) return score;   // (checked by the host's level 1 already)
     }
     if (dev_final) return score;   // (the final level is done: enqueued behind the levels)
     // final 128-column blocks: each view walks its own into its strings

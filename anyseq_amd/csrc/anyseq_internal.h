@@ -268,6 +268,13 @@ struct AffLevelPlan {
     uint32_t* xq;
     uint8_t* scode;   // the level's subject-code rows (DPProblem::scode), packed by the plan
     int64_t scode_cap;   // their bytes (a plan that needs more fails the level's bound check)
+    // sharded construct: world > 1 deals the level's halves
+    // round-robin in part order (the host's half_owner: ordinal % world, counting only
+    // parts with halves).  rank >= 0 (one rank per GPU): the other ranks' halves get no
+    // groups; rank < 0 (emulated ranks): every half runs and writes the columns / best
+    // cells of its owner's view (+ owner * vstride / + owner * pstride)
+    int32_t world, rank;
+    int64_t vstride, pstride;
 };
 
 // The tail of a device-planned level, one launch: the join of level L
@@ -317,6 +324,7 @@ struct AffFinalPlan {
     int32_t* tall;         // 1 + nb: count, then the blocks taller than small_rows
     uint32_t* err;         // set to 1 on a bad split table
     int nb, n, m, kind, small_rows;
+    int world, rank;       // sharded: only the blocks b with b % world == rank (world <= 1: all)
 };
 inline int pred_lds_bytes(int rows) { return (rows + 128) * 128 + ((rows + 15) & ~15) + 1024; }
 

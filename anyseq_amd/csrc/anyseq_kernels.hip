@@ -2922,7 +2922,7 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
     // kind != global with a level-1 value <= 0: the empty alignment, no halves
     const bool stop = a.score && a.kind != KIND_GLOBAL && *a.score <= 0;
     RowToCol* jobs = a.jobs;
-    int64_t rb_base = 0, rp_base = 0, sc_base = 0;
+    int64_t rb_base = 0, rp_base = 0, sc_base = 0, hb_base = 0;
     for (int t0 = 0; t0 < a.parts; t0 += blockDim.x) {
         const int p = t0 + (int)threadIdx.x;
         PartInfo pi{};
@@ -2961,17 +2961,24 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
             a.parts_out[p] = pi;
             if (gl.ngroups > a.bound || gr.ngroups > a.bound) atomicOr(&bad, 1);
         }
-        int64_t tot_rb, tot_rp, tot_sc;
+        int64_t tot_rb, tot_rp, tot_sc, tot_hb;
         const int64_t rb = rb_base + block_scan_excl(gl.rowbuf + gr.rowbuf, sh, &tot_rb);
         const int64_t rp = rp_base + block_scan_excl(gl.rowpool + gr.rowpool, sh, &tot_rp);
         const int64_t sco = sc_base + block_scan_excl(gl.scode + gr.scode, sh, &tot_sc);
+        // sharded: the part's ordinal among the parts with halves (the host's half_index / 2)
+        const int64_t hord = hb_base + block_scan_excl(p < a.parts && len > 0 ? 1 : 0, sh, &tot_hb);
         rb_base += tot_rb;
         rp_base += tot_rp;
         sc_base += tot_sc;
+        hb_base += tot_hb;
         if (p < a.parts) {
             for (int side = 0; side < 2; ++side) {
                 const AffHalfGeo& g = side ? gr : gl;
                 const int idx = 2 * p + side;
+                // sharded: the half's owner; view: where its columns / best cell go
+                const int own = a.world > 1 ? (int)((2 * hord + side) % a.world) : 0;
+                const bool mine = a.world <= 1 || a.rank < 0 || own == a.rank;
+                const int64_t view = a.world > 1 && a.rank < 0 ? own : 0;
                 DPProblem P{};
                 RowToCol J{};
                 if (g.h > 0) {
@@ -2981,9 +2988,9 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
                     const int bm = side ? pi.emode : pi.smode;
                     const bool fr = side ? sfree : efree;
                     const int amode = (bm == BM_FREE_LOCAL ? AM_CLAMP : 0) | (fr ? a.best_bits : 0);
-                    int32_t* H = (side ? a.RH : a.LH) + off;
-                    int32_t* E = (side ? a.RE : a.LE) + off;
-                    P.best = fr ? a.pbest + 2 * p + side : nullptr;
+                    int32_t* H = (side ? a.RH : a.LH) + view * a.vstride + off;
+                    int32_t* E = (side ? a.RE : a.LE) + view * a.vstride + off;
+                    P.best = fr ? a.pbest + view * a.pstride + 2 * p + side : nullptr;
                     if (g.tr) {
                         P.q = a.s;
                         P.q_off = soff;
@@ -3017,13 +3024,13 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
                     P.h = g.h;
                     P.w = g.w;
                     P.nbands = (g.h + 63) / 64;
-                    P.ngroups = g.ngroups;
+                    P.ngroups = mine ? g.ngroups : 0;   // (another rank's half: every group slot skipped)
                     P.wpad = g.wpad;
                     P.nslots = g.nslots;
                     P.rowbuf = a.rowbuf + rb + (side ? gl.rowbuf : 0);
                     const int64_t so = sco + (side ? gl.scode : 0);
                     P.scode = a.scode && so + g.scode <= a.scode_cap ? a.scode + so : nullptr;
-                    atomicAdd(&cells, (unsigned long long)((int64_t)g.h * g.w));
+                    if (mine) atomicAdd(&cells, (unsigned long long)((int64_t)g.h * g.w));
                 } else {
                     P.nslots = 1;
                 }
@@ -3823,6 +3830,7 @@ __global__ __launch_bounds__(1024) void aff_final_blocks_kernel(const AffFinalPl
         bi.e_end = te == T_H ? 0 : te == T_E ? 1 : 2;
         bi.flags = (a.kind == KIND_LOCAL ? 1 : 0) | (bi.oj + bi.w == a.m ? 2 : 0);
         if (stop || ts == T_BEFORE || te == T_AFTER) bi.flags |= 4;
+        if (a.world > 1 && b % a.world != a.rank) bi.flags |= 4;   // sharded: another rank walks it
         a.blocks[b] = bi;
         if (!(bi.flags & 4) && bi.h > a.small_rows) a.tall[1 + atomicAdd(&ntall, 1)] = b;
     }
