@@ -2165,13 +2165,16 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
             g_out = rows + (size_t)(gr.group % P.nslots) * P.wpad;
         else if (P.out_row)
             g_out = reinterpret_cast<int2*>(P.out_row);
-        if (wave == NW && kAffGS && fp.io_fwd) {
+        // (GS: always the forwarder -- the I/O wave has no subject work; io_wave, a called
+        // function, would give the kernel a stack and every launch a scratch setup)
+        if (wave == NW && (kAffGS || fp.io_fwd)) {
             const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
             io_forward<int2>(lane, P.w, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
                              P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc, 2, 2, fp.prio == 3,
                              fp.dbg && first < 2048 ? fp.dbg + 16 + 4 * 4096 + 16 * (first + (P.q_step < 0 ? 2048 : 0))
                                                     : nullptr);
         } else if (wave == NW) {
+          if constexpr (!kAffGS) {
             const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
             io_wave<32, true, int2>(lane, P.w, P.s, P.s_off, P.s_step, sh.s_ring, &sh.skew[0][0][0], &sh.s_filled,
                                     &sh.tail, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
@@ -2180,6 +2183,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                                                            : nullptr,
                                     fp.io_stage, fp.io_skew != 0 ? fp.io_skew : kIoSkewPolling, fp.io_poll2 != 0,
                                     kAffGS);
+          }
         } else {
             const int band = first + wave;
             if (band <= last) {

@@ -110,9 +110,10 @@ def test_affine_waves_per_group(anyseq, oracle, nw):
 
 
 @pytest.mark.parametrize("option,value,default", [
+    # (the round-4 I/O wave's options: the default build, with code rows in HBM, always runs
+    # the forwarder and ignores them -- kept so that a non-GS build still runs them)
     ("io_stage", 0, 3), ("io_stage", 1, 3), ("io_stage", 2, 3),   # the I/O wave's subject staging
     ("io_poll2", 1, 0),                                           # two hand-off polls in flight
-    ("io_forward", 0, 1),                                         # code rows: the full I/O wave, not the forwarder
     ("io_skew", 2, 0),                                            # skewed blocks per polling pass
     ("priority", 0, -1), ("priority", 3, -1),                     # issue priority
     ("affine_asm", 97, 1), ("affine_asm", 33, 1), ("affine_asm", 65, 1),   # round-3 ends / the start only / the end only
