@@ -1435,6 +1435,16 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         // final level's check word is written by aff_final_blocks_kernel)
         uint32_t* d_rchk = d_tail + 9 * (size_t)nlev;   // check words of level li at + 8 * li
         if (check_rows) HIPCHECK(hipMemsetD32Async(d_rchk, 0xffffffffu, 8 * (size_t)nlev, st));
+        // diagnostics: the tail launches' phases (aff_level_tail_kernel stamps, 8 words a level)
+        static const int tail_stamps = env_int("ANYSEQ_TAIL_STAMPS", 0);
+        unsigned long long* d_tst = nullptr;
+        if (tail_stamps) {
+            d_tst = (unsigned long long*)E.tst.get((size_t)16 * std::max(nlev, 1) * 8);
+            std::vector<unsigned long long> init((size_t)16 * std::max(nlev, 1), 0ull);
+            for (size_t i = 0; i < init.size(); i += 16) init[i] = ~0ull;
+            HIPCHECK(hipMemcpyAsync(d_tst, init.data(), init.size() * 8, hipMemcpyHostToDevice, st));
+            HIPCHECK(hipStreamSynchronize(st));
+        }
         static std::atomic<int32_t> g_plan_epoch{0x40000};
         uint32_t* ctr = (uint32_t*)meta;
         std::vector<AffLevelPlan> plans((size_t)nlev);
@@ -1564,6 +1574,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             T.types = d_typ;
             T.score = li == 0 && P0 == 1 ? d_score : nullptr;
             T.done = d_hdr + 8 * li + 4;
+            T.stamps = d_tst ? d_tst + 16 * li : nullptr;
             T.has_next = li + 1 < nlev;
             if (T.has_next) {
                 const Lev& N = lv[li + 1];
@@ -1620,6 +1631,18 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         {
             const hipError_t e = stream_wait_spin(st);
             if (e != hipSuccess) fail("affine construct levels failed: %s", hipGetErrorString(e));
+        }
+        if (d_tst) {
+            std::vector<unsigned long long> h((size_t)16 * nlev);
+            HIPCHECK(hipMemcpy(h.data(), d_tst, h.size() * 8, hipMemcpyDeviceToHost));
+            for (int li = 0; li < nlev; ++li) {
+                const unsigned long long* q = h.data() + 16 * li;
+                auto d = [&](int a, int b) { return q[a] && q[b] ? ((double)q[b] - (double)q[a]) / 100.0 : 0.0; };
+                fprintf(stderr, "tail %d: join %.2f us, final pass %.2f, counters %.2f, plan %.2f | plan: enter %.2f, "
+                        "parts %.2f, scans %.2f, halves %.2f, groups %.2f, end %.2f\n",
+                        lev0 + li + 1, d(0, 1), d(1, 2), d(2, 3), d(3, 4), d(3, 8), d(8, 9), d(9, 10), d(10, 11),
+                        d(11, 12), d(12, 4));
+            }
         }
         bool any_err = false;
         for (int li = 0; li < nlev; ++li) any_err |= h_tail[8 * nlev + li] != 0;

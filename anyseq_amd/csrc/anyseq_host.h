@@ -166,6 +166,7 @@ struct Engine {
     // row-to-column jobs, per-level header and error words (+ their pinned download)
     DevBuf pl_meta, pl_rowbuf, pl_parts, pl_jobs, pl_hdr;
     DevBuf pl_scode;           // the planned levels' subject-code rows (DPProblem::scode)
+    DevBuf tst;                // diagnostics: tail-launch stamps (ANYSEQ_TAIL_STAMPS)
     PinBuf pl_pin;
     std::vector<hipEvent_t> pl_ev;
     bool pl_dirty = true;      // pl_rowbuf may hold non-sentinel words (fresh, or a failed call)

@@ -79,10 +79,15 @@ __host__ __device__ inline int64_t scode_len(int w) { return 32 * (int64_t)((w +
 // kProbMagic ^ index ^ (epoch << 12) ^ digest: a fill group recomputes it from the
 // descriptor it read, so a descriptor that is stale or torn in ANY word (not only in
 // its magic) raises ERR_BAD_DESC instead of running on its pointers.
+// (round 5: four interleaved FNV-1a streams over words i = k mod 4, folded at the end --
+// a quarter of the dependent multiply chain, which every group start and every planned
+// half's descriptor pays)
 __host__ __device__ inline uint32_t desc_digest(const uint32_t* w, int nwords) {
-    uint32_t h = 0x811c9dc5u;
-    for (int i = 0; i < nwords; ++i) h = (h ^ w[i]) * 16777619u;
-    return h;
+    uint32_t h[4] = {0x811c9dc5u, 0x811c9dc5u ^ 1u, 0x811c9dc5u ^ 2u, 0x811c9dc5u ^ 3u};
+    for (int i = 0; i < nwords; ++i) h[i & 3] = (h[i & 3] ^ w[i]) * 16777619u;
+    uint32_t r = 0x811c9dc5u;
+    for (int k = 0; k < 4; ++k) r = (r ^ h[k]) * 16777619u;
+    return r;
 }
 constexpr int kDescWords = (int)(offsetof(DPProblem, magic) / 4);
 __host__ __device__ inline int32_t prob_magic(const DPProblem* P, int index, int epoch) {
@@ -275,6 +280,7 @@ struct AffLevelPlan {
     // cells of its owner's view (+ owner * vstride / + owner * pstride)
     int32_t world, rank;
     int64_t vstride, pstride;
+    unsigned long long* stamps;   // diagnostics (ANYSEQ_TAIL_STAMPS): the plan's phases, or null
 };
 
 // The tail of a device-planned level, one launch: the join of level L
@@ -299,6 +305,7 @@ struct AffLevelTail {
     void* sent;            // next level's hand-off rows (uint4 units)
     size_t nsent16;
     int32_t has_next;
+    unsigned long long* stamps;   // diagnostics (ANYSEQ_TAIL_STAMPS): 16 s_memrealtime words, or null
     uint32_t* zero;        // next level's counters + group flags
     int32_t nzero;
     int32_t* init;         // next level's best cells

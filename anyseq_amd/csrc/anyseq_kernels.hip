@@ -2914,10 +2914,80 @@ __device__ int64_t block_scan_excl(int64_t v, int64_t* sh, int64_t* total) {
     return r;
 }
 
+// Four block-wide exclusive scans at once (the plan's ring, bottom-row, code-row and
+// half-ordinal packing): one pass of shuffles, the wave totals scanned by wave 0's lanes
+// (no serial loop), three barriers for all four (round 5: four separate scans were
+// 3.5 us of every level's tail).
+struct Scan4 {
+    int64_t v[4];
+};
+__device__ Scan4 block_scan_excl4(const Scan4& in, int64_t (*sh)[4], Scan4* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = (int)(blockDim.x >> 6);
+    Scan4 x = in;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t y = __shfl_up(x.v[k], o);
+            if (lane >= o) x.v[k] += y;
+        }
+    }
+    if (lane == 63)
+        for (int k = 0; k < 4; ++k) sh[wv][k] = x.v[k];
+    __syncthreads();
+    if (wv == 0) {   // exclusive scan of the (at most 16) wave totals
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t t = lane < nw ? sh[lane][k] : 0;
+            int64_t c = t;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const int64_t y = __shfl_up(c, o);
+                if (lane >= o) c += y;
+            }
+            if (lane < nw) sh[lane][k] = c - t;
+            if (lane == nw - 1) sh[16][k] = c;
+        }
+    }
+    __syncthreads();
+    Scan4 r;
+    for (int k = 0; k < 4; ++k) {
+        r.v[k] = sh[wv][k] + x.v[k] - in.v[k];
+        total->v[k] = sh[16][k];
+    }
+    __syncthreads();
+    return r;
+}
+
+// The same within each wave alone (no LDS, no barrier): a level of at most 64 parts has
+// all of them in wave 0 (the other waves scan zeros).
+__device__ Scan4 wave_scan_excl4(const Scan4& in, Scan4* total) {
+    const int lane = threadIdx.x & 63;
+    Scan4 x = in, r;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t y = __shfl_up(x.v[k], o);
+            if (lane >= o) x.v[k] += y;
+        }
+    }
+    for (int k = 0; k < 4; ++k) {
+        total->v[k] = __shfl(x.v[k], 63);
+        r.v[k] = x.v[k] - in.v[k];
+    }
+    return r;
+}
+
 __device__ void aff_level_plan_body(const AffLevelPlan& a) {
     __shared__ int64_t sh[17];
+    __shared__ int64_t sh4[17][4];
     __shared__ unsigned long long cells;
     __shared__ int32_t bad;
+    auto stamp = [&](int k) {   // diagnostics: the plan's phases (a.stamps[k], ANYSEQ_TAIL_STAMPS)
+        if (a.stamps && threadIdx.x == 0) a.stamps[k] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
     if (threadIdx.x == 0) {
         cells = 0;
         bad = 0;
@@ -2927,6 +2997,7 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
     const bool stop = a.score && a.kind != KIND_GLOBAL && *a.score <= 0;
     RowToCol* jobs = a.jobs;
     int64_t rb_base = 0, rp_base = 0, sc_base = 0, hb_base = 0;
+    unsigned long long my_cells = 0;   // this thread's halves' cells (summed per wave below)
     for (int t0 = 0; t0 < a.parts; t0 += blockDim.x) {
         const int p = t0 + (int)threadIdx.x;
         PartInfo pi{};
@@ -2965,16 +3036,22 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
             a.parts_out[p] = pi;
             if (gl.ngroups > a.bound || gr.ngroups > a.bound) atomicOr(&bad, 1);
         }
-        int64_t tot_rb, tot_rp, tot_sc, tot_hb;
-        const int64_t rb = rb_base + block_scan_excl(gl.rowbuf + gr.rowbuf, sh, &tot_rb);
-        const int64_t rp = rp_base + block_scan_excl(gl.rowpool + gr.rowpool, sh, &tot_rp);
-        const int64_t sco = sc_base + block_scan_excl(gl.scode + gr.scode, sh, &tot_sc);
-        // sharded: the part's ordinal among the parts with halves (the host's half_index / 2)
-        const int64_t hord = hb_base + block_scan_excl(p < a.parts && len > 0 ? 1 : 0, sh, &tot_hb);
-        rb_base += tot_rb;
-        rp_base += tot_rp;
-        sc_base += tot_sc;
-        hb_base += tot_hb;
+        stamp(1);
+        // ring, bottom-row and code-row offsets; sharded: the part's ordinal among the parts
+        // with halves (the host's half_index / 2)
+        Scan4 in4, tot4;
+        in4.v[0] = gl.rowbuf + gr.rowbuf;
+        in4.v[1] = gl.rowpool + gr.rowpool;
+        in4.v[2] = gl.scode + gr.scode;
+        in4.v[3] = p < a.parts && len > 0 ? 1 : 0;
+        const Scan4 ex4 = a.parts <= 64 ? wave_scan_excl4(in4, &tot4) : block_scan_excl4(in4, sh4, &tot4);
+        const int64_t rb = rb_base + ex4.v[0], rp = rp_base + ex4.v[1], sco = sc_base + ex4.v[2];
+        const int64_t hord = hb_base + ex4.v[3];
+        rb_base += tot4.v[0];
+        rp_base += tot4.v[1];
+        sc_base += tot4.v[2];
+        hb_base += tot4.v[3];
+        stamp(2);
         if (p < a.parts) {
             for (int side = 0; side < 2; ++side) {
                 const AffHalfGeo& g = side ? gr : gl;
@@ -3034,7 +3111,7 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
                     P.rowbuf = a.rowbuf + rb + (side ? gl.rowbuf : 0);
                     const int64_t so = sco + (side ? gl.scode : 0);
                     P.scode = a.scode && so + g.scode <= a.scode_cap ? a.scode + so : nullptr;
-                    if (mine) atomicAdd(&cells, (unsigned long long)((int64_t)g.h * g.w));
+                    if (mine) my_cells += (unsigned long long)((int64_t)g.h * g.w);
                 } else {
                     P.nslots = 1;
                 }
@@ -3046,6 +3123,12 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
             }
         }
     }
+    {   // the level's cells: a wave sum, one LDS add per wave (not one per half)
+        unsigned long long c = my_cells;
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd(&cells, c);
+    }
+    stamp(3);
     // the group table, k-major over the half slots (a half's groups in increasing k);
     // XCD-local groups (a.xrun > 0, FillParams::xq): stably partitioned by XCD
     const int nh = 2 * a.parts;
@@ -3087,6 +3170,7 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
         }
     }
     __syncthreads();
+    stamp(4);
     if (threadIdx.x == 0) {
         a.hdr[0] = (uint32_t)(rb_base / 4);   // sentinel uint4s (every ring is a multiple of 128 ints)
         a.hdr[1] = (uint32_t)(bad || sc_base > a.scode_cap);
@@ -3119,6 +3203,16 @@ __global__ __launch_bounds__(kTailThreads) void aff_level_tail_kernel(const AffL
     __shared__ int last;
     const int nj = t.nslices * t.nparts;
     const int b = blockIdx.x;
+    // diagnostics: [0] first workgroup start, [1] last join done, [2] the last workgroup's
+    // final pass done, [3] its counters / best cells, [4] the plan done (s_memrealtime)
+    auto stamp = [&](int k, bool first) {
+        if (t.stamps && threadIdx.x == 0) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            if (first) atomicMin(t.stamps + k, now);
+            else atomicMax(t.stamps + k, now);
+        }
+    };
+    stamp(0, true);
     if (t.has_next) {
         const uint4 v = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
         for (size_t i = (size_t)b * blockDim.x + threadIdx.x; i < t.nsent16; i += (size_t)gridDim.x * blockDim.x)
@@ -3218,6 +3312,7 @@ __global__ __launch_bounds__(kTailThreads) void aff_level_tail_kernel(const AffL
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         last = atomicAdd(t.done, 1u) == gridDim.x - 1;
     }
+    stamp(1, false);
     __syncthreads();
     if (!last) return;
     // the final pass over chunks of parts: every partial of the chunk is loaded at once
@@ -3262,13 +3357,23 @@ __global__ __launch_bounds__(kTailThreads) void aff_level_tail_kernel(const AffL
         t.types[pi.split_index + 1] = type;
         if (t.score && part == 0) *t.score = best;
     }
-    if (!t.has_next) return;
     __syncthreads();
+    stamp(2, false);
+    if (!t.has_next) return;
     __threadfence_block();
     for (int i = threadIdx.x; i < t.nzero; i += blockDim.x) t.zero[i] = 0u;
     for (int i = threadIdx.x; i < t.ninit; i += blockDim.x) t.init[i] = kAffNeg;
     __syncthreads();
-    aff_level_plan_body(t.next);
+    stamp(3, false);
+    if (t.stamps) {
+        AffLevelPlan nx = t.next;
+        nx.stamps = t.stamps + 8;
+        aff_level_plan_body(nx);
+    } else {
+        aff_level_plan_body(t.next);
+    }
+    __syncthreads();
+    stamp(4, false);
 }
 
 // Final level: Gotoh with predecessor bytes for one 128-column block per wave,
