@@ -1372,7 +1372,8 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             max_meta = std::max(max_meta, meta);
             max_rowbuf = std::max(max_rowbuf, L.rowbuf_bytes);
             max_rowpool = std::max(max_rowpool, (size_t)2 * ((size_t)n + 64 * (size_t)L.parts) * 2 * 4);
-            max_joinbuf = std::max(max_joinbuf, (size_t)L.parts * nsl * 8);
+            // (the tail's join: at most ~256 workgroups, nslices = min(nsl, 256 / parts) per part)
+            max_joinbuf = std::max(max_joinbuf, (size_t)L.parts * std::max(1, std::min(nsl, (256 + L.parts - 1) / L.parts)) * 8);
             max_parts = std::max(max_parts, L.parts);
             lv.push_back(L);
         }
