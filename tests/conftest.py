@@ -34,3 +34,34 @@ def oracle():
 def anyseq():
     import anyseq_amd
     return anyseq_amd
+
+
+def loaded_libraries():
+    """The in-tree shared objects this process has mapped (/proc/self/maps), each with the
+    first 16 hex digits of its sha256 -- the evidence of which native code a GPU run used."""
+    import hashlib
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if len(line.split()) >= 6 else ""
+                if p.endswith(".so") or ".so." in p:
+                    paths.add(p)
+    except OSError:
+        return []
+    out = []
+    for p in sorted(paths):
+        if not os.path.realpath(p).startswith(os.path.realpath(ROOT)):
+            continue
+        with open(p, "rb") as f:
+            out.append((os.path.relpath(p, ROOT), hashlib.sha256(f.read()).hexdigest()[:16]))
+    return out
+
+
+def pytest_sessionfinish(session, exitstatus):
+    # ANYSEQ_MAPS_OUT=<file>: record the in-tree libraries the test process loaded
+    path = os.environ.get("ANYSEQ_MAPS_OUT")
+    if path:
+        with open(path, "w") as f:
+            for rel, digest in loaded_libraries():
+                f.write(f"{rel} sha256[:16]={digest}\n")
