@@ -243,9 +243,12 @@ def shard_score_local(kind, query, subject, nshards: int, match=2, mismatch=-1, 
 
 def construct_local_sharded(kind, query, subject, nshards: int, match=2, mismatch=-1, gap_open=-2, gap_extend=-1):
     """Sharded affine construct with `nshards` virtual ranks in this process on one GPU:
-    the plan of the RCCL path: level 1 column-blocked over the ranks
-    when its halves run transposed, later levels' halves dealt round-robin, one fill
-    launch per rank per level.  Returns (optimal_score, alQuery, alSubject)."""
+    the plan of the RCCL path: the leading levels column-blocked over
+    rank subgroups (world >= 2 x parts, each part's query rows split over its subgroup;
+    one fill per rank), the rest dealt round-robin by half and device-planned (one fill
+    launch per level, every view's columns reduced between the fill and the join;
+    ANYSEQ_SHARD_DEVPLAN=0: host-built, one launch per rank).  Returns (optimal_score,
+    alQuery, alSubject)."""
     q, s = _b(query), _b(subject)
     L = len(q) + len(s)
     aq = ctypes.create_string_buffer(max(L, 1))
