@@ -307,6 +307,7 @@ void init_tuning_locked() {
     g_tuning.io_skew = env_int("ANYSEQ_IO_SKEW", g_tuning.io_skew);
     g_tuning.io_poll2 = env_int("ANYSEQ_IO_POLL2", g_tuning.io_poll2);
     g_tuning.io_fwd = env_int("ANYSEQ_IO_FWD", g_tuning.io_fwd);
+    g_tuning.fill_events = env_int("ANYSEQ_FILL_EVENTS", g_tuning.fill_events);
     g_tuning.virtbest = env_int("ANYSEQ_VIRT_BEST", g_tuning.virtbest);
     g_tuning.devplan = env_int("ANYSEQ_AFF_DEVPLAN", g_tuning.devplan);
     g_tuning.devfinal = env_int("ANYSEQ_AFF_DEVFINAL", g_tuning.devfinal);
@@ -558,6 +559,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
         if (ub) HIPCHECK(hipMemcpyAsync(meta + zb, pin + 64, ub, hipMemcpyHostToDevice, st));
         if (init_words) HIPCHECK(hipMemsetD32Async(init, init_value, (size_t)init_words, st));
         if (C.err_host) *C.err_host = 0u;   // (no copy targets it: the previous launch has completed)
+        C.timed = true;
         HIPCHECK(hipEventRecord(C.ev0, st));
         HIPCHECK(hipEventRecord(C.ev1, st));
         HIPCHECK(hipEventRecord(C.ev2, st));
@@ -599,13 +601,14 @@ void fill_launch(FillCtx& C) {
     if (!C.pending) return;   // nothing to compute (events already recorded)
     C.pending = false;
     uint32_t* ctr = (uint32_t*)C.probs.p;   // the launch block's counters (fill_prepare)
-    HIPCHECK(hipEventRecord(C.ev0, C.st));
+    C.timed = g_tuning.fill_events != 0;
+    if (C.timed) HIPCHECK(hipEventRecord(C.ev0, C.st));
     if (C.aff)
         HIPCHECK(anyseq_launch_fill_affine(C.NW, C.d_probs, C.d_groups, C.ngroups, ctr, ctr + 1, &C.fp, C.grid, C.st));
     else
         HIPCHECK(anyseq_launch_fill(C.R, g_tuning.CH, C.NW, C.d_probs, C.d_groups, C.ngroups, ctr, ctr + 1, &C.fp,
                                     C.grid, C.st));
-    HIPCHECK(hipEventRecord(C.ev1, C.st));
+    if (C.timed) HIPCHECK(hipEventRecord(C.ev1, C.st));
     // ANYSEQ_CHECK_ROWS (host-built affine launches, round 5): every ring that is reused
     // within the launch (nslots < ngroups - 1: each reader puts the sentinel back) must
     // be all sentinel again afterwards, as the device-planned levels' rows;
@@ -677,7 +680,7 @@ void stage_check(hipStream_t st, const char* what) {
 
 void fill_finish(FillCtx& C) {
     {
-        const hipError_t e = hipEventSynchronize(C.ev1);
+        const hipError_t e = hipEventSynchronize(C.timed ? C.ev1 : C.ev2);
         if (e != hipSuccess) fail("fill failed: %s (%s)", hipGetErrorString(e), fill_summary(C).c_str());
     }
     fill_collect(C);
@@ -705,7 +708,7 @@ void fill_collect(FillCtx& C) {
         }
     }
     float ms = 0.f;
-    HIPCHECK(hipEventElapsedTime(&ms, C.ev0, C.ev1));
+    if (C.timed) HIPCHECK(hipEventElapsedTime(&ms, C.ev0, C.ev1));
     g_fill_ms += ms;
     g_fill_launches += 1;
     g_fill_cells += C.cells;
@@ -1422,6 +1425,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             d_tall = (int32_t*)E.tall.get((size_t)nviews * ((size_t)sp.nb + 1) * 4);
             d_fpred = (uint8_t*)E.pred.get((size_t)std::max<int64_t>(slab_bound, 16));
         }
+        const bool timed = g_tuning.fill_events != 0;   // (events around each planned fill: last_fill_stats)
         while ((int)E.pl_ev.size() < 2 * nlev) {
             hipEvent_t ev;
             HIPCHECK(hipEventCreate(&ev));
@@ -1530,9 +1534,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             fpl.xq = A.xrun > 0 ? A.xq : nullptr;
             // the level's subject-code rows, from the descriptors its plan just wrote
             HIPCHECK(anyseq_launch_aff_scode(d_probs, L.nh, std::max(n, m), st));
-            HIPCHECK(hipEventRecord(E.pl_ev[2 * li], st));
+            if (timed) HIPCHECK(hipEventRecord(E.pl_ev[2 * li], st));
             HIPCHECK(anyseq_launch_fill_affine(L.nw, d_probs, d_groups, L.slots, ctr, d_err + li, &fpl, L.grid, st));
-            HIPCHECK(hipEventRecord(E.pl_ev[2 * li + 1], st));
+            if (timed) HIPCHECK(hipEventRecord(E.pl_ev[2 * li + 1], st));
             if (check_rows) {
                 // the invariant the next launch relies on: every hand-off row word is the
                 // sentinel again (ANYSEQ_CHECK_ROWS=2 first leaves a stale word past w in
@@ -1663,7 +1667,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             if (err) fail("fill kernel reported error %u (spin timeout; planned level %d)", err, li + 1);
             if (h_tail[8 * li + 1]) fail("internal: planned level %d: a half exceeds its group slots", li + 1);
             float ms = 0.f;
-            HIPCHECK(hipEventElapsedTime(&ms, E.pl_ev[2 * li], E.pl_ev[2 * li + 1]));
+            if (timed) HIPCHECK(hipEventElapsedTime(&ms, E.pl_ev[2 * li], E.pl_ev[2 * li + 1]));
             g_fill_ms += ms;
             g_fill_launches += 1;
             uint64_t cells;
@@ -2280,6 +2284,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "io_skew") g_tuning.io_skew = value;
     else if (n == "io_poll2") g_tuning.io_poll2 = value;
     else if (n == "io_forward") g_tuning.io_fwd = value;
+    else if (n == "fill_events") g_tuning.fill_events = value;
     else if (n == "virtual_best") g_tuning.virtbest = value;
     else if (n == "affine_device_plan") g_tuning.devplan = value;
     else if (n == "affine_device_final") g_tuning.devfinal = value;

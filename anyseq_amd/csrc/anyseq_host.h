@@ -98,6 +98,10 @@ struct Tuning {
     int io_skew = 0;     // affine fill: the I/O wave's skewed blocks per pass while a poll is out (0: 8)
     int io_poll2 = 0;    // affine fill: the I/O wave keeps two hand-off polls in flight
     int io_fwd = 1;      // affine fill with code rows: the I/O wave as the plain forwarder (io_forward)
+    // HIP events around every fill launch (its duration for last_fill_stats); each record
+    // costs a ~5 us gap in the queue before and after the launch (tools/micro/gap_micro.hip),
+    // so bench.py times its steps with them off and the kernels in a separate pass
+    int fill_events = 1;
     int devplan = 1;     // affine construct: Hirschberg levels planned on the device (one download)
     int devfinal = 1;    // affine construct, device-planned: the final level's blocks built on the device too
     int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe
@@ -119,6 +123,7 @@ struct FillCtx {
     DevBuf scode;                           // affine: the problems' subject-code rows (DPProblem::scode)
     DevBuf rcheck;                          // ANYSEQ_CHECK_ROWS: the hand-off row check's result words
     bool rows_checked = false;
+    bool timed = true;                      // ev0 / ev1 recorded around the launch (Tuning::fill_events)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int R = 1, NW = 4;
     unsigned long long* stamps = nullptr;   // diagnostic build only

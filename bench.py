@@ -86,6 +86,9 @@ def parse():
                     help="config 1 only: affine gap open (extend -1); 0 = the reference's linear scheme")
     ap.add_argument("--fasta", nargs=2, metavar=("QUERY", "SUBJECT"), help="configs 3/4: real genome files")
     ap.add_argument("--cpu-runs", type=int, default=5, help="CPU baseline repetitions per thread count")
+    ap.add_argument("--kernel-steps", type=int, default=3,
+                    help="steps of the kernel-timing pass after the timed region (configs 1 / 2 at 65536^2: "
+                         "HIP events around every fill launch; the timed region runs without them)")
     ap.add_argument("--no-anchor", action="store_true",
                     help="N=1 configs[2] line: skip the configs[4] N=1 scaling anchor (a child run)")
     ap.add_argument("--dry-run", action="store_true",
@@ -313,6 +316,12 @@ def construct_bench(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # configs[2]: the timed steps run without the per-launch fill events (each record costs
+    # a ~5 us queue gap before and after the launch, ~0.1 ms per construct); the fill
+    # kernels are timed with them in a pass of --kernel-steps right after
+    separate = args.config == 2
+    if separate:
+        A.set_option("fill_events", 0)
     A.last_fill_stats()
     ts = []
     score = None
@@ -323,6 +332,18 @@ def construct_bench(args):
         ts.append(time.perf_counter() - t)
     elapsed = sum(ts)
     fill_ms, launches, fill_cells = A.last_fill_stats()
+    kernel_timing = {"steps": args.steps, "how": "HIP events around every fill launch, inside the timed region"}
+    if separate:
+        A.set_option("fill_events", 1)
+        kt = max(1, args.kernel_steps)
+        for _ in range(kt):
+            step()
+        torch.cuda.synchronize()
+        fill_ms, launches, fill_cells = A.last_fill_stats()
+        fill_ms, launches, fill_cells = fill_ms * args.steps / kt, launches * args.steps // kt, fill_cells * args.steps // kt
+        kernel_timing = {"steps": kt, "how": "HIP events around every fill launch (stream order) in a pass of "
+                         "--kernel-steps construct steps right after the timed region, which runs without them: "
+                         "each record adds a ~5 us queue gap before and after a launch (tools/micro/gap_micro.hip)"}
     # size-independent check: the alignment re-scored on the host equals the optimum
     rs = genome.affine_rescore(alq.cpu().numpy().tobytes(), als.cpu().numpy().tobytes(), **AFFINE)
     if rs != score:
@@ -343,6 +364,7 @@ def construct_bench(args):
                              "affine_local" if kind == "local" else "affine",
                              f"fill_affine_kernel<{kind}> construct {n}x{m}"),
     }
+    out["roofline"]["kernel_timing"] = kernel_timing
     if args.config == 2:
         out["roofline"]["chain_model"] = chain_model(n, m, fill_ms / max(args.steps, 1), elapsed * 1e3 / args.steps)
         out["roofline"]["binding"] = (
@@ -478,6 +500,11 @@ def score_bench(args, world, rank, local_rank):
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    # one GPU, 65536^2: timed without the per-launch fill events, the kernels in a separate
+    # pass (as construct_bench; the genome-length and multi-rank steps keep them inline)
+    separate = world == 1 and not args.sharded and not genome
+    if separate:
+        A.set_option("fill_events", 0)
     A.last_fill_timing()
     ts = []
     t0 = time.perf_counter()
@@ -491,6 +518,17 @@ def score_bench(args, world, rank, local_rank):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     fill_ms, launches = A.last_fill_timing()
+    kernel_timing = {"steps": args.steps, "how": "HIP events around every fill launch, inside the timed region"}
+    if separate:
+        A.set_option("fill_events", 1)
+        kt = max(1, args.kernel_steps)
+        for _ in range(kt):
+            step()
+        torch.cuda.synchronize()
+        fill_ms, launches = A.last_fill_timing()
+        kernel_timing = {"steps": kt, "how": "HIP events around every fill launch (stream order) in a pass of "
+                         "--kernel-steps steps right after the timed region, which runs without them: each "
+                         "record adds a ~5 us queue gap before and after a launch (tools/micro/gap_micro.hip)"}
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -533,6 +571,7 @@ def score_bench(args, world, rank, local_rank):
             "roofline": roofline("fill_affine_kernel" if aff else "fill_kernel", cells_per_launch, kernel_ms,
                                  valu_key, tag),
         }
+        out["roofline"]["kernel_timing"] = kernel_timing
         if world == 1 and not args.no_cpu_baseline:
             from oracle import oracle as O
             if genome or aff:

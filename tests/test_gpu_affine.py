@@ -116,6 +116,7 @@ def test_affine_waves_per_group(anyseq, oracle, nw):
     ("io_poll2", 1, 0),                                           # two hand-off polls in flight
     ("io_skew", 2, 0),                                            # skewed blocks per polling pass
     ("priority", 0, -1), ("priority", 3, -1),                     # issue priority
+    ("fill_events", 0, 1),                                        # no HIP events around the fills (bench's timed steps)
     ("affine_asm", 97, 1), ("affine_asm", 33, 1), ("affine_asm", 65, 1),   # round-3 ends / the start only / the end only
 ])
 def test_affine_io_modes(anyseq, oracle, option, value, default):
