@@ -3,7 +3,7 @@
 # with test ids and the in-tree libraries it loaded, smoke, the profile set (bench lines,
 # kernel traces, PMC passes: tools/profile.sh), configs[3] and configs[4] at N=1.
 set -o pipefail
-O=gpurun_out/r05z; mkdir -p $O
+O=gpurun_out/r05z; mkdir -p $O   # (rerun: the final build)
 ANYSEQ_MAPS_OUT=$O/loaded_libs.txt timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rA --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || exit 1
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); import sys; sys.path.insert(0, 'tests'); import conftest; [print('loaded', r, d) for r, d in conftest.loaded_libraries()]" > $O/smoke.log 2>&1 || exit 1
 timeout -k 10 1500 bash tools/profile.sh r05z > $O/profile.log 2>&1 || exit 1
