@@ -115,6 +115,63 @@ SUBST = {
 }
 
 
+def r2_transform(body):
+    """Two rows per lane (round 5 projection, G space): after each step's cell A (row 2l)
+    the lane computes cell B (row 2l+1) from A without a lane shift -- B's own E chain,
+    its LUT (the other query code, the same subject byte), its diagonal from A's previous
+    step, F and H from A's new cell -- and the lane shifts, the shift register and the
+    publish carry B's cells (the band's bottom row).  A's rotation v128..v135 is mirrored
+    by B's v168..v175; v176 / v177 are B's diagonal sum and weight bytes."""
+    def bmap(r):
+        n = int(r[1:])
+        return f"v{n + 40}" if 128 <= n <= 135 else r
+    out, prev_oga, perm_src, byte, cur_oga = [], "v134", None, 0, None
+    for l in body:
+        m = re.match(r"v_mov_b32_dpp (v\d+), (\S+) (wave_shr|wave_shl)(.*)", l)
+        if m:
+            dst, src = m.group(1), m.group(2)
+            if m.group(3) == "wave_shl":
+                dst = bmap(dst)
+            src = bmap(src) if src.startswith("v") else src
+            out.append(f"v_mov_b32_dpp {dst}, {src} {m.group(3)}{m.group(4)}")
+            continue
+        m = re.match(r"ds_write_b64 (v\d+), v\[(\d+):(\d+)\](.*)", l)
+        if m:
+            a0, a1 = int(m.group(2)), int(m.group(3))
+            if 128 <= a0 <= 135:
+                a0, a1 = a0 + 40, a1 + 40
+            out.append(f"ds_write_b64 {m.group(1)}, v[{a0}:{a1}]{m.group(4)}")
+            continue
+        m = re.match(r"v_mov_b32_e32 (%\[(?:cur|fd)\]), (v\d+)$", l)
+        if m:
+            out.append(f"v_mov_b32_e32 {m.group(1)}, {bmap(m.group(2))}")
+            continue
+        m = re.match(r"v_perm_b32 v160, %\[lh\], %\[ll\], (v\d+)", l)
+        if m:
+            perm_src = m.group(1)
+        m = re.search(r"src1_sel:BYTE_(\d)", l)
+        if m and l.startswith("v_add_u32_sdwa v137"):
+            byte = int(m.group(1))
+        m = re.match(r"v_max3_i32 (v\d+), v137, %\[e\], (v\d+)", l)
+        if m:
+            cur_oga = m.group(1)
+        out.append(l)
+        m = re.match(r"v_max_i32_e32 (v\d+), (v\d+), %\[hg\]$", l)
+        if m and cur_oga:
+            ofa = m.group(1)
+            out.append("v_max_i32_e32 %[eb], %[eb], %[hgb]")
+            if perm_src:
+                out.append(f"v_perm_b32 v177, %[lhb], %[llb], {perm_src}")
+                perm_src = None
+            out.append(f"v_add_u32_sdwa v176, {prev_oga}, sext(v177) dst_sel:DWORD dst_unused:UNUSED_PAD "
+                       f"src0_sel:DWORD src1_sel:BYTE_{byte}")
+            out.append(f"v_max3_i32 {bmap(cur_oga)}, v176, %[eb], {ofa}")
+            out.append(f"v_add_u32_e32 %[hgb], %[go], {bmap(cur_oga)}")
+            out.append(f"v_max_i32_e32 {bmap(ofa)}, {ofa}, %[hgb]")
+            prev_oga, cur_oga = cur_oga, None
+    return out
+
+
 def main():
     name, out = sys.argv[1], sys.argv[2]
     text = open("anyseq_amd/csrc/anyseq_block_asm.inc").read()
@@ -132,6 +189,15 @@ def main():
             for l in sel:
                 f.write(f'    "{l}\\n" \\\n')
             f.write('    ""\n')
+        r2 = r2_transform(body)
+        for sub, keep in (("R2FULL", SUBSETS["FULL"]), ("R2VALU", SUBSETS["VALU"])):
+            sel = [l for l in r2 if kind(l) in keep]
+            f.write(f"#define MIX_{sub}_N {len(sel)}\n")
+            f.write(f"#define MIX_{sub} \\\n")
+            for l in sel:
+                f.write(f'    "{l}\\n" \\\n')
+            f.write('    ""\n')
+        f.write("#define MIX_R2_CLOBBERS " + ", ".join(f'"v{n}"' for n in range(168, 178)) + "\n")
         valu = [l for l in body if kind(l) == "valu"]
         for sub, fn in SUBST.items():
             f.write(f"#define MIX_{sub}_N {len(valu)}\n")
