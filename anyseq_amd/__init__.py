@@ -97,6 +97,7 @@ _lib.anyseq_last_fill_timing.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes
 _lib.anyseq_last_fill_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int),
                                         ctypes.POINTER(_c_i64)]
 _lib.anyseq_last_shard_plan.restype = _c_int
+_lib.anyseq_last_fill_two_row_launches.restype = _c_int
 _lib.anyseq_main_random_pair.argtypes = [_c_i64, _c_i64, _vp, ctypes.POINTER(_c_i64), _vp,
                                          ctypes.POINTER(_c_i64)]
 
@@ -287,6 +288,11 @@ def last_fill_stats():
     ms, n, c = ctypes.c_double(0.0), _c_int(0), _c_i64(0)
     _lib.anyseq_last_fill_stats(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(c))
     return ms.value, n.value, c.value
+
+
+def last_fill_two_row_launches() -> int:
+    """Affine fill launches since the previous call that ran two rows per lane; resets it."""
+    return int(_lib.anyseq_last_fill_two_row_launches())
 
 
 def last_shard_plan() -> int:

@@ -88,6 +88,7 @@ constexpr int CPU_BLOCK_WIDTH = 1024;              // iteration_cpu.impala:1 (hb
 thread_local std::string g_last_error;
 thread_local double g_fill_ms = 0.0;
 thread_local int g_fill_launches = 0;
+thread_local int g_fill_r2 = 0;   // affine launches with two rows per lane (anyseq_last_fill_two_row_launches)
 thread_local int g_shard_blocked_levels = 0;   // anyseq_last_shard_plan
 thread_local int64_t g_fill_cells = 0;
 
@@ -300,6 +301,7 @@ void init_tuning_locked() {
     g_tuning.prio = env_int("ANYSEQ_PRIO", g_tuning.prio);
     g_tuning.thr = env_int("ANYSEQ_THROTTLE", g_tuning.thr);
     g_tuning.NWa = env_int("ANYSEQ_NWA", g_tuning.NWa);
+    g_tuning.arows = env_int("ANYSEQ_AFF_ROWS", g_tuning.arows);
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
@@ -374,13 +376,32 @@ int aff_waves_for(int64_t chain_steps, int64_t wave_steps, int grid) {
     return t7 < 0.9 * t4 ? 7 : 4;
 }
 
+// Affine fill, rows per lane of one launch (round 5): two rows per lane
+// share the step's lane shifts, so a wave covers 128 rows per step at 1.5x the one-row step
+// time at two waves per SIMD (124.9 against 83.3 cycles per wave, tools/micro/mix_micro.hip
+// R2FULL / FULL, profiles/r05aa_mix_micro_r2.txt): 1.33x the throughput, but the band
+// chain steps at 1.5x for a hop over 128 rows (chain2 = w + 0.64 h).  Taken by NW 7
+// launches (throughput-bound) when the model gains >= 10 %; an explicit
+// affine_rows_per_lane wins (2 needs NW 4 or 7).
+int aff_rows_for(int NW, int64_t chain, int64_t chain2, int64_t work, int grid) {
+    if (g_tuning.arows == 1) return 1;
+    if (g_tuning.arows == 2) return NW == 4 || NW == 7 ? 2 : 1;
+    if (NW != 7) return 1;
+    const double g = (double)std::max(grid, 1);
+    const double t1 = std::max((double)chain, (double)work / (7.0 * g));
+    const double t2 = 1.5 * std::max((double)chain2, (double)work / (14.0 * g));
+    return t2 < 0.9 * t1 ? 2 : 1;
+}
+
 namespace {
-void aff_launch_model(const std::vector<DPProblem>& probs, int64_t& chain, int64_t& work) {
+void aff_launch_model(const std::vector<DPProblem>& probs, int64_t& chain, int64_t& work, int64_t* chain2 = nullptr) {
     chain = 0;
     work = 0;
+    if (chain2) *chain2 = 0;
     for (const DPProblem& P : probs) {
         if (P.h <= 0 || P.w <= 0) continue;
         chain = std::max(chain, (int64_t)P.w + (int64_t)P.h * 128 / 100);
+        if (chain2) *chain2 = std::max(*chain2, (int64_t)P.w + (int64_t)P.h * 64 / 100);
         work += (int64_t)((P.h + 63) / 64) * ((int64_t)P.w + 64);
     }
 }
@@ -432,12 +453,13 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     const bool aff = fp.affine != 0;
     // the affine fill has one row per lane and hands (G, F) pairs over (twice the row bytes)
     int NW = waves_per_group();
-    const int R = aff ? 1 : rows_per_lane();
+    int R = aff ? 1 : rows_per_lane();
     if (aff) {
-        int64_t chain, work;
-        aff_launch_model(probs, chain, work);
+        int64_t chain, work, chain2;
+        aff_launch_model(probs, chain, work, &chain2);
         const int g0 = grid_req > 0 ? grid_req : (g_tuning.grida > 0 ? g_tuning.grida : E.num_cus);
         NW = aff_waves_for(chain, work, g0);
+        R = aff_rows_for(NW, chain, chain2, work, g0);   // (affine bands: 64 R rows)
     }
     const int vpc = aff ? 2 : 1;
     // Persistent grid: at most `grid` groups are in flight, and a group finishes only after
@@ -574,6 +596,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     if (aff) HIPCHECK(anyseq_launch_aff_scode(d_probs, (int)probs.size(), scode_max_w, st));
     FillParams fpl = fp;
     fpl.epoch = epoch;
+    fpl.arows = aff ? R : 0;
     fpl.xq = xrun > 0 ? reinterpret_cast<const uint32_t*>(d_groups + groups.size()) : nullptr;
     fpl.prio = fill_prio(aff);
     fpl.throttle = g_tuning.thr;
@@ -712,6 +735,7 @@ void fill_collect(FillCtx& C) {
     g_fill_ms += ms;
     g_fill_launches += 1;
     g_fill_cells += C.cells;
+    if (C.aff && C.R == 2) g_fill_r2 += 1;
     const uint32_t err = C.err_host ? *(volatile uint32_t*)C.err_host : 0u;
     if (C.rows_checked && !err) {
         uint32_t c[8];
@@ -2272,6 +2296,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "grid") g_tuning.grid = value;
     else if (n == "fronts") g_tuning.fronts = value;
     else if (n == "affine_waves_per_group") g_tuning.NWa = value;
+    else if (n == "affine_rows_per_lane") g_tuning.arows = value;
     else if (n == "affine_grid") g_tuning.grida = value;
     else if (n == "affine_asm") g_tuning.affasm = value;
     else if (n == "ring_slots") g_tuning.ring_slots = value;
@@ -2305,6 +2330,12 @@ void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells) {
     g_fill_ms = 0.0;
     g_fill_launches = 0;
     g_fill_cells = 0;
+}
+
+int anyseq_last_fill_two_row_launches(void) {
+    const int v = g_fill_r2;
+    g_fill_r2 = 0;
+    return v;
 }
 
 int anyseq_last_shard_plan(void) {

@@ -150,6 +150,7 @@ struct FillParams {
     int32_t io_skew;                  // affine I/O wave: skewed blocks per pass while a poll is out (0: 8)
     int32_t io_poll2;                 // affine I/O wave: two hand-off polls in flight
     int32_t io_fwd;                   // affine I/O wave with code rows (GS): 1 the forwarder io_forward, 0 io_wave
+    int32_t arows;                    // affine: rows per lane, 1 or 2 (0 = 1); nbands counts 64 * arows rows
     // XCD-local groups (round 5): null = one global queue in group-table
     // order; else the table is partitioned by XCD (xcd_of_group), xq[x] .. xq[x+1] the
     // groups of XCD x in k-major order, dequeued by that XCD's workgroups through the

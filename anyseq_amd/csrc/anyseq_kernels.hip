@@ -390,14 +390,14 @@ __device__ __forceinline__ void load_sbytes(const uint8_t* s_ring, int p, uint32
 }
 
 // Column-block sharding: wait until the transported left column holds every row
-// this band reads (rows rb-1 .. min(rb+63, h-1), rb = lane 0's row): the chunk
+// this band reads (rows rb-1 .. min(rb+span-1, h-1), rb = lane 0's row): the chunk
 // flag of the band's last row (flags are set in chunk order, DPProblem::left_flag).
 // Without flags (local direct mode) the kernel-written words themselves are polled
 // against the sentinel.  Returns false on timeout.
-__device__ __forceinline__ bool wait_left(const DPProblem& P, int row, uint32_t* err) {
+__device__ __forceinline__ bool wait_left(const DPProblem& P, int row, uint32_t* err, int span = 64) {
     if (!P.left_flag) return true;
     const int rb = __builtin_amdgcn_readfirstlane(row);
-    const int last = min(rb + 63, P.h - 1);
+    const int last = min(rb + span - 1, P.h - 1);
     if (last < 0) return true;
     uint32_t* f = const_cast<uint32_t*>(P.left_flag) + last / P.left_chunk;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -415,8 +415,9 @@ __device__ __forceinline__ bool wait_left(const DPProblem& P, int row, uint32_t*
 // This lane's left-border values H[row][-1] and H[row-1][-1] from the problem's
 // left_in buffer (row -1 is the corner, whose value is the scheme's border in
 // every shard frame).  Returns false on timeout.
-__device__ __forceinline__ bool poll_left(const DPProblem& P, int row, int32_t& v1, int32_t& v0, uint32_t* err) {
-    if (!wait_left(P, row, err)) return false;
+__device__ __forceinline__ bool poll_left(const DPProblem& P, int row, int32_t& v1, int32_t& v0, uint32_t* err,
+                                          int span = 64) {
+    if (!wait_left(P, row, err, span)) return false;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t it = 0;
     for (;;) {
@@ -458,9 +459,12 @@ __device__ __forceinline__ bool poll_left_e(const DPProblem& P, int row, int32_t
 // band order (waits for the band above to publish first), system scope, so the
 // transport stream's hipStreamWaitValue32 and the kernel that sends the rows see
 // the data.  Returns false on timeout.
-__device__ __forceinline__ bool publish_progress(const DPProblem& P, int band, int lane, uint32_t* err) {
+// (units: 64-row bands; a band of `units` x 64 rows publishes that many at once)
+__device__ __forceinline__ bool publish_progress(const DPProblem& P, int band, int lane, uint32_t* err,
+                                                 int units = 1) {
     __threadfence_system();
     bool ok = true;
+    band *= units;
     if (lane == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint32_t it = 0;
@@ -472,7 +476,7 @@ __device__ __forceinline__ bool publish_progress(const DPProblem& P, int band, i
                 break;
             }
         }
-        if (ok) __hip_atomic_store(P.progress, (uint32_t)(band + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (ok) __hip_atomic_store(P.progress, (uint32_t)(band + units), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     return __shfl(ok ? 1 : 0, 0) != 0;
 }
@@ -1540,6 +1544,7 @@ struct Aff2Args {
     uint64_t gp;
     uint64_t sg;   // GS: the problem's subject-code rows (skb: the lane's byte offset at block 0)
     int q, wm, wx, ll, lh, zlp;
+    int qb, llb, lhb, zlpb;   // two rows per lane: row B's query code, LUT and clamp bound
 };
 #ifdef ANYSEQ_STAMPS
 #define AF2_NAME(NAME) NAME##_TS
@@ -1654,9 +1659,148 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
 #undef AF2E_ASM
 #undef AF2F_ASM
 
-template <bool PARTIAL>
-__device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k,
+// Two rows per lane (gen_aff2 r2): row A's state in e / hg / bx and the loop-carried cell
+// ga (row B's diagonal), row B's in g / fdn (the lane-shifted cell, as one row's) and
+// eb / hgb / bxb.  No diagnostic-stamp variants.
+#define AF2R_OUTS                                                                                              \
+    [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e), [hg] "+v"(hg), \
+        [best] "+v"(bx), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf), [sc] "+s"(sc), [pf] "+s"(pf), [st] "=&s"(st), \
+        [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3), [x4] "=&s"(x4), [ga] "+v"(ga),            \
+        [eb] "+v"(eb), [hgb] "+v"(hgb), [bestb] "+v"(bxb)
+#define AF2R_INS                                                                                               \
+    [be] "s"(be), [q] "v"(a.q), [wm] "v"(a.wm), [wx] "v"(a.wx), [ll] "v"(a.ll), [lh] "v"(a.lh), [go] "v"(go),     \
+        [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr), [acn] "v"(a.acn),          \
+        [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl), [skb] "v"(a.skb), [lo] "v"(a.lo),  \
+        [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp), [thr] "s"(thr),         \
+        [sg] "s"(sg), [qb] "v"(a.qb), [llb] "v"(a.llb), [lhb] "v"(a.lhb), [zlpb] "v"(a.zlpb)
+#define AF2R_ASM(NAME) asm volatile(NAME : AF2R_OUTS : AF2R_INS : ANYSEQ_AF2R_ASM_CLOBBERS, "memory")
+#define AF2RE_ASM(NAME)                                                                                   \
+    asm volatile(NAME : AF2R_OUTS, [cnt] "+v"(cnt), [gc] "+v"(gc), [ec] "+v"(ec), [gcb] "+v"(gcb),        \
+                 [ecb] "+v"(ecb), [fc] "+v"(fc) : AF2R_INS, [nch] "s"(nch) : ANYSEQ_AF2R_ASM_CLOBBERS, "memory")
+#define AF2RF_ASM(NAME)                                                                                   \
+    asm volatile(NAME : AF2R_OUTS : AF2R_INS, [nch] "s"(nch), [neg] "s"(negp) : ANYSEQ_AF2R_ASM_CLOBBERS, "memory")
+// EPI as aff2_loop_asm; cap = {cnt, ga, ea, g, e, fdn} (EPI 1)
+template <bool L, bool BORDER, int PUB, bool LUT, int EPI = 0>
+__device__ __forceinline__ uint32_t aff2r_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
+                                                   const Aff2Args& a, int go, int nge, int& g, int& fdn, int& dg,
+                                                   int2& tf, int& e, int& hg, int& bx, int& ga, int& eb, int& hgb,
+                                                   int& bxb, uint32_t nch = 0, int* cap = nullptr) {
+    uint32_t st, x0, x1, x2, x3, x4, pf = 0;
+    const uint64_t hm = 0xffff000000000000ull;   // lanes 48..63 (publishing)
+#define RFL(x) __builtin_amdgcn_readfirstlane(x)
+    b = RFL(b);
+    sp = RFL(sp);
+    sf = RFL(sf);
+    sc = RFL(sc);
+    be = RFL(be);
+    const uint32_t rb = RFL(a.rb), nb = RFL(a.nb), bvs = RFL(a.bvs), thr = RFL(a.thr);
+    const int ge = RFL(-nge);
+    const uint64_t gp = ((uint64_t)(uint32_t)RFL((uint32_t)(a.gp >> 32)) << 32) | (uint32_t)RFL((uint32_t)a.gp);
+    const uint64_t sg = ((uint64_t)(uint32_t)RFL((uint32_t)(a.sg >> 32)) << 32) | (uint32_t)RFL((uint32_t)a.sg);
+#undef RFL
+    int tfg = tf.x, tff = tf.y;
+#define AF2R_SEL(A, V, K, U)                                                          \
+    if constexpr (BORDER && PUB == 0) A(ANYSEQ_##V##_##K##_B1_NONE_U##U);            \
+    if constexpr (BORDER && PUB == 1) A(ANYSEQ_##V##_##K##_B1_LDS_U##U);             \
+    if constexpr (BORDER && PUB == 2) A(ANYSEQ_##V##_##K##_B1_GLOB_U##U);            \
+    if constexpr (!BORDER && PUB == 0) A(ANYSEQ_##V##_##K##_B0_NONE_U##U);           \
+    if constexpr (!BORDER && PUB == 1) A(ANYSEQ_##V##_##K##_B0_LDS_U##U);            \
+    if constexpr (!BORDER && PUB == 2) A(ANYSEQ_##V##_##K##_B0_GLOB_U##U);
+    if constexpr (EPI == 1) {
+        nch = __builtin_amdgcn_readfirstlane(nch);
+        int cnt = cap[0], gc = cap[1], ec = cap[2], gcb = cap[3], ecb = cap[4], fc = cap[5];
+        if constexpr (L && LUT) { AF2R_SEL(AF2RE_ASM, AF2RE, L, 1) }
+        if constexpr (L && !LUT) { AF2R_SEL(AF2RE_ASM, AF2RE, L, 0) }
+        if constexpr (!L && LUT) { AF2R_SEL(AF2RE_ASM, AF2RE, G, 1) }
+        if constexpr (!L && !LUT) { AF2R_SEL(AF2RE_ASM, AF2RE, G, 0) }
+        cap[0] = cnt, cap[1] = gc, cap[2] = ec, cap[3] = gcb, cap[4] = ecb, cap[5] = fc;
+    } else if constexpr (EPI == 2) {
+        nch = __builtin_amdgcn_readfirstlane(nch);
+        const uint32_t negp = __builtin_amdgcn_readfirstlane(a.neg);
+        if constexpr (L && LUT) { AF2R_SEL(AF2RF_ASM, AF2RF, L, 1) }
+        if constexpr (L && !LUT) { AF2R_SEL(AF2RF_ASM, AF2RF, L, 0) }
+        if constexpr (!L && LUT) { AF2R_SEL(AF2RF_ASM, AF2RF, G, 1) }
+        if constexpr (!L && !LUT) { AF2R_SEL(AF2RF_ASM, AF2RF, G, 0) }
+    } else {
+        (void)nch;
+        if constexpr (L && LUT) { AF2R_SEL(AF2R_ASM, AF2R, L, 1) }
+        if constexpr (L && !LUT) { AF2R_SEL(AF2R_ASM, AF2R, L, 0) }
+        if constexpr (!L && LUT) { AF2R_SEL(AF2R_ASM, AF2R, G, 1) }
+        if constexpr (!L && !LUT) { AF2R_SEL(AF2R_ASM, AF2R, G, 0) }
+    }
+#undef AF2R_SEL
+    tf = make_int2(tfg, tff);
+    return st;
+}
+#undef AF2R_OUTS
+#undef AF2R_INS
+#undef AF2R_ASM
+#undef AF2RE_ASM
+#undef AF2RF_ASM
+
+// Two rows per lane: aff_block for rows A = 2l and B = 2l+1 of a 128-row band at the
+// same column (the lane's column c0 + u at step u).  Row A takes its up / F-in from row B
+// of the lane above (DPP, lane 0: the top row); row B its diagonal from A's previous
+// cell (ga), its up and F-in from A's new cell.  og / of: row B's (the band's bottom
+// row at lane 63).  zca / zba: row A's clamp bound / true Z of the first step (row B's
+// are one -ge further).  PARTIAL: a dead row passes the row above through.
+template <bool MASK, bool PARTIAL, bool VIRT>
+__device__ __forceinline__ void aff_block2(int c0, int w, int2 tf, const int2 (&rv)[32], const uint32_t (&sw)[8],
+                                           int qa, int qb, bool deada, bool deadb, int zca, int zba, int& ga,
+                                           int& ea, int& hga, int& dg, int& g, int& e, int& hg, int& fdn, int& besta,
+                                           int& best, int (&og)[32], int (&of)[32], const AffK k) {
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+        const int2 top = u == 0 ? tf : rv[u - 1];
+        const int upg = wave_shr1(top.x, g);
+        const int fin = wave_shr1(top.y, fdn);
+        const bool vcol = VIRT && c0 + u < 0;
+        const int sb = (int)((sw[u >> 2] >> (8 * (u & 3))) & 0xffu);
+        const int wa = vcol ? kAffNeg : (qa == sb ? k.wm : k.wx);
+        const int wb = vcol ? kAffNeg : (qb == sb ? k.wm : k.wx);
+        const int zu = zca + u * k.nge, zt = zba + u * k.nge;
+        // row A
+        const int ena = max(ea, hga);
+        int va = max(max(max(dg + wa, ena), fin), zu);
+        const int hna = va + k.go;
+        int fna = max(fin, hna);
+        if (PARTIAL && deada) {
+            va = upg;
+            fna = fin;
+        }
+        // row B
+        const int enb = max(e, hg);
+        int vb = max(max(max(ga + wb, enb), fna), zu + k.nge);
+        const int hnb = vb + k.go;
+        int fnb = max(fna, hnb);
+        if (PARTIAL && deadb) {
+            vb = va;
+            fnb = fna;
+        }
+        const bool act = MASK ? (VIRT ? (c0 + u < w) : ((unsigned)(c0 + u) < (unsigned)w)) : true;
+        ea = act ? ena : ea;
+        ga = act ? va : ga;
+        hga = act ? hna : hga;
+        besta = act ? max(besta, va - zt) : besta;
+        e = act ? enb : e;
+        g = act ? vb : g;
+        hg = act ? hnb : hg;
+        fdn = act ? fnb : fdn;
+        best = act ? max(best, vb - (zt + k.nge)) : best;
+        dg = upg;
+        og[u] = g;
+        of[u] = fdn;
+    }
+}
+
+// RR: rows per lane.  RR 2 (round 5): lane l holds rows 2l (A) and 2l+1 (B) of a 128-row
+// band at the same column (aff_block2, gen_aff2 r2); `row`, g / e / hg / fdn are the lane's
+// bottom row (B), ga / ea / hga / besta row A, dg row A's diagonal.  The hand-off rows,
+// rings and steps are the one-row band's.
+template <bool PARTIAL, int RR>
+__device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k,
                              unsigned long long* dbg) {
+    static_assert(RR == 1 || RR == 2, "one or two rows per lane");
     constexpr int CH = 32;
     constexpr int IRM = kSlots * CH - 1;
     constexpr int LAG = 2;   // lane 63 finishes column c at step c + 64: chunk j is complete after block j + 2
@@ -1700,30 +1844,46 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     const bool ff_loses = k.lut || k.wx <= 2 * nge;
     const bool virt = ASM_OK && !shard_left && !zero_open && !(bestmode == 2 && finite_left) && best_border_ok &&
                       (!clamp || (k.codes && ff_loses)) && !(k.flags & 1);
-    const int rb = band * 64;
-    const int row = rb + lane;
+    const int rb = band * 64 * RR;
+    const int row = rb + RR * lane + (RR - 1);   // the lane's bottom row
+    const int rowt = row - (RR - 1);             // its top row (RR 2: row A)
     const bool dead = row >= h;
     const bool lastrow = row == h - 1;
+    const bool deada = rowt >= h, lasta = RR == 2 && rowt == h - 1;
     int q = dead ? 0x100 : (int)gmem(P.q)[P.q_off + P.q_step * row];
-    // settle the query load here: a vmcnt wait inside the step loop would also wait
+    int qa = RR == 1 ? q : deada ? 0x100 : (int)gmem(P.q)[P.q_off + P.q_step * rowt];
+    // settle the query loads here: a vmcnt wait inside the step loop would also wait
     // for lane 63's HBM row stores
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(q)::"memory");
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(q), "+v"(qa)::"memory");
     if (kAffGS && !P.scode) {   // (a planned level whose code rows did not fit: its bound check fails too)
         if (lane == 0) atomicOr(err, ERR_BAD_DESC);
         return;
     }
     int g, e = kAffNeg, hg, fdn = kAffNeg, dg;
+    int ga = kAffNeg, ea = kAffNeg, hga = kAffNeg;   // RR 2: row A
     int2 tf;
     if (shard_left) {
         int32_t lh1 = 0, lh0 = 0, le1 = 0;
-        if (!poll_left(P, row, lh1, lh0, err)) return;
+        if constexpr (RR == 2) {
+            // row A first (waits for the band's 128 rows), then row B (already landed)
+            int32_t a1 = 0, a0 = 0, ae = 0;
+            if (!poll_left(P, rowt, a1, a0, err, 128)) return;
+            if (!poll_left_e(P, rowt, ae, err)) return;
+            ga = a1 + (rowt + 1) * nge;
+            ea = ae + (rowt + 1) * nge;
+            hga = ga + go;
+            lh0 = a0;
+        }
+        int32_t l0 = 0;
+        if (!poll_left(P, row, lh1, l0, err, RR == 2 ? 127 : 64)) return;
+        if constexpr (RR == 1) lh0 = l0;
         if (!poll_left_e(P, row, le1, err)) return;
         // H space -> G space at column -1: G = H + (r + 1) (-ge); row -1 is the top
         // border of the shard frame (the scheme's: global go, free 0)
         g = lh1 + (row + 1) * nge;
         e = le1 + (row + 1) * nge;
         hg = g + go;
-        dg = row == 0 ? (bm == BM_NORMAL ? go : 0) : lh0 + row * nge;
+        dg = rowt == 0 ? (bm == BM_NORMAL ? go : 0) : lh0 + rowt * nge;
         tf = make_int2(__shfl(dg, 0), kAffNeg);
     } else if (virt) {
         g = kAffNeg;
@@ -1737,10 +1897,14 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
     } else {
         g = B.left(row, nge);
         hg = g + go;   // the next column's E candidate: G[r][-1] + go
-        dg = B.left(row - 1, nge);
+        dg = B.left(rowt - 1, nge);
         tf = make_int2(B.left(rb - 1, nge), kAffNeg);
+        if constexpr (RR == 2) {
+            ga = B.left(rowt, nge);   // (also row B's diagonal at column 0)
+            hga = ga + go;
+        }
     }
-    int best = kAffNeg;
+    int best = kAffNeg, besta = kAffNeg;
     const int nchunks = (w + CH - 1) / CH;
     const int nblocks = nchunks + LAG;
     const int fe = w >= CH - 1 ? (w - (CH - 1)) / CH + 1 : 0;   // full blocks: 32b + 30 < w
@@ -1795,18 +1959,24 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         la.gp = (uint64_t)(size_t)io.gout;
         // diagonal weights in the loop's space: G adds sub - 2 ge, X adds sub - ge
         const int wm = xs ? k.wm - nge : k.wm, wx = xs ? k.wx - nge : k.wx;
-        la.q = q;
         la.wm = wm;
         la.wx = wx;
-        uint32_t ll = 0, lh = 0;
+        // per row: the query code, its LUT (weights against subject codes 0..7) and the
+        // X-space clamp bound - ge (RR 2: %[q] / %[ll] / %[lh] / %[zlp] row A's)
+        auto row_consts = [&](int qr, int r, int& qo, int& llo, int& lho, int& zo) {
+            uint32_t ll = 0, lh = 0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            ll |= (uint32_t)((q == c ? wm : wx) & 0xff) << (8 * c);
-            lh |= (uint32_t)((q == c + 4 ? wm : wx) & 0xff) << (8 * c);
-        }
-        la.ll = (int)ll;
-        la.lh = (int)lh;
-        la.zlp = clamp ? (row + 3) * nge : 2 * kAffNeg;   // X-space clamp bound - ge
+            for (int c = 0; c < 4; ++c) {
+                ll |= (uint32_t)((qr == c ? wm : wx) & 0xff) << (8 * c);
+                lh |= (uint32_t)((qr == c + 4 ? wm : wx) & 0xff) << (8 * c);
+            }
+            qo = qr;
+            llo = (int)ll;
+            lho = (int)lh;
+            zo = clamp ? (r + 3) * nge : 2 * kAffNeg;
+        };
+        row_consts(qa, rowt, la.q, la.ll, la.lh, la.zlp);
+        if constexpr (RR == 2) row_consts(q, row, la.qb, la.llb, la.lhb, la.zlpb);
     }
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
@@ -1825,6 +1995,7 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 // state into the loop's space: the lane's cell of step t0-1 is column t0-2-lane
                 const int cs = t0 - 2 - lane;
                 int bx = kAffNeg;
+                int bxa = kAffNeg;
                 if (xs) {
                     g = to_x(g, cs);
                     hg = to_x(hg, cs);
@@ -1832,6 +2003,11 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                     fdn = to_x(fdn, cs);
                     dg = to_x(dg, cs);
                     tf = make_int2(to_x(tf.x, t0 - 1), to_x(tf.y, t0 - 1));
+                    if constexpr (RR == 2) {
+                        ga = to_x(ga, cs);
+                        hga = to_x(hga, cs);
+                        ea = to_x(ea, cs);
+                    }
                 }
                 uint32_t bb = (uint32_t)b;
                 const int role = (io.in_border ? 3 : 0) + (io.out_lds ? 1 : (io.gout ? 2 : 0));
@@ -1864,9 +2040,13 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                 const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || !best_safe || (k.flags & 32);
                 if (epi && !need_cap) {
 #define AF2_CALL(LV, BD, PB, LU)                                                                                  \
-    st = aff2_loop_asm<LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
-                                          fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), \
-                                          nullptr, dbp)
+    if constexpr (RR == 2)                                                                                        \
+        st = aff2r_loop_asm<LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, \
+                                               g, fdn, dg, tf, ea, hga, bxa, ga, e, hg, bx, (uint32_t)(2 * nchunks)); \
+    else                                                                                                          \
+        st = aff2_loop_asm<LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
+                                              fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), \
+                                              nullptr, dbp)
                     if (xs) {
                         if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
                     } else {
@@ -1877,12 +2057,19 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                         atomicOr(err, ERR_SPIN_TIMEOUT);
                         return;
                     }
-                    if (xs) best = max(best, bx - (row + 2) * nge);
+                    if (xs) {
+                        best = max(best, bx - (row + 2) * nge);
+                        besta = max(besta, bxa - (rowt + 2) * nge);
+                    }
                     break;   // band done (g / e / fdn: nobody reads them)
                 }
 #define AF2_CALL(LV, BD, PB, LU)                                                                               \
-    st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, fdn, \
-                                       dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, nullptr, dbp)
+    if constexpr (RR == 2)                                                                                     \
+        st = aff2r_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
+                                            fdn, dg, tf, ea, hga, bxa, ga, e, hg, bx);                          \
+    else                                                                                                       \
+        st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, fdn, \
+                                           dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, nullptr, dbp)
                 if (xs) {
                     if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
                 } else {
@@ -1896,10 +2083,17 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                     ev_store(7, te_v);                               // main loop end
                     ev_store(8, __builtin_amdgcn_s_memrealtime());   // epilogue entry
 #endif
-                    int cap[4] = {w + lane - (int)bb * CH, g, e, fdn};   // steps until column w-1
+                    // steps until column w-1; the state kept there (RR 2: cap = {cnt, ga, ea, g, e, fdn})
+                    int cap[6] = {w + lane - (int)bb * CH, RR == 2 ? ga : g, RR == 2 ? ea : e, RR == 2 ? g : fdn, e, fdn};
 #define AF2_CALL(LV, BD, PB, LU)                                                                               \
-    st = aff2_loop_asm<LV, BD, PB, LU, 1>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
-                                          fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), cap, dbp)
+    if constexpr (RR == 2)                                                                                     \
+        st = aff2r_loop_asm<LV, BD, PB, LU, 1>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, \
+                                               g, fdn, dg, tf, ea, hga, bxa, ga, e, hg, bx, (uint32_t)(2 * nchunks), \
+                                               cap);                                                           \
+    else                                                                                                       \
+        st = aff2_loop_asm<LV, BD, PB, LU, 1>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
+                                              fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), \
+                                              cap, dbp)
                     if (xs) {
                         if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
                     } else {
@@ -1913,14 +2107,27 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
 #ifdef ANYSEQ_STAMPS
                     ev_store(9, te_v);   // epilogue end
 #endif
-                    g = cap[1];
-                    e = cap[2];
-                    fdn = cap[3];
+                    if constexpr (RR == 2) {
+                        ga = cap[1];
+                        ea = cap[2];
+                        g = cap[3];
+                        e = cap[4];
+                        fdn = cap[5];
+                    } else {
+                        g = cap[1];
+                        e = cap[2];
+                        fdn = cap[3];
+                    }
                     if (xs) {
                         g = to_g(g, w - 1);
                         e = to_g(e, w - 1);
                         fdn = to_g(fdn, w - 1);
                         best = max(best, bx - (row + 2) * nge);
+                        if constexpr (RR == 2) {
+                            ga = to_g(ga, w - 1);
+                            ea = to_g(ea, w - 1);
+                            besta = max(besta, bxa - (rowt + 2) * nge);
+                        }
                     }
                     break;   // band done
                 }
@@ -1939,6 +2146,12 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
                     dg = to_g(dg, ce);
                     tf = make_int2(to_g(tf.x, t1 - 1), to_g(tf.y, t1 - 1));
                     best = max(best, bx - (row + 2) * nge);
+                    if constexpr (RR == 2) {
+                        ga = to_g(ga, ce);
+                        hga = to_g(hga, ce);
+                        ea = to_g(ea, ce);
+                        besta = max(besta, bxa - (rowt + 2) * nge);
+                    }
                 }
                 b = (int)bb - 1;   // ++b of the for
                 continue;
@@ -1994,10 +2207,26 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         if (b == 0) t_b0 = __builtin_amdgcn_s_memrealtime();   // block 0's inputs are ready
 #endif
         const int c0 = t0 - 1 - lane;
-        const int zb = (rb + t0 + 1) * nge;
+        // Z of the lane's first step: (r + c + 2)(-ge), r + c = rb + t0 - 1 (+ lane for row A of RR 2)
+        const int zb = (rb + t0 + 1 + (RR == 2 ? lane : 0)) * nge;
         const int zc = zb + zoff;
         const bool full = (virt || t0 >= 64) && b < fe;
-        if (full) {
+        if constexpr (RR == 2) {
+            if (full) {
+                if (virt)
+                    aff_block2<false, PARTIAL, true>(c0, w, tf, rv, sw, qa, q, deada, dead, zc, zb, ga, ea, hga, dg, g,
+                                                     e, hg, fdn, besta, best, og, of, k);
+                else
+                    aff_block2<false, PARTIAL, false>(c0, w, tf, rv, sw, qa, q, deada, dead, zc, zb, ga, ea, hga, dg,
+                                                      g, e, hg, fdn, besta, best, og, of, k);
+            } else if (virt) {
+                aff_block2<true, PARTIAL, true>(c0, w, tf, rv, sw, qa, q, deada, dead, zc, zb, ga, ea, hga, dg, g, e,
+                                                hg, fdn, besta, best, og, of, k);
+            } else {
+                aff_block2<true, PARTIAL, false>(c0, w, tf, rv, sw, qa, q, deada, dead, zc, zb, ga, ea, hga, dg, g, e,
+                                                 hg, fdn, besta, best, og, of, k);
+            }
+        } else if (full) {
             if (virt)
                 aff_block<false, PARTIAL, true>(c0, w, tf, rv, sw, q, dead, zc, zb, g, e, hg, fdn,
                                                         dg, best, og, of, k);
@@ -2075,19 +2304,32 @@ __device__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO
         // shard: F-down of the last row at the last column (the combine pairs it across shards)
         if (lastrow && P.out_f_last) *gmem(P.out_f_last) = aff_to_h(fdn, row, w - 1, nge);
     }
-    if (P.progress && !publish_progress(P, band, lane, err)) return;
+    if constexpr (RR == 2) {
+        if (!deada) {
+            if (P.out_col) gmem(P.out_col)[rowt] = aff_to_h(ga, rowt, w - 1, nge);
+            if (P.out_col_e) gmem(P.out_col_e)[rowt] = aff_to_h(ea, rowt, w - 1, nge);
+            // (row A last: row B is dead and passed A's F-down through, in fdn)
+            if (lasta && P.out_f_last) *gmem(P.out_f_last) = aff_to_h(fdn, rowt, w - 1, nge);
+        }
+    }
+    if (P.progress && !publish_progress(P, band, lane, err, RR)) return;
     if (bestmode && P.best) {
         // the lane's best covers its row; last-row mode keeps the problem's last row only,
         // last-column mode the lane's cell in the last column
         if (bestmode == 3) best = aff_to_h(g, row, w - 1, nge);
         if (dead || (bestmode == 2 && !lastrow)) best = kAffNeg;
+        if constexpr (RR == 2) {
+            if (bestmode == 3) besta = aff_to_h(ga, rowt, w - 1, nge);
+            if (deada || (bestmode == 2 && !lasta)) besta = kAffNeg;
+            best = max(best, besta);
+        }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
         if (lane == 0) atomicMax(P.best, best);
     }
 }
 
-template <int NW>
+template <int NW, int RR>
 __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProblem* __restrict__ probs,
                                                                      const GroupRef* __restrict__ groups,
                                                                      int ngroups_total, uint32_t* dq, uint32_t* err,
@@ -2203,8 +2445,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                 io.next_prod = band < last ? &sh.prod[wave + 1] : nullptr;
                 io.next_cons = band < last ? &sh.cons[wave + 1] : nullptr;
                 io.gout = band < last ? nullptr : g_out;
-                if ((band + 1) * 64 > P.h) run_band_aff<true>(P, band, lane, io, err, k, fp.dbg);
-                else run_band_aff<false>(P, band, lane, io, err, k, fp.dbg);
+                if ((band + 1) * 64 * RR > P.h) run_band_aff<true, RR>(P, band, lane, io, err, k, fp.dbg);
+                else run_band_aff<false, RR>(P, band, lane, io, err, k, fp.dbg);
             }
         }
         __syncthreads();
@@ -3991,11 +4233,11 @@ static hipError_t launch_fill_c(int R, int NW, const DPProblem* probs, const Gro
     }
 }
 
-template <int NW>
+template <int NW, int RR>
 static hipError_t launch_fill_aff_n(const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
                                     uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((fill_affine_kernel<NW>), dim3(grid), dim3(64 * (NW + 1)), 0, st, probs, groups, ngroups, dq,
-                       err, fp);
+    hipLaunchKernelGGL((fill_affine_kernel<NW, RR>), dim3(grid), dim3(64 * (NW + 1)), 0, st, probs, groups, ngroups,
+                       dq, err, fp);
     return hipGetLastError();
 }
 #endif  // ANYSEQ_MICRO
@@ -4225,9 +4467,15 @@ hipError_t anyseq_launch_fill_affine(int NW, const anyseq::DPProblem* probs, con
                                      hipStream_t st) {
     using namespace anyseq;
     // (the asm steady state holds ~150 fixed VGPRs: at most 2 waves per SIMD, NW <= 7)
-    if (NW == 3) return launch_fill_aff_n<3>(probs, groups, ngroups, dq, err, *fp, grid, st);
-    if (NW == 7) return launch_fill_aff_n<7>(probs, groups, ngroups, dq, err, *fp, grid, st);
-    return launch_fill_aff_n<4>(probs, groups, ngroups, dq, err, *fp, grid, st);
+    // fp->arows 2: two rows per lane (NW 4 or 7; the descriptors' nbands count 128-row bands)
+    if (fp->arows == 2) {
+        if (NW == 7) return launch_fill_aff_n<7, 2>(probs, groups, ngroups, dq, err, *fp, grid, st);
+        if (NW == 4) return launch_fill_aff_n<4, 2>(probs, groups, ngroups, dq, err, *fp, grid, st);
+        return hipErrorInvalidValue;
+    }
+    if (NW == 3) return launch_fill_aff_n<3, 1>(probs, groups, ngroups, dq, err, *fp, grid, st);
+    if (NW == 7) return launch_fill_aff_n<7, 1>(probs, groups, ngroups, dq, err, *fp, grid, st);
+    return launch_fill_aff_n<4, 1>(probs, groups, ngroups, dq, err, *fp, grid, st);
 }
 
 hipError_t anyseq_launch_aff_reduce(int kind, int two, const void* rowF, int h1, const void* rowB, int h2, int m,

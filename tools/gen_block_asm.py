@@ -344,7 +344,19 @@ TSLIGHT = int(os.environ.get("ANYSEQ_GEN_TSLIGHT", "0"))
 AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
-def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
+BR0 = 162          # R2: the second row's cell (G, F) pairs v162..v169 (step u: u % 4)
+B_AAB, B_WBB = 170, 171   # R2: the second row's diagonal + weight, LUT weight bytes
+
+
+def OGB_(u):
+    return v(BR0 + 2 * (u % 4))
+
+
+def OFB_(u):
+    return v(BR0 + 2 * (u % 4) + 1)
+
+
+def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, r2=False):
     """Affine steady-state loop, round 3: full blocks b .. be-1.
     kind G: G space (X_G = X + (r+c+2)|ge|), no clamp, no best (amode 0).
     kind L: X space (X = H + (r+2)|ge|, a per-ROW shift): the local clamp H >= 0 is
@@ -375,8 +387,20 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     a real cell's H; the clamp's 0 is a real cell's floor too), so the maximum is the
     same.  The capture made the epilogue ~1.6x slower per step, and every band's
     epilogue sits on the band chain (a consumer's last main-loop block waits for its
-    producer's last publish, at the producer's epilogue end)."""
+    producer's last publish, at the producer's epilogue end).
+    r2 (round 5): two rows per lane -- lane l holds rows 2l (A) and 2l+1 (B) of a 128-row
+    band at the same column.  A's step is the one-row step with the lane shift reading
+    B's cells of the lane above (%[cur] / %[fd] are B's); B follows without a lane
+    shift: its diagonal is A's cell of the previous step (OG_(u-1); at step 0 the
+    loop-carried %[ga]), its up and F-in A's new cell, its own E chain (%[eb] / %[hgb]),
+    weights (%[qb] or %[llb] / %[lhb]), clamp bound (%[zlpb]) and best (%[bestb]).  The
+    shift register, the publish and the block-end state carry B's cells (the band's bottom
+    row), so the hand-off is the one-row kernel's.  The DPP moves are shared by two cells:
+    16.4 instead of 2 x 11.2 instructions per step (tools/micro/gen_mix_micro.py)."""
     L = kind == "L"
+    assert not r2 or (REORDER and LEAN and SLIM and GS and not ts)
+    OGP, OFP = (OGB_, OFB_) if r2 else (OG_, OF_)   # the published / lane-shifted cells
+    PUBREG = BR0 + 6 if r2 else AO0 + 6
     trailing = pub != "lds"
     out = []
     e = out.append
@@ -596,7 +620,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
             # publishing shift register the cell pair of step 31 does too
             dg = TG_(30)
             if pub == "none":
-                g, f = OG_(31), OF_(31)
+                g, f = OGP(31), OFP(31)
         nsub = (0 if GS else 4) + (1 if border else 0)   # subject reads (+ the border write) at step 8
         for u in range(32):
             if u == 8 and GS:
@@ -688,14 +712,40 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
                     e("v_add_u32_e32 %[e], %[ge], %[e]")
                 e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_max3_i32 {OG_(u)}, v{B_AA}, %[e], {tf}")
-                if sr:
+                if sr and not r2:
                     e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
                 if L and u % 2 == 1 and not (epi and cap):
                     e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
-                if sr:
+                if sr and not r2:
                     e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_max_i32_e32 {OF_(u)}, {tf}, %[hg]")
+                if r2:
+                    # row B: diagonal A's previous cell, up / F-in A's new cell, no lane shift
+                    dgb = OG_(u - 1)   # (step 0: OG_(31), loaded from %[ga] at entry)
+                    if L:
+                        e("v_max3_i32 %[eb], %[eb], %[hgb], %[zlpb]")
+                    else:
+                        e("v_max_i32_e32 %[eb], %[eb], %[hgb]")
+                    if lut:
+                        if u % 4 == 0:
+                            e(f"v_perm_b32 v{B_WBB}, %[lhb], %[llb], {sw}")
+                        e(f"v_add_u32_sdwa v{B_AAB}, {dgb}, sext(v{B_WBB}) dst_sel:DWORD dst_unused:UNUSED_PAD "
+                          f"src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+                    else:
+                        e(f"v_cmp_eq_u32_sdwa vcc, %[qb], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+                        e(f"v_cndmask_b32_e32 v{B_AW}, %[wx], %[wm], vcc")
+                        e(f"v_add_u32_e32 v{B_AAB}, {dgb}, v{B_AW}")
+                    if L:
+                        e("v_add_u32_e32 %[eb], %[ge], %[eb]")
+                    e(f"v_max3_i32 {OGB_(u)}, v{B_AAB}, %[eb], {OF_(u)}")
+                    e(f"v_add_u32_e32 %[hgb], %[go], {OGB_(u)}")
+                    if L and u % 2 == 1 and not (epi and cap):
+                        e(f"v_max3_i32 %[bestb], %[bestb], {OGB_(u - 1)}, {OGB_(u)}")
+                    e(f"v_max_i32_e32 {OFB_(u)}, {OF_(u)}, %[hgb]")
+                    if sr:
+                        e(f"v_mov_b32_dpp {OGB_(u - 1)}, {OGB_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+                        e(f"v_mov_b32_dpp {OFB_(u - 1)}, {OFB_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
             else:
                 if L:
                     e("v_max3_i32 %[e], %[e], %[hg], %[zlp]")
@@ -713,11 +763,20 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
                     e(f"v_max_i32_e32 v{B_AT}, %[best], {OG_(u)}")
                     e("v_cmp_le_i32_e32 vcc, 0, %[cnt]")
                     e(f"v_cndmask_b32_e32 %[best], %[best], v{B_AT}, vcc")
+                    if r2:
+                        e(f"v_max_i32_e32 v{B_AT}, %[bestb], {OGB_(u)}")
+                        e(f"v_cndmask_b32_e32 %[bestb], %[bestb], v{B_AT}, vcc")
                 # the lane whose cell is column w-1 at this step keeps its state
                 e("v_cmp_eq_u32_e32 vcc, 0, %[cnt]")
                 e(f"v_cndmask_b32_e32 %[gc], %[gc], {OG_(u)}, vcc")
                 e("v_cndmask_b32_e32 %[ec], %[ec], %[e], vcc")
-                e(f"v_cndmask_b32_e32 %[fc], %[fc], {OF_(u)}, vcc")
+                if r2:
+                    # (row A's F-down is row B's F-in: only B's is kept)
+                    e(f"v_cndmask_b32_e32 %[gcb], %[gcb], {OGB_(u)}, vcc")
+                    e("v_cndmask_b32_e32 %[ecb], %[ecb], %[eb], vcc")
+                    e(f"v_cndmask_b32_e32 %[fc], %[fc], {OFB_(u)}, vcc")
+                else:
+                    e(f"v_cndmask_b32_e32 %[fc], %[fc], {OF_(u)}, vcc")
                 e("v_add_u32_e32 %[cnt], -1, %[cnt]")
             if not REORDER:
                 if L and u % 2 == 1 and not (epi and cap):
@@ -726,22 +785,22 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
                     e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
                     e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
             if u == 16 and pub != "none":
-                publish(k, 0, AO0 + 6)             # cell pair of step 15: steps 0..15 in lanes 48..63
+                publish(k, 0, PUBREG)              # cell pair of step 15: steps 0..15 in lanes 48..63
                 event(k, 1, EVB + 2)               # producer: first half of chunk EVB published
-            g, f, dg = OG_(u), OF_(u), tg
+            g, f, dg = OGP(u), OFP(u), tg
         if not LEAN or pub != "none":
-            e(f"v_mov_b32_e32 %[cur], {OG_(31)}")
-            e(f"v_mov_b32_e32 %[fd], {OF_(31)}")
+            e(f"v_mov_b32_e32 %[cur], {OGP(31)}")
+            e(f"v_mov_b32_e32 %[fd], {OFP(31)}")
         if not LEAN:
             e(f"v_mov_b32_e32 %[dg], {TG_(30)}")
         if pub != "none":
-            e(f"v_mov_b32_dpp {OG_(31)}, {OG_(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-            e(f"v_mov_b32_dpp {OF_(31)}, {OF_(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_mov_b32_dpp {OGP(31)}, {OGP(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_mov_b32_dpp {OFP(31)}, {OFP(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
         if not LEAN:
             e(f"v_mov_b32_e32 %[tfg], {TG_(31)}")
             e(f"v_mov_b32_e32 %[tff], {TF_(31)}")
         if pub != "none":
-            publish(k, 1, AO0 + 6)                 # pair of step 31: steps 16..31 in lanes 48..63
+            publish(k, 1, PUBREG)                  # pair of step 31: steps 16..31 in lanes 48..63
             event(k, 2, EVB + 2)                   # producer: second half published
             event_last(k, 14, -2)                  # producer: the band's last half published
         event(k, 6, EVB)                           # consumer: block EVB ends
@@ -776,7 +835,9 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True):
     # publish is checked here (the loop checks every other block)
     lean_regs = [("%[dg]", TG_(30)), ("%[tfg]", TG_(31)), ("%[tff]", TF_(31))]
     if pub == "none":
-        lean_regs += [("%[cur]", OG_(31)), ("%[fd]", OF_(31))]
+        lean_regs += [("%[cur]", OGP(31)), ("%[fd]", OFP(31))]
+    if r2:
+        lean_regs += [("%[ga]", OG_(31))]   # row A's cell of the previous step: B's diagonal
     if LEAN:
         for named, reg in lean_regs:
             e(f"v_mov_b32_e32 {reg}, {named}")
@@ -869,9 +930,22 @@ def main():
                             for ln in gen_aff2(kind, border, pub, lut, ts, epi, cap):
                                 lines.append(f'    "{ln}\\n" \\')
                             lines.append("")
+    # two rows per lane (no diagnostic-stamp variants)
+    for kind in ("G", "L"):
+        for border in (0, 1):
+            for pub in ("none", "lds", "glob"):
+                for lut in (0, 1):
+                    for epi, cap, tag in ((False, True, ""), (True, True, "E"), (True, False, "F")):
+                        name = f"ANYSEQ_AF2R{tag}_{kind}_B{border}_{pub.upper()}_U{lut}"
+                        lines.append(f"#define {name} \\")
+                        for ln in gen_aff2(kind, border, pub, lut, False, epi, cap, r2=True):
+                            lines.append(f'    "{ln}\\n" \\')
+                        lines.append("")
     sclob = ", ".join(f'"s{n}"' for n in range(TA, TB + 2))
     clob = ", ".join(f'"v{n}"' for n in range(AT0, B_WB + 1))
     lines.append(f"#define ANYSEQ_AF2_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
+    clob = ", ".join(f'"v{n}"' for n in range(AT0, B_WBB + 1))
+    lines.append(f"#define ANYSEQ_AF2R_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, A + 1))
     lines.append(f"#define ANYSEQ_BLOCK_ASM_CLOBBERS {clob}, \"vcc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, SKB_ + 8))
