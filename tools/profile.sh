@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round profile collection on the GPU box (repo root): bench lines, kernel-trace
 # stats, PMC passes (HBM bytes and SQ counters), for the default workload
-# (configs[2]) and configs[1].  Every step has its own time limit; the first
+# (configs[2]), configs[1] and configs[4] at N=1.  Every step has its own time limit; the first
 # failure ends the script.
 # Usage: bash tools/profile.sh <tag>
 set -e
@@ -32,4 +32,9 @@ run sq_c1 120 rocprofv3 --pmc $SQ --output-format csv -d $OUT/pmc_sq_c1 -o run -
 B2="python3 bench.py --config 1 --kind local --gap-open -2 --steps 3 --warmup 1 --no-cpu-baseline"
 run sq_aff_local 120 rocprofv3 --pmc $SQ --output-format csv -d $OUT/pmc_sq_aff_local -o run -- $B2
 run trace_aff_local 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_aff_local -o run -- $B2
+# configs[4] at N=1 (throughput-bound: two rows per lane, round 5)
+B4="python3 bench.py --config 4 --steps 1 --warmup 1 --no-cpu-baseline"
+run bench_c4 300 $B4
+run trace_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_c4 -o run -- $B4
+run sq_c4 200 rocprofv3 --pmc $SQ --output-format csv -d $OUT/pmc_sq_c4 -o run -- $B4
 echo "[profile] done" >&2

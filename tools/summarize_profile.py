@@ -95,7 +95,7 @@ def main():
                      "counters + GRBM_GUI_ACTIVE; traffic = (2*FETCH_SIZE + WRITE_SIZE) KiB per launch (gfx950 "
                      "read correction); clock = GRBM_GUI_ACTIVE / 8 XCDs / average kernel time",
            "benches": {}, "kernels": {}}
-    for name, suffix in (("bench", ""), ("bench_c1", "_c1"), ("bench_aff_local", "_aff_local")):
+    for name, suffix in (("bench", ""), ("bench_c1", "_c1"), ("bench_aff_local", "_aff_local"), ("bench_c4", "_c4")):
         p = f"{src}/{name}.json"
         if not os.path.exists(p):
             continue
