@@ -97,7 +97,8 @@ _lib.anyseq_last_fill_timing.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes
 _lib.anyseq_last_fill_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int),
                                         ctypes.POINTER(_c_i64)]
 _lib.anyseq_last_shard_plan.restype = _c_int
-_lib.anyseq_last_fill_two_row_launches.restype = _c_int
+_lib.anyseq_last_fill_multi_row_launches.restype = _c_int
+_lib.anyseq_last_fill_multi_row_launches.argtypes = [ctypes.POINTER(_c_int)]
 _lib.anyseq_main_random_pair.argtypes = [_c_i64, _c_i64, _vp, ctypes.POINTER(_c_i64), _vp,
                                          ctypes.POINTER(_c_i64)]
 
@@ -290,9 +291,12 @@ def last_fill_stats():
     return ms.value, n.value, c.value
 
 
-def last_fill_two_row_launches() -> int:
-    """Affine fill launches since the previous call that ran two rows per lane; resets it."""
-    return int(_lib.anyseq_last_fill_two_row_launches())
+def last_fill_multi_row_launches():
+    """(affine fill launches since the previous call that ran two or three rows per lane,
+    the most rows per lane among them); resets both."""
+    r = _c_int(1)
+    n = int(_lib.anyseq_last_fill_multi_row_launches(ctypes.byref(r)))
+    return n, r.value
 
 
 def last_shard_plan() -> int:

@@ -88,7 +88,8 @@ constexpr int CPU_BLOCK_WIDTH = 1024;              // iteration_cpu.impala:1 (hb
 thread_local std::string g_last_error;
 thread_local double g_fill_ms = 0.0;
 thread_local int g_fill_launches = 0;
-thread_local int g_fill_r2 = 0;   // affine launches with two rows per lane (anyseq_last_fill_two_row_launches)
+thread_local int g_fill_r2 = 0;     // affine launches with >= 2 rows per lane (anyseq_last_fill_multi_row_launches)
+thread_local int g_fill_rmax = 1;   // the most rows per lane among them
 thread_local int g_shard_blocked_levels = 0;   // anyseq_last_shard_plan
 thread_local int64_t g_fill_cells = 0;
 
@@ -376,32 +377,34 @@ int aff_waves_for(int64_t chain_steps, int64_t wave_steps, int grid) {
     return t7 < 0.9 * t4 ? 7 : 4;
 }
 
-// Affine fill, rows per lane of one launch (round 5): two rows per lane
-// share the step's lane shifts, so a wave covers 128 rows per step at 1.5x the one-row step
-// time at two waves per SIMD (124.9 against 83.3 cycles per wave, tools/micro/mix_micro.hip
-// R2FULL / FULL, profiles/r05aa_mix_micro_r2.txt): 1.33x the throughput, but the band
-// chain steps at 1.5x for a hop over 128 rows (chain2 = w + 0.64 h).  Taken by NW 7
-// launches (throughput-bound) when the model gains >= 10 %; an explicit
-// affine_rows_per_lane wins (2 needs NW 4 or 7).
-int aff_rows_for(int NW, int64_t chain, int64_t chain2, int64_t work, int grid) {
-    if (g_tuning.arows == 1) return 1;
-    if (g_tuning.arows == 2) return NW == 4 || NW == 7 ? 2 : 1;
+// Affine fill, rows per lane of one launch (round 5): R rows per lane share
+// the step's lane shifts, so a wave covers 64 R rows per step at s_R times the one-row step
+// time at two waves per SIMD: s_2 = 1.5 (124.9 against 83.3 cycles per wave, tools/micro/
+// mix_micro.hip R2FULL / FULL, profiles/r05aa_mix_micro_r2.txt), s_3 = 2.13 (the projection
+// says 2.01, R3FULL 167.6; the product measures 1.054x over two rows at configs[4], 1.063x at
+// configs[3], gpurun_out/r05af / r05ag).  The throughput gains, but the band chain steps at
+// s_R for a hop over 64 R rows (chain_R = w + 1.28 h / R).  NW 7 launches take the R with the
+// least model time when it gains >= 10 % over one row; an explicit affine_rows_per_lane wins
+// (2 and 3 need NW 4 or 7).
+int aff_rows_for(int NW, const int64_t (&chain)[3], int64_t work, int grid) {
+    if (g_tuning.arows >= 1 && g_tuning.arows <= 3) return g_tuning.arows == 1 || NW == 4 || NW == 7 ? g_tuning.arows : 1;
     if (NW != 7) return 1;
-    const double g = (double)std::max(grid, 1);
-    const double t1 = std::max((double)chain, (double)work / (7.0 * g));
-    const double t2 = 1.5 * std::max((double)chain2, (double)work / (14.0 * g));
-    return t2 < 0.9 * t1 ? 2 : 1;
+    const double g = (double)std::max(grid, 1), s[3] = {1.0, 1.5, 2.13};
+    double t[3];
+    for (int r = 0; r < 3; ++r) t[r] = s[r] * std::max((double)chain[r], (double)work / (7.0 * (r + 1) * g));
+    const int best = t[2] < t[1] ? 3 : 2;
+    return t[best - 1] < 0.9 * t[0] ? best : 1;
 }
 
 namespace {
-void aff_launch_model(const std::vector<DPProblem>& probs, int64_t& chain, int64_t& work, int64_t* chain2 = nullptr) {
-    chain = 0;
+// chain[r]: the longest band chain with r+1 rows per lane, w + 1.28 h / (r+1) steps; work:
+// one-row wave steps of the launch
+void aff_launch_model(const std::vector<DPProblem>& probs, int64_t (&chain)[3], int64_t& work) {
+    chain[0] = chain[1] = chain[2] = 0;
     work = 0;
-    if (chain2) *chain2 = 0;
     for (const DPProblem& P : probs) {
         if (P.h <= 0 || P.w <= 0) continue;
-        chain = std::max(chain, (int64_t)P.w + (int64_t)P.h * 128 / 100);
-        if (chain2) *chain2 = std::max(*chain2, (int64_t)P.w + (int64_t)P.h * 64 / 100);
+        for (int r = 0; r < 3; ++r) chain[r] = std::max(chain[r], (int64_t)P.w + (int64_t)P.h * 128 / (100 * (r + 1)));
         work += (int64_t)((P.h + 63) / 64) * ((int64_t)P.w + 64);
     }
 }
@@ -455,11 +458,11 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     int NW = waves_per_group();
     int R = aff ? 1 : rows_per_lane();
     if (aff) {
-        int64_t chain, work, chain2;
-        aff_launch_model(probs, chain, work, &chain2);
+        int64_t chain[3], work;
+        aff_launch_model(probs, chain, work);
         const int g0 = grid_req > 0 ? grid_req : (g_tuning.grida > 0 ? g_tuning.grida : E.num_cus);
-        NW = aff_waves_for(chain, work, g0);
-        R = aff_rows_for(NW, chain, chain2, work, g0);   // (affine bands: 64 R rows)
+        NW = aff_waves_for(chain[0], work, g0);
+        R = aff_rows_for(NW, chain, work, g0);   // (affine bands: 64 R rows)
     }
     const int vpc = aff ? 2 : 1;
     // Persistent grid: at most `grid` groups are in flight, and a group finishes only after
@@ -735,7 +738,10 @@ void fill_collect(FillCtx& C) {
     g_fill_ms += ms;
     g_fill_launches += 1;
     g_fill_cells += C.cells;
-    if (C.aff && C.R == 2) g_fill_r2 += 1;
+    if (C.aff && C.R >= 2) {
+        g_fill_r2 += 1;
+        g_fill_rmax = std::max(g_fill_rmax, C.R);
+    }
     const uint32_t err = C.err_host ? *(volatile uint32_t*)C.err_host : 0u;
     if (C.rows_checked && !err) {
         uint32_t c[8];
@@ -2332,9 +2338,11 @@ void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells) {
     g_fill_cells = 0;
 }
 
-int anyseq_last_fill_two_row_launches(void) {
+int anyseq_last_fill_multi_row_launches(int* max_rows) {
     const int v = g_fill_r2;
+    if (max_rows) *max_rows = g_fill_rmax;
     g_fill_r2 = 0;
+    g_fill_rmax = 1;
     return v;
 }
 

@@ -1544,7 +1544,8 @@ struct Aff2Args {
     uint64_t gp;
     uint64_t sg;   // GS: the problem's subject-code rows (skb: the lane's byte offset at block 0)
     int q, wm, wx, ll, lh, zlp;
-    int qb, llb, lhb, zlpb;   // two rows per lane: row B's query code, LUT and clamp bound
+    int qb, llb, lhb, zlpb;   // rows per lane > 1: row 1's query code, LUT and clamp bound
+    int qx, llx, lhx, zlpx;   // three rows per lane: row 2's
 };
 #ifdef ANYSEQ_STAMPS
 #define AF2_NAME(NAME) NAME##_TS
@@ -1659,32 +1660,50 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
 #undef AF2E_ASM
 #undef AF2F_ASM
 
-// Two rows per lane (gen_aff2 r2): row A's state in e / hg / bx and the loop-carried cell
-// ga (row B's diagonal), row B's in g / fdn (the lane-shifted cell, as one row's) and
-// eb / hgb / bxb.  No diagnostic-stamp variants.
-#define AF2R_OUTS                                                                                              \
-    [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e), [hg] "+v"(hg), \
-        [best] "+v"(bx), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf), [sc] "+s"(sc), [pf] "+s"(pf), [st] "=&s"(st), \
-        [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3), [x4] "=&s"(x4), [ga] "+v"(ga),            \
-        [eb] "+v"(eb), [hgb] "+v"(hgb), [bestb] "+v"(bxb)
-#define AF2R_INS                                                                                               \
+// Two or three rows per lane (gen_aff2 nrows): the upper rows' state in gu / eu / hgu / bxu
+// (row 0: %[ga] / %[e] / %[hg] / %[best], row 1 of three: %[gb] / %[eb] / %[hgb] / %[bestb]),
+// the bottom row's in g / fdn (the lane-shifted cell, as one row's) and e / hg / bx (%[eb]..
+// of two rows, %[ex].. of three).  No diagnostic-stamp variants.
+#define AF2N_OUTS                                                                                              \
+    [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(eu[0]),           \
+        [hg] "+v"(hgu[0]), [best] "+v"(bxu[0]), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf), [sc] "+s"(sc),          \
+        [pf] "+s"(pf), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3),            \
+        [x4] "=&s"(x4), [ga] "+v"(gu[0])
+#define AF2N_INS                                                                                               \
     [be] "s"(be), [q] "v"(a.q), [wm] "v"(a.wm), [wx] "v"(a.wx), [ll] "v"(a.ll), [lh] "v"(a.lh), [go] "v"(go),     \
         [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr), [acn] "v"(a.acn),          \
         [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl), [skb] "v"(a.skb), [lo] "v"(a.lo),  \
         [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp), [thr] "s"(thr),         \
         [sg] "s"(sg), [qb] "v"(a.qb), [llb] "v"(a.llb), [lhb] "v"(a.lhb), [zlpb] "v"(a.zlpb)
-#define AF2R_ASM(NAME) asm volatile(NAME : AF2R_OUTS : AF2R_INS : ANYSEQ_AF2R_ASM_CLOBBERS, "memory")
+// two rows: row 1 is the bottom row
+#define AF2R_OUTS AF2N_OUTS, [eb] "+v"(e), [hgb] "+v"(hg), [bestb] "+v"(bx)
+#define AF2R_ASM(NAME) asm volatile(NAME : AF2R_OUTS : AF2N_INS : ANYSEQ_AF2R_ASM_CLOBBERS, "memory")
 #define AF2RE_ASM(NAME)                                                                                   \
-    asm volatile(NAME : AF2R_OUTS, [cnt] "+v"(cnt), [gc] "+v"(gc), [ec] "+v"(ec), [gcb] "+v"(gcb),        \
-                 [ecb] "+v"(ecb), [fc] "+v"(fc) : AF2R_INS, [nch] "s"(nch) : ANYSEQ_AF2R_ASM_CLOBBERS, "memory")
+    asm volatile(NAME : AF2R_OUTS, [cnt] "+v"(cap[0]), [gc] "+v"(cap[1]), [ec] "+v"(cap[2]),               \
+                 [gcb] "+v"(cap[3]), [ecb] "+v"(cap[4]), [fc] "+v"(cap[5]) : AF2N_INS, [nch] "s"(nch)      \
+                 : ANYSEQ_AF2R_ASM_CLOBBERS, "memory")
 #define AF2RF_ASM(NAME)                                                                                   \
-    asm volatile(NAME : AF2R_OUTS : AF2R_INS, [nch] "s"(nch), [neg] "s"(negp) : ANYSEQ_AF2R_ASM_CLOBBERS, "memory")
-// EPI as aff2_loop_asm; cap = {cnt, ga, ea, g, e, fdn} (EPI 1)
-template <bool L, bool BORDER, int PUB, bool LUT, int EPI = 0>
-__device__ __forceinline__ uint32_t aff2r_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
+    asm volatile(NAME : AF2R_OUTS : AF2N_INS, [nch] "s"(nch), [neg] "s"(negp) : ANYSEQ_AF2R_ASM_CLOBBERS, "memory")
+// three rows: row 1 upper (gu[1] ..), row 2 the bottom row
+#define AF2R3_OUTS                                                                                        \
+    AF2N_OUTS, [gb] "+v"(gu[NU - 1]), [eb] "+v"(eu[NU - 1]), [hgb] "+v"(hgu[NU - 1]), [bestb] "+v"(bxu[NU - 1]), \
+        [ex] "+v"(e), [hgx] "+v"(hg), [bestx] "+v"(bx)
+#define AF2R3_INS AF2N_INS, [qx] "v"(a.qx), [llx] "v"(a.llx), [lhx] "v"(a.lhx), [zlpx] "v"(a.zlpx)
+#define AF2R3_ASM(NAME) asm volatile(NAME : AF2R3_OUTS : AF2R3_INS : ANYSEQ_AF2R3_ASM_CLOBBERS, "memory")
+#define AF2R3E_ASM(NAME)                                                                                  \
+    asm volatile(NAME : AF2R3_OUTS, [cnt] "+v"(cap[0]), [gc] "+v"(cap[1]), [ec] "+v"(cap[2]),              \
+                 [gcb] "+v"(cap[3]), [ecb] "+v"(cap[4]), [gcx] "+v"(cap[5]), [ecx] "+v"(cap[6]),           \
+                 [fc] "+v"(cap[7]) : AF2R3_INS, [nch] "s"(nch) : ANYSEQ_AF2R3_ASM_CLOBBERS, "memory")
+#define AF2R3F_ASM(NAME)                                                                                  \
+    asm volatile(NAME : AF2R3_OUTS : AF2R3_INS, [nch] "s"(nch), [neg] "s"(negp) : ANYSEQ_AF2R3_ASM_CLOBBERS, "memory")
+// EPI as aff2_loop_asm; cap = {cnt, then (g, e) of rows 0 .. RR-1, then the bottom row's F-down} (EPI 1)
+template <int RR, bool L, bool BORDER, int PUB, bool LUT, int EPI = 0, int NU = RR - 1>
+__device__ __forceinline__ uint32_t aff2n_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                    const Aff2Args& a, int go, int nge, int& g, int& fdn, int& dg,
-                                                   int2& tf, int& e, int& hg, int& bx, int& ga, int& eb, int& hgb,
-                                                   int& bxb, uint32_t nch = 0, int* cap = nullptr) {
+                                                   int2& tf, int& e, int& hg, int& bx, int (&gu)[NU], int (&eu)[NU],
+                                                   int (&hgu)[NU], int (&bxu)[NU], uint32_t nch = 0,
+                                                   int* cap = nullptr) {
+    static_assert(RR == 2 || RR == 3, "two or three rows per lane");
     uint32_t st, x0, x1, x2, x3, x4, pf = 0;
     const uint64_t hm = 0xffff000000000000ull;   // lanes 48..63 (publishing)
 #define RFL(x) __builtin_amdgcn_readfirstlane(x)
@@ -1706,49 +1725,54 @@ __device__ __forceinline__ uint32_t aff2r_loop_asm(uint32_t& b, uint32_t be, uin
     if constexpr (!BORDER && PUB == 0) A(ANYSEQ_##V##_##K##_B0_NONE_U##U);           \
     if constexpr (!BORDER && PUB == 1) A(ANYSEQ_##V##_##K##_B0_LDS_U##U);            \
     if constexpr (!BORDER && PUB == 2) A(ANYSEQ_##V##_##K##_B0_GLOB_U##U);
+#define AF2R_KINDS(A, V)                                  \
+    if constexpr (L && LUT) { AF2R_SEL(A, V, L, 1) }      \
+    if constexpr (L && !LUT) { AF2R_SEL(A, V, L, 0) }     \
+    if constexpr (!L && LUT) { AF2R_SEL(A, V, G, 1) }     \
+    if constexpr (!L && !LUT) { AF2R_SEL(A, V, G, 0) }
     if constexpr (EPI == 1) {
         nch = __builtin_amdgcn_readfirstlane(nch);
-        int cnt = cap[0], gc = cap[1], ec = cap[2], gcb = cap[3], ecb = cap[4], fc = cap[5];
-        if constexpr (L && LUT) { AF2R_SEL(AF2RE_ASM, AF2RE, L, 1) }
-        if constexpr (L && !LUT) { AF2R_SEL(AF2RE_ASM, AF2RE, L, 0) }
-        if constexpr (!L && LUT) { AF2R_SEL(AF2RE_ASM, AF2RE, G, 1) }
-        if constexpr (!L && !LUT) { AF2R_SEL(AF2RE_ASM, AF2RE, G, 0) }
-        cap[0] = cnt, cap[1] = gc, cap[2] = ec, cap[3] = gcb, cap[4] = ecb, cap[5] = fc;
+        if constexpr (RR == 2) { AF2R_KINDS(AF2RE_ASM, AF2RE) } else { AF2R_KINDS(AF2R3E_ASM, AF2R3E) }
     } else if constexpr (EPI == 2) {
         nch = __builtin_amdgcn_readfirstlane(nch);
         const uint32_t negp = __builtin_amdgcn_readfirstlane(a.neg);
-        if constexpr (L && LUT) { AF2R_SEL(AF2RF_ASM, AF2RF, L, 1) }
-        if constexpr (L && !LUT) { AF2R_SEL(AF2RF_ASM, AF2RF, L, 0) }
-        if constexpr (!L && LUT) { AF2R_SEL(AF2RF_ASM, AF2RF, G, 1) }
-        if constexpr (!L && !LUT) { AF2R_SEL(AF2RF_ASM, AF2RF, G, 0) }
+        (void)cap;
+        if constexpr (RR == 2) { AF2R_KINDS(AF2RF_ASM, AF2RF) } else { AF2R_KINDS(AF2R3F_ASM, AF2R3F) }
     } else {
-        (void)nch;
-        if constexpr (L && LUT) { AF2R_SEL(AF2R_ASM, AF2R, L, 1) }
-        if constexpr (L && !LUT) { AF2R_SEL(AF2R_ASM, AF2R, L, 0) }
-        if constexpr (!L && LUT) { AF2R_SEL(AF2R_ASM, AF2R, G, 1) }
-        if constexpr (!L && !LUT) { AF2R_SEL(AF2R_ASM, AF2R, G, 0) }
+        (void)nch, (void)cap;
+        if constexpr (RR == 2) { AF2R_KINDS(AF2R_ASM, AF2R) } else { AF2R_KINDS(AF2R3_ASM, AF2R3) }
     }
+#undef AF2R_KINDS
 #undef AF2R_SEL
     tf = make_int2(tfg, tff);
     return st;
 }
+#undef AF2N_OUTS
+#undef AF2N_INS
 #undef AF2R_OUTS
-#undef AF2R_INS
 #undef AF2R_ASM
 #undef AF2RE_ASM
 #undef AF2RF_ASM
+#undef AF2R3_OUTS
+#undef AF2R3_INS
+#undef AF2R3_ASM
+#undef AF2R3E_ASM
+#undef AF2R3F_ASM
 
-// Two rows per lane: aff_block for rows A = 2l and B = 2l+1 of a 128-row band at the
-// same column (the lane's column c0 + u at step u).  Row A takes its up / F-in from row B
-// of the lane above (DPP, lane 0: the top row); row B its diagonal from A's previous
-// cell (ga), its up and F-in from A's new cell.  og / of: row B's (the band's bottom
-// row at lane 63).  zca / zba: row A's clamp bound / true Z of the first step (row B's
-// are one -ge further).  PARTIAL: a dead row passes the row above through.
-template <bool MASK, bool PARTIAL, bool VIRT>
-__device__ __forceinline__ void aff_block2(int c0, int w, int2 tf, const int2 (&rv)[32], const uint32_t (&sw)[8],
-                                           int qa, int qb, bool deada, bool deadb, int zca, int zba, int& ga,
-                                           int& ea, int& hga, int& dg, int& g, int& e, int& hg, int& fdn, int& besta,
-                                           int& best, int (&og)[32], int (&of)[32], const AffK k) {
+// RR rows per lane (2 or 3): aff_block for rows RR l .. RR l + RR-1 of a 64 RR-row band
+// at the same column (the lane's column c0 + u at step u).  Row 0 takes its up / F-in
+// from the bottom row of the lane above (DPP, lane 0: the top row); row i > 0 its diagonal
+// from row i-1's previous cell, its up and F-in from row i-1's new cell.  The upper rows'
+// state in gu / eu / hgu / bestu, the bottom row's in g / e / hg / fdn / best; og / of:
+// the bottom row's (the band's bottom row at lane 63).  zc0 / zb0: row 0's clamp bound /
+// true Z of the first step (row i's are i (-ge) further).  PARTIAL: a dead row passes the
+// row above through.
+template <int RR, bool MASK, bool PARTIAL, bool VIRT, int NU = RR - 1>
+__device__ __forceinline__ void aff_blockn(int c0, int w, int2 tf, const int2 (&rv)[32], const uint32_t (&sw)[8],
+                                           const int (&qu)[NU], int q, const bool (&deadu)[NU], bool dead, int zc0,
+                                           int zb0, int (&gu)[NU], int (&eu)[NU], int (&hgu)[NU], int& dg, int& g,
+                                           int& e, int& hg, int& fdn, int (&bestu)[NU], int& best, int (&og)[32],
+                                           int (&of)[32], const AffK k) {
 #pragma unroll
     for (int u = 0; u < 32; ++u) {
         const int2 top = u == 0 ? tf : rv[u - 1];
@@ -1756,51 +1780,57 @@ __device__ __forceinline__ void aff_block2(int c0, int w, int2 tf, const int2 (&
         const int fin = wave_shr1(top.y, fdn);
         const bool vcol = VIRT && c0 + u < 0;
         const int sb = (int)((sw[u >> 2] >> (8 * (u & 3))) & 0xffu);
-        const int wa = vcol ? kAffNeg : (qa == sb ? k.wm : k.wx);
-        const int wb = vcol ? kAffNeg : (qb == sb ? k.wm : k.wx);
-        const int zu = zca + u * k.nge, zt = zba + u * k.nge;
-        // row A
-        const int ena = max(ea, hga);
-        int va = max(max(max(dg + wa, ena), fin), zu);
-        const int hna = va + k.go;
-        int fna = max(fin, hna);
-        if (PARTIAL && deada) {
-            va = upg;
-            fna = fin;
-        }
-        // row B
-        const int enb = max(e, hg);
-        int vb = max(max(max(ga + wb, enb), fna), zu + k.nge);
-        const int hnb = vb + k.go;
-        int fnb = max(fna, hnb);
-        if (PARTIAL && deadb) {
-            vb = va;
-            fnb = fna;
-        }
+        const int zu = zc0 + u * k.nge, zt = zb0 + u * k.nge;
         const bool act = MASK ? (VIRT ? (c0 + u < w) : ((unsigned)(c0 + u) < (unsigned)w)) : true;
-        ea = act ? ena : ea;
-        ga = act ? va : ga;
-        hga = act ? hna : hga;
-        besta = act ? max(besta, va - zt) : besta;
+        int dgi = dg, upi = upg, fi = fin;   // row i's diagonal, up, F-in
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+            const int wi = vcol ? kAffNeg : (qu[i] == sb ? k.wm : k.wx);
+            const int en = max(eu[i], hgu[i]);
+            int v = max(max(max(dgi + wi, en), fi), zu + i * k.nge);
+            const int hn = v + k.go;
+            int fn = max(fi, hn);
+            if (PARTIAL && deadu[i]) {
+                v = upi;
+                fn = fi;
+            }
+            dgi = gu[i];   // the next row's diagonal: this row's previous cell
+            eu[i] = act ? en : eu[i];
+            gu[i] = act ? v : gu[i];
+            hgu[i] = act ? hn : hgu[i];
+            bestu[i] = act ? max(bestu[i], v - (zt + i * k.nge)) : bestu[i];
+            upi = v;
+            fi = fn;
+        }
+        const int wb = vcol ? kAffNeg : (q == sb ? k.wm : k.wx);
+        const int enb = max(e, hg);
+        int vb = max(max(max(dgi + wb, enb), fi), zu + NU * k.nge);
+        const int hnb = vb + k.go;
+        int fnb = max(fi, hnb);
+        if (PARTIAL && dead) {
+            vb = upi;
+            fnb = fi;
+        }
         e = act ? enb : e;
         g = act ? vb : g;
         hg = act ? hnb : hg;
         fdn = act ? fnb : fdn;
-        best = act ? max(best, vb - (zt + k.nge)) : best;
+        best = act ? max(best, vb - (zt + NU * k.nge)) : best;
         dg = upg;
         og[u] = g;
         of[u] = fdn;
     }
 }
 
-// RR: rows per lane.  RR 2 (round 5): lane l holds rows 2l (A) and 2l+1 (B) of a 128-row
-// band at the same column (aff_block2, gen_aff2 r2); `row`, g / e / hg / fdn are the lane's
-// bottom row (B), ga / ea / hga / besta row A, dg row A's diagonal.  The hand-off rows,
-// rings and steps are the one-row band's.
+// RR: rows per lane.  RR 2 / 3 (round 5): lane l holds rows RR l .. RR l + RR-1 of a
+// 64 RR-row band at the same column (aff_blockn, gen_aff2 nrows); `row`, g / e / hg / fdn
+// are the lane's bottom row, gu / eu / hgu / bestu its upper rows (row rowt + i), dg row
+// 0's diagonal.  The hand-off rows, rings and steps are the one-row band's.
 template <bool PARTIAL, int RR>
 __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int lane, const AffIO& io, uint32_t* err, const AffK k,
                              unsigned long long* dbg) {
-    static_assert(RR == 1 || RR == 2, "one or two rows per lane");
+    static_assert(RR >= 1 && RR <= 3, "one to three rows per lane");
+    constexpr int NU = RR > 1 ? RR - 1 : 1;   // upper rows (unused for RR 1)
     constexpr int CH = 32;
     constexpr int IRM = kSlots * CH - 1;
     constexpr int LAG = 2;   // lane 63 finishes column c at step c + 64: chunk j is complete after block j + 2
@@ -1846,36 +1876,46 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                       (!clamp || (k.codes && ff_loses)) && !(k.flags & 1);
     const int rb = band * 64 * RR;
     const int row = rb + RR * lane + (RR - 1);   // the lane's bottom row
-    const int rowt = row - (RR - 1);             // its top row (RR 2: row A)
+    const int rowt = row - (RR - 1);             // its top row
     const bool dead = row >= h;
     const bool lastrow = row == h - 1;
-    const bool deada = rowt >= h, lasta = RR == 2 && rowt == h - 1;
     int q = dead ? 0x100 : (int)gmem(P.q)[P.q_off + P.q_step * row];
-    int qa = RR == 1 ? q : deada ? 0x100 : (int)gmem(P.q)[P.q_off + P.q_step * rowt];
+    int qu[NU];
+    bool deadu[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        deadu[i] = RR == 1 || rowt + i >= h;
+        qu[i] = deadu[i] ? 0x100 : (int)gmem(P.q)[P.q_off + P.q_step * (rowt + i)];
+    }
     // settle the query loads here: a vmcnt wait inside the step loop would also wait
     // for lane 63's HBM row stores
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(q), "+v"(qa)::"memory");
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(q), "+v"(qu[0]), "+v"(qu[NU - 1])::"memory");
     if (kAffGS && !P.scode) {   // (a planned level whose code rows did not fit: its bound check fails too)
         if (lane == 0) atomicOr(err, ERR_BAD_DESC);
         return;
     }
     int g, e = kAffNeg, hg, fdn = kAffNeg, dg;
-    int ga = kAffNeg, ea = kAffNeg, hga = kAffNeg;   // RR 2: row A
+    int gu[NU], eu[NU], hgu[NU];   // RR > 1: the upper rows
+#pragma unroll
+    for (int i = 0; i < NU; ++i) gu[i] = eu[i] = hgu[i] = kAffNeg;
     int2 tf;
     if (shard_left) {
         int32_t lh1 = 0, lh0 = 0, le1 = 0;
-        if constexpr (RR == 2) {
-            // row A first (waits for the band's 128 rows), then row B (already landed)
-            int32_t a1 = 0, a0 = 0, ae = 0;
-            if (!poll_left(P, rowt, a1, a0, err, 128)) return;
-            if (!poll_left_e(P, rowt, ae, err)) return;
-            ga = a1 + (rowt + 1) * nge;
-            ea = ae + (rowt + 1) * nge;
-            hga = ga + go;
-            lh0 = a0;
+        if constexpr (RR > 1) {
+            // row 0 first (waits for the band's 64 RR rows), then the rows below (landed)
+#pragma unroll
+            for (int i = 0; i < NU; ++i) {
+                int32_t a1 = 0, a0 = 0, ae = 0;
+                if (!poll_left(P, rowt + i, a1, a0, err, 64 * RR - i)) return;
+                if (!poll_left_e(P, rowt + i, ae, err)) return;
+                gu[i] = a1 + (rowt + i + 1) * nge;
+                eu[i] = ae + (rowt + i + 1) * nge;
+                hgu[i] = gu[i] + go;
+                if (i == 0) lh0 = a0;
+            }
         }
         int32_t l0 = 0;
-        if (!poll_left(P, row, lh1, l0, err, RR == 2 ? 127 : 64)) return;
+        if (!poll_left(P, row, lh1, l0, err, 64 * RR - (RR - 1))) return;
         if constexpr (RR == 1) lh0 = l0;
         if (!poll_left_e(P, row, le1, err)) return;
         // H space -> G space at column -1: G = H + (r + 1) (-ge); row -1 is the top
@@ -1899,12 +1939,17 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
         hg = g + go;   // the next column's E candidate: G[r][-1] + go
         dg = B.left(rowt - 1, nge);
         tf = make_int2(B.left(rb - 1, nge), kAffNeg);
-        if constexpr (RR == 2) {
-            ga = B.left(rowt, nge);   // (also row B's diagonal at column 0)
-            hga = ga + go;
+        if constexpr (RR > 1) {
+#pragma unroll
+            for (int i = 0; i < NU; ++i) {
+                gu[i] = B.left(rowt + i, nge);   // (also row i+1's diagonal at column 0)
+                hgu[i] = gu[i] + go;
+            }
         }
     }
-    int best = kAffNeg, besta = kAffNeg;
+    int best = kAffNeg, bestu[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) bestu[i] = kAffNeg;
     const int nchunks = (w + CH - 1) / CH;
     const int nblocks = nchunks + LAG;
     const int fe = w >= CH - 1 ? (w - (CH - 1)) / CH + 1 : 0;   // full blocks: 32b + 30 < w
@@ -1975,8 +2020,12 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
             lho = (int)lh;
             zo = clamp ? (r + 3) * nge : 2 * kAffNeg;
         };
-        row_consts(qa, rowt, la.q, la.ll, la.lh, la.zlp);
+        row_consts(RR == 1 ? q : qu[0], rowt, la.q, la.ll, la.lh, la.zlp);
         if constexpr (RR == 2) row_consts(q, row, la.qb, la.llb, la.lhb, la.zlpb);
+        if constexpr (RR == 3) {
+            row_consts(qu[NU - 1], rowt + 1, la.qb, la.llb, la.lhb, la.zlpb);
+            row_consts(q, row, la.qx, la.llx, la.lhx, la.zlpx);
+        }
     }
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
@@ -1995,7 +2044,9 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                 // state into the loop's space: the lane's cell of step t0-1 is column t0-2-lane
                 const int cs = t0 - 2 - lane;
                 int bx = kAffNeg;
-                int bxa = kAffNeg;
+                int bxu[NU];
+#pragma unroll
+                for (int i = 0; i < NU; ++i) bxu[i] = kAffNeg;
                 if (xs) {
                     g = to_x(g, cs);
                     hg = to_x(hg, cs);
@@ -2003,10 +2054,13 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                     fdn = to_x(fdn, cs);
                     dg = to_x(dg, cs);
                     tf = make_int2(to_x(tf.x, t0 - 1), to_x(tf.y, t0 - 1));
-                    if constexpr (RR == 2) {
-                        ga = to_x(ga, cs);
-                        hga = to_x(hga, cs);
-                        ea = to_x(ea, cs);
+                    if constexpr (RR > 1) {
+#pragma unroll
+                        for (int i = 0; i < NU; ++i) {
+                            gu[i] = to_x(gu[i], cs);
+                            hgu[i] = to_x(hgu[i], cs);
+                            eu[i] = to_x(eu[i], cs);
+                        }
                     }
                 }
                 uint32_t bb = (uint32_t)b;
@@ -2040,9 +2094,10 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                 const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || !best_safe || (k.flags & 32);
                 if (epi && !need_cap) {
 #define AF2_CALL(LV, BD, PB, LU)                                                                                  \
-    if constexpr (RR == 2)                                                                                        \
-        st = aff2r_loop_asm<LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, \
-                                               g, fdn, dg, tf, ea, hga, bxa, ga, e, hg, bx, (uint32_t)(2 * nchunks)); \
+    if constexpr (RR > 1)                                                                                         \
+        st = aff2n_loop_asm<RR, LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, \
+                                                   nge, g, fdn, dg, tf, e, hg, bx, gu, eu, hgu, bxu,             \
+                                                   (uint32_t)(2 * nchunks));                                     \
     else                                                                                                          \
         st = aff2_loop_asm<LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
                                               fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), \
@@ -2059,14 +2114,15 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                     }
                     if (xs) {
                         best = max(best, bx - (row + 2) * nge);
-                        besta = max(besta, bxa - (rowt + 2) * nge);
+#pragma unroll
+                        for (int i = 0; i < NU; ++i) bestu[i] = max(bestu[i], bxu[i] - (rowt + i + 2) * nge);
                     }
                     break;   // band done (g / e / fdn: nobody reads them)
                 }
 #define AF2_CALL(LV, BD, PB, LU)                                                                               \
-    if constexpr (RR == 2)                                                                                     \
-        st = aff2r_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
-                                            fdn, dg, tf, ea, hga, bxa, ga, e, hg, bx);                          \
+    if constexpr (RR > 1)                                                                                      \
+        st = aff2n_loop_asm<RR, LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, \
+                                                g, fdn, dg, tf, e, hg, bx, gu, eu, hgu, bxu);                    \
     else                                                                                                       \
         st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, fdn, \
                                            dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, nullptr, dbp)
@@ -2083,13 +2139,23 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                     ev_store(7, te_v);                               // main loop end
                     ev_store(8, __builtin_amdgcn_s_memrealtime());   // epilogue entry
 #endif
-                    // steps until column w-1; the state kept there (RR 2: cap = {cnt, ga, ea, g, e, fdn})
-                    int cap[6] = {w + lane - (int)bb * CH, RR == 2 ? ga : g, RR == 2 ? ea : e, RR == 2 ? g : fdn, e, fdn};
+                    // steps until column w-1, then the state kept there: (g, e) of rows 0 .. RR-1, the
+                    // bottom row's F-down
+                    int cap[2 * RR + 2];
+                    cap[0] = w + lane - (int)bb * CH;
+#pragma unroll
+                    for (int i = 0; i < RR - 1; ++i) {
+                        cap[1 + 2 * i] = gu[i];
+                        cap[2 + 2 * i] = eu[i];
+                    }
+                    cap[2 * RR - 1] = g;
+                    cap[2 * RR] = e;
+                    cap[2 * RR + 1] = fdn;
 #define AF2_CALL(LV, BD, PB, LU)                                                                               \
-    if constexpr (RR == 2)                                                                                     \
-        st = aff2r_loop_asm<LV, BD, PB, LU, 1>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, \
-                                               g, fdn, dg, tf, ea, hga, bxa, ga, e, hg, bx, (uint32_t)(2 * nchunks), \
-                                               cap);                                                           \
+    if constexpr (RR > 1)                                                                                      \
+        st = aff2n_loop_asm<RR, LV, BD, PB, LU, 1>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, \
+                                                   nge, g, fdn, dg, tf, e, hg, bx, gu, eu, hgu, bxu,             \
+                                                   (uint32_t)(2 * nchunks), cap);                                \
     else                                                                                                       \
         st = aff2_loop_asm<LV, BD, PB, LU, 1>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
                                               fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), \
@@ -2107,26 +2173,24 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
 #ifdef ANYSEQ_STAMPS
                     ev_store(9, te_v);   // epilogue end
 #endif
-                    if constexpr (RR == 2) {
-                        ga = cap[1];
-                        ea = cap[2];
-                        g = cap[3];
-                        e = cap[4];
-                        fdn = cap[5];
-                    } else {
-                        g = cap[1];
-                        e = cap[2];
-                        fdn = cap[3];
+#pragma unroll
+                    for (int i = 0; i < RR - 1; ++i) {
+                        gu[i] = cap[1 + 2 * i];
+                        eu[i] = cap[2 + 2 * i];
                     }
+                    g = cap[2 * RR - 1];
+                    e = cap[2 * RR];
+                    fdn = cap[2 * RR + 1];
                     if (xs) {
                         g = to_g(g, w - 1);
                         e = to_g(e, w - 1);
                         fdn = to_g(fdn, w - 1);
                         best = max(best, bx - (row + 2) * nge);
-                        if constexpr (RR == 2) {
-                            ga = to_g(ga, w - 1);
-                            ea = to_g(ea, w - 1);
-                            besta = max(besta, bxa - (rowt + 2) * nge);
+#pragma unroll
+                        for (int i = 0; i < RR - 1; ++i) {
+                            gu[i] = to_g(gu[i], w - 1);
+                            eu[i] = to_g(eu[i], w - 1);
+                            bestu[i] = max(bestu[i], bxu[i] - (rowt + i + 2) * nge);
                         }
                     }
                     break;   // band done
@@ -2146,11 +2210,12 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                     dg = to_g(dg, ce);
                     tf = make_int2(to_g(tf.x, t1 - 1), to_g(tf.y, t1 - 1));
                     best = max(best, bx - (row + 2) * nge);
-                    if constexpr (RR == 2) {
-                        ga = to_g(ga, ce);
-                        hga = to_g(hga, ce);
-                        ea = to_g(ea, ce);
-                        besta = max(besta, bxa - (rowt + 2) * nge);
+#pragma unroll
+                    for (int i = 0; i < RR - 1; ++i) {
+                        gu[i] = to_g(gu[i], ce);
+                        hgu[i] = to_g(hgu[i], ce);
+                        eu[i] = to_g(eu[i], ce);
+                        bestu[i] = max(bestu[i], bxu[i] - (rowt + i + 2) * nge);
                     }
                 }
                 b = (int)bb - 1;   // ++b of the for
@@ -2207,24 +2272,24 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
         if (b == 0) t_b0 = __builtin_amdgcn_s_memrealtime();   // block 0's inputs are ready
 #endif
         const int c0 = t0 - 1 - lane;
-        // Z of the lane's first step: (r + c + 2)(-ge), r + c = rb + t0 - 1 (+ lane for row A of RR 2)
-        const int zb = (rb + t0 + 1 + (RR == 2 ? lane : 0)) * nge;
+        // Z of the lane's first step (row 0): (r + c + 2)(-ge), r + c = rb + t0 - 1 + (RR-1) lane
+        const int zb = (rb + t0 + 1 + (RR - 1) * lane) * nge;
         const int zc = zb + zoff;
         const bool full = (virt || t0 >= 64) && b < fe;
-        if constexpr (RR == 2) {
+        if constexpr (RR > 1) {
             if (full) {
                 if (virt)
-                    aff_block2<false, PARTIAL, true>(c0, w, tf, rv, sw, qa, q, deada, dead, zc, zb, ga, ea, hga, dg, g,
-                                                     e, hg, fdn, besta, best, og, of, k);
+                    aff_blockn<RR, false, PARTIAL, true>(c0, w, tf, rv, sw, qu, q, deadu, dead, zc, zb, gu, eu, hgu, dg,
+                                                         g, e, hg, fdn, bestu, best, og, of, k);
                 else
-                    aff_block2<false, PARTIAL, false>(c0, w, tf, rv, sw, qa, q, deada, dead, zc, zb, ga, ea, hga, dg,
-                                                      g, e, hg, fdn, besta, best, og, of, k);
+                    aff_blockn<RR, false, PARTIAL, false>(c0, w, tf, rv, sw, qu, q, deadu, dead, zc, zb, gu, eu, hgu,
+                                                          dg, g, e, hg, fdn, bestu, best, og, of, k);
             } else if (virt) {
-                aff_block2<true, PARTIAL, true>(c0, w, tf, rv, sw, qa, q, deada, dead, zc, zb, ga, ea, hga, dg, g, e,
-                                                hg, fdn, besta, best, og, of, k);
+                aff_blockn<RR, true, PARTIAL, true>(c0, w, tf, rv, sw, qu, q, deadu, dead, zc, zb, gu, eu, hgu, dg, g,
+                                                    e, hg, fdn, bestu, best, og, of, k);
             } else {
-                aff_block2<true, PARTIAL, false>(c0, w, tf, rv, sw, qa, q, deada, dead, zc, zb, ga, ea, hga, dg, g, e,
-                                                 hg, fdn, besta, best, og, of, k);
+                aff_blockn<RR, true, PARTIAL, false>(c0, w, tf, rv, sw, qu, q, deadu, dead, zc, zb, gu, eu, hgu, dg, g,
+                                                     e, hg, fdn, bestu, best, og, of, k);
             }
         } else if (full) {
             if (virt)
@@ -2304,12 +2369,15 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
         // shard: F-down of the last row at the last column (the combine pairs it across shards)
         if (lastrow && P.out_f_last) *gmem(P.out_f_last) = aff_to_h(fdn, row, w - 1, nge);
     }
-    if constexpr (RR == 2) {
-        if (!deada) {
-            if (P.out_col) gmem(P.out_col)[rowt] = aff_to_h(ga, rowt, w - 1, nge);
-            if (P.out_col_e) gmem(P.out_col_e)[rowt] = aff_to_h(ea, rowt, w - 1, nge);
-            // (row A last: row B is dead and passed A's F-down through, in fdn)
-            if (lasta && P.out_f_last) *gmem(P.out_f_last) = aff_to_h(fdn, rowt, w - 1, nge);
+    if constexpr (RR > 1) {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+            const int r = rowt + i;
+            if (deadu[i]) continue;
+            if (P.out_col) gmem(P.out_col)[r] = aff_to_h(gu[i], r, w - 1, nge);
+            if (P.out_col_e) gmem(P.out_col_e)[r] = aff_to_h(eu[i], r, w - 1, nge);
+            // (an upper row last: the rows below are dead and passed its F-down through, in fdn)
+            if (r == h - 1 && P.out_f_last) *gmem(P.out_f_last) = aff_to_h(fdn, r, w - 1, nge);
         }
     }
     if (P.progress && !publish_progress(P, band, lane, err, RR)) return;
@@ -2318,10 +2386,14 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
         // last-column mode the lane's cell in the last column
         if (bestmode == 3) best = aff_to_h(g, row, w - 1, nge);
         if (dead || (bestmode == 2 && !lastrow)) best = kAffNeg;
-        if constexpr (RR == 2) {
-            if (bestmode == 3) besta = aff_to_h(ga, rowt, w - 1, nge);
-            if (deada || (bestmode == 2 && !lasta)) besta = kAffNeg;
-            best = max(best, besta);
+        if constexpr (RR > 1) {
+#pragma unroll
+            for (int i = 0; i < NU; ++i) {
+                int bu = bestu[i];
+                if (bestmode == 3) bu = aff_to_h(gu[i], rowt + i, w - 1, nge);
+                if (deadu[i] || (bestmode == 2 && rowt + i != h - 1)) bu = kAffNeg;
+                best = max(best, bu);
+            }
         }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) best = max(best, __shfl_xor(best, off));
@@ -4467,10 +4539,12 @@ hipError_t anyseq_launch_fill_affine(int NW, const anyseq::DPProblem* probs, con
                                      hipStream_t st) {
     using namespace anyseq;
     // (the asm steady state holds ~150 fixed VGPRs: at most 2 waves per SIMD, NW <= 7)
-    // fp->arows 2: two rows per lane (NW 4 or 7; the descriptors' nbands count 128-row bands)
-    if (fp->arows == 2) {
-        if (NW == 7) return launch_fill_aff_n<7, 2>(probs, groups, ngroups, dq, err, *fp, grid, st);
-        if (NW == 4) return launch_fill_aff_n<4, 2>(probs, groups, ngroups, dq, err, *fp, grid, st);
+    // fp->arows 2 / 3: rows per lane (NW 4 or 7; the descriptors' nbands count 64 arows-row bands)
+    if (fp->arows == 2 || fp->arows == 3) {
+        if (NW == 7 && fp->arows == 2) return launch_fill_aff_n<7, 2>(probs, groups, ngroups, dq, err, *fp, grid, st);
+        if (NW == 4 && fp->arows == 2) return launch_fill_aff_n<4, 2>(probs, groups, ngroups, dq, err, *fp, grid, st);
+        if (NW == 7) return launch_fill_aff_n<7, 3>(probs, groups, ngroups, dq, err, *fp, grid, st);
+        if (NW == 4) return launch_fill_aff_n<4, 3>(probs, groups, ngroups, dq, err, *fp, grid, st);
         return hipErrorInvalidValue;
     }
     if (NW == 3) return launch_fill_aff_n<3, 1>(probs, groups, ngroups, dq, err, *fp, grid, st);

@@ -323,7 +323,7 @@ def construct_bench(args):
     if separate:
         A.set_option("fill_events", 0)
     A.last_fill_stats()
-    A.last_fill_two_row_launches()
+    A.last_fill_multi_row_launches()
     ts = []
     score = None
     for _ in range(args.steps):
@@ -333,7 +333,7 @@ def construct_bench(args):
         ts.append(time.perf_counter() - t)
     elapsed = sum(ts)
     fill_ms, launches, fill_cells = A.last_fill_stats()
-    two_row = A.last_fill_two_row_launches()
+    multi_row, rows_max = A.last_fill_multi_row_launches()
     kernel_timing = {"steps": args.steps, "how": "HIP events around every fill launch, inside the timed region"}
     if separate:
         A.set_option("fill_events", 1)
@@ -360,7 +360,8 @@ def construct_bench(args):
                    "scoring": "match +2, mismatch -1, gap open -2, extend -1", "parallelism": "single GPU",
                    "score": int(score), "fill_cells_per_step": fill_cells // max(args.steps, 1),
                    "fill_launches_per_step": launches // max(args.steps, 1),
-                   "fill_two_row_launches_per_step": two_row // max(args.steps, 1),
+                   "fill_multi_row_launches_per_step": multi_row // max(args.steps, 1),
+                   "fill_rows_per_lane_max": rows_max,
                    "fill_ms_per_step": round(fill_ms / max(args.steps, 1), 4),
                    "fill_gcups": round(fill_cells / (fill_ms * 1e-3) / 1e9, 2) if fill_ms > 0 else None},
         "roofline": roofline("fill_affine_kernel", fill_cells / max(launches, 1), kernel_ms,
@@ -509,7 +510,7 @@ def score_bench(args, world, rank, local_rank):
     if separate:
         A.set_option("fill_events", 0)
     A.last_fill_timing()
-    A.last_fill_two_row_launches()
+    A.last_fill_multi_row_launches()
     ts = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -522,7 +523,7 @@ def score_bench(args, world, rank, local_rank):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     fill_ms, launches = A.last_fill_timing()
-    two_row = A.last_fill_two_row_launches()
+    multi_row, rows_max = A.last_fill_multi_row_launches()
     kernel_timing = {"steps": args.steps, "how": "HIP events around every fill launch, inside the timed region"}
     if separate:
         A.set_option("fill_events", 1)
@@ -572,7 +573,8 @@ def score_bench(args, world, rank, local_rank):
                        "baseline_config": args.config, "query_len": n, "subject_len": m,
                        "parallelism": parallelism, "score": int(score),
                        "fill_launches_per_step": launches // max(args.steps, 1),
-                       "fill_two_row_launches_per_step": two_row // max(args.steps, 1),
+                       "fill_multi_row_launches_per_step": multi_row // max(args.steps, 1),
+                   "fill_rows_per_lane_max": rows_max,
                        "transport": ("RCCL send/recv (host-polled chunk trigger), unmeasured on hardware "
                                      "(no multi-GPU run before this one)" if world > 1 else None)},
             "roofline": roofline("fill_affine_kernel" if aff else "fill_kernel", cells_per_launch, kernel_ms,

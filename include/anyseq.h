@@ -121,10 +121,11 @@ void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells);
  * level dealt round-robin, e.g. when GPU_MAX_HW_QUEUES is too small for the concurrent
  * shard streams).  Resets it. */
 int anyseq_last_shard_plan(void);
-/* Affine fill launches of the calling thread since the previous call that ran two rows
- * per lane (128-row bands; chosen per launch or by the option
- * "affine_rows_per_lane").  Resets the count. */
-int anyseq_last_fill_two_row_launches(void);
+/* Affine fill launches of the calling thread since the previous call that ran two or three
+ * rows per lane (64 R-row bands; chosen per launch or by the option
+ * "affine_rows_per_lane"); *max_rows (may be null) gets the most rows per lane among the
+ * launches (1 when none).  Resets both. */
+int anyseq_last_fill_multi_row_launches(int* max_rows);
 
 /* ---- column-block sharded score (build-defined) ----
  * Subject columns are split into contiguous blocks, block g = [g*m/N, (g+1)*m/N);

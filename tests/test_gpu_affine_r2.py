@@ -1,11 +1,12 @@
-"""GPU parity of the affine fill with TWO ROWS PER LANE (round 5): lane l
-holds rows 2l and 2l+1 of a 128-row band (aff_block2 / gen_aff2 r2), chosen per launch for
-throughput-bound launches (aff_rows_for) and forced here with `affine_rows_per_lane` 2 at
-four and seven compute waves.  Scores, host-built construct levels (the device-planned
-levels keep one row per lane) and the column-block shards (left border of both rows,
-progress in 64-row units) against the affine oracle, bit-exact: odd row counts (a dead
-row B beside a live row A), band-size edges (127 / 128 / 129 rows), both weight paths
-(LUT: <= 8 symbols; compare: bytes), every border mode, the asm band ends and starts."""
+"""GPU parity of the affine fill with TWO AND THREE ROWS PER LANE (round 5):
+lane l holds rows R l .. R l + R-1 of a 64 R-row band (aff_blockn / gen_aff2 nrows), chosen
+per launch for throughput-bound launches (aff_rows_for) and forced here with
+`affine_rows_per_lane` 2 and 3 at four and seven compute waves.  Scores, host-built construct
+levels (the device-planned levels keep one row per lane) and the column-block shards (the
+left border of every row, the band's rows waited for, progress in 64-row units) against the
+affine oracle, bit-exact: row counts that leave dead rows beside live ones in a lane,
+band-size edges (127-129, 191-193 rows), both weight paths (LUT: <= 8 symbols; compare:
+bytes), every border mode, the asm band ends and starts."""
 import random
 
 import pytest
@@ -28,15 +29,16 @@ def ora(oracle, kind, q, s, sc):
     return oracle.affine_score(kind, q, s, *sc)
 
 
-@pytest.fixture(params=[7, 4])
+@pytest.fixture(params=[(2, 7), (2, 4), (3, 7), (3, 4)], ids=lambda p: f"rows{p[0]}-nw{p[1]}")
 def r2(anyseq, request):
-    anyseq.set_option("affine_rows_per_lane", 2)
-    anyseq.set_option("affine_waves_per_group", request.param)
-    anyseq.last_fill_two_row_launches()
+    anyseq.set_option("affine_rows_per_lane", request.param[0])
+    anyseq.set_option("affine_waves_per_group", request.param[1])
+    anyseq.last_fill_multi_row_launches()
     try:
         yield request.param
-        # the two-row kernel actually ran (host-built fills of this test)
-        assert anyseq.last_fill_two_row_launches() > 0
+        # the multi-row kernel actually ran (host-built fills of this test), with the rows asked for
+        n, rmax = anyseq.last_fill_multi_row_launches()
+        assert n > 0 and rmax == request.param[0], (n, rmax)
     finally:
         anyseq.set_option("affine_rows_per_lane", 0)
         anyseq.set_option("affine_waves_per_group", 0)
@@ -55,7 +57,8 @@ def test_r2_small_random(anyseq, oracle, r2):
 def test_r2_edge_shapes(anyseq, oracle, r2):
     rng = random.Random(42)
     sc = (2, -1, -2, -1)
-    for n in [1, 2, 3, 63, 64, 65, 127, 128, 129, 255, 256, 257, 895, 896, 897, 1025, 2049]:
+    for n in [1, 2, 3, 4, 63, 64, 65, 127, 128, 129, 191, 192, 193, 255, 256, 257, 383, 384, 385, 895, 896, 897,
+              1025, 2049]:
         for m in (1, 31, 32, 33, 64, 65, 1000):
             q, s = rnd(rng, n), rnd(rng, m)
             for kind in KINDS:

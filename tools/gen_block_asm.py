@@ -344,19 +344,29 @@ TSLIGHT = int(os.environ.get("ANYSEQ_GEN_TSLIGHT", "0"))
 AT0, AO0 = 64, 128          # TOP (G,F) pairs v64..v127, cell (G,F) pairs v128..v135 (step u: u % 4)
 
 
-BR0 = 162          # R2: the second row's cell (G, F) pairs v162..v169 (step u: u % 4)
-B_AAB, B_WBB = 170, 171   # R2: the second row's diagonal + weight, LUT weight bytes
+BR0 = 162          # rows per lane > 1: row k >= 1's cell (G, F) pairs from v(BR0 + 10 (k-1)), then
+                   # its diagonal + weight and LUT weight bytes (row 1: v162..v169, v170, v171)
+ROWTAG = {0: "", 1: "b", 2: "x"}   # named operands of row k: %[e], %[eb], %[ex] ... (%[ec]: a capture)
+B_WBB = BR0 + 9    # (two rows: the last clobbered register)
+
+
+def OGk_(k, u):
+    return OG_(u) if k == 0 else v(BR0 + 10 * (k - 1) + 2 * (u % 4))
+
+
+def OFk_(k, u):
+    return OF_(u) if k == 0 else v(BR0 + 10 * (k - 1) + 2 * (u % 4) + 1)
 
 
 def OGB_(u):
-    return v(BR0 + 2 * (u % 4))
+    return OGk_(1, u)
 
 
 def OFB_(u):
-    return v(BR0 + 2 * (u % 4) + 1)
+    return OFk_(1, u)
 
 
-def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, r2=False):
+def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1):
     """Affine steady-state loop, round 3: full blocks b .. be-1.
     kind G: G space (X_G = X + (r+c+2)|ge|), no clamp, no best (amode 0).
     kind L: X space (X = H + (r+2)|ge|, a per-ROW shift): the local clamp H >= 0 is
@@ -396,11 +406,15 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, r2=False):
     weights (%[qb] or %[llb] / %[lhb]), clamp bound (%[zlpb]) and best (%[bestb]).  The
     shift register, the publish and the block-end state carry B's cells (the band's bottom
     row), so the hand-off is the one-row kernel's.  The DPP moves are shared by two cells:
-    16.4 instead of 2 x 11.2 instructions per step (tools/micro/gen_mix_micro.py)."""
+    16.4 instead of 2 x 11.2 instructions per step (tools/micro/gen_mix_micro.py).
+    nrows 3: rows 3l, 3l+1, 3l+2 the same way (row k from row k-1; %[gb] carries row B's
+    cell of the previous step into row C's diagonal; %[ex] / %[hgx] / ... row C's)."""
     L = kind == "L"
+    r2 = nrows > 1
+    last = nrows - 1
     assert not r2 or (REORDER and LEAN and SLIM and GS and not ts)
-    OGP, OFP = (OGB_, OFB_) if r2 else (OG_, OF_)   # the published / lane-shifted cells
-    PUBREG = BR0 + 6 if r2 else AO0 + 6
+    OGP, OFP = (lambda u: OGk_(last, u)), (lambda u: OFk_(last, u))   # the published / lane-shifted cells
+    PUBREG = int(OGk_(last, 3)[1:])
     trailing = pub != "lds"
     out = []
     e = out.append
@@ -720,32 +734,34 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, r2=False):
                 if sr and not r2:
                     e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_max_i32_e32 {OF_(u)}, {tf}, %[hg]")
-                if r2:
-                    # row B: diagonal A's previous cell, up / F-in A's new cell, no lane shift
-                    dgb = OG_(u - 1)   # (step 0: OG_(31), loaded from %[ga] at entry)
+                for rk in range(1, nrows):
+                    # row k: diagonal row k-1's previous cell, up / F-in its new cell, no lane shift
+                    t = ROWTAG[rk]
+                    dgk = OGk_(rk - 1, u - 1)   # (step 0: the rotation's last slot, loaded from %[ga] / %[gb])
+                    aak, wbk = BR0 + 10 * (rk - 1) + 8, BR0 + 10 * (rk - 1) + 9
                     if L:
-                        e("v_max3_i32 %[eb], %[eb], %[hgb], %[zlpb]")
+                        e(f"v_max3_i32 %[e{t}], %[e{t}], %[hg{t}], %[zlp{t}]")
                     else:
-                        e("v_max_i32_e32 %[eb], %[eb], %[hgb]")
+                        e(f"v_max_i32_e32 %[e{t}], %[e{t}], %[hg{t}]")
                     if lut:
                         if u % 4 == 0:
-                            e(f"v_perm_b32 v{B_WBB}, %[lhb], %[llb], {sw}")
-                        e(f"v_add_u32_sdwa v{B_AAB}, {dgb}, sext(v{B_WBB}) dst_sel:DWORD dst_unused:UNUSED_PAD "
+                            e(f"v_perm_b32 v{wbk}, %[lh{t}], %[ll{t}], {sw}")
+                        e(f"v_add_u32_sdwa v{aak}, {dgk}, sext(v{wbk}) dst_sel:DWORD dst_unused:UNUSED_PAD "
                           f"src0_sel:DWORD src1_sel:BYTE_{u % 4}")
                     else:
-                        e(f"v_cmp_eq_u32_sdwa vcc, %[qb], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+                        e(f"v_cmp_eq_u32_sdwa vcc, %[q{t}], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
                         e(f"v_cndmask_b32_e32 v{B_AW}, %[wx], %[wm], vcc")
-                        e(f"v_add_u32_e32 v{B_AAB}, {dgb}, v{B_AW}")
+                        e(f"v_add_u32_e32 v{aak}, {dgk}, v{B_AW}")
                     if L:
-                        e("v_add_u32_e32 %[eb], %[ge], %[eb]")
-                    e(f"v_max3_i32 {OGB_(u)}, v{B_AAB}, %[eb], {OF_(u)}")
-                    e(f"v_add_u32_e32 %[hgb], %[go], {OGB_(u)}")
+                        e(f"v_add_u32_e32 %[e{t}], %[ge], %[e{t}]")
+                    e(f"v_max3_i32 {OGk_(rk, u)}, v{aak}, %[e{t}], {OFk_(rk - 1, u)}")
+                    e(f"v_add_u32_e32 %[hg{t}], %[go], {OGk_(rk, u)}")
                     if L and u % 2 == 1 and not (epi and cap):
-                        e(f"v_max3_i32 %[bestb], %[bestb], {OGB_(u - 1)}, {OGB_(u)}")
-                    e(f"v_max_i32_e32 {OFB_(u)}, {OF_(u)}, %[hgb]")
-                    if sr:
-                        e(f"v_mov_b32_dpp {OGB_(u - 1)}, {OGB_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-                        e(f"v_mov_b32_dpp {OFB_(u - 1)}, {OFB_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+                        e(f"v_max3_i32 %[best{t}], %[best{t}], {OGk_(rk, u - 1)}, {OGk_(rk, u)}")
+                    e(f"v_max_i32_e32 {OFk_(rk, u)}, {OFk_(rk - 1, u)}, %[hg{t}]")
+                    if sr and rk == last:
+                        e(f"v_mov_b32_dpp {OGk_(rk, u - 1)}, {OGk_(rk, u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+                        e(f"v_mov_b32_dpp {OFk_(rk, u - 1)}, {OFk_(rk, u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
             else:
                 if L:
                     e("v_max3_i32 %[e], %[e], %[hg], %[zlp]")
@@ -763,18 +779,21 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, r2=False):
                     e(f"v_max_i32_e32 v{B_AT}, %[best], {OG_(u)}")
                     e("v_cmp_le_i32_e32 vcc, 0, %[cnt]")
                     e(f"v_cndmask_b32_e32 %[best], %[best], v{B_AT}, vcc")
-                    if r2:
-                        e(f"v_max_i32_e32 v{B_AT}, %[bestb], {OGB_(u)}")
-                        e(f"v_cndmask_b32_e32 %[bestb], %[bestb], v{B_AT}, vcc")
+                    for rk in range(1, nrows):
+                        t = ROWTAG[rk]
+                        e(f"v_max_i32_e32 v{B_AT}, %[best{t}], {OGk_(rk, u)}")
+                        e(f"v_cndmask_b32_e32 %[best{t}], %[best{t}], v{B_AT}, vcc")
                 # the lane whose cell is column w-1 at this step keeps its state
                 e("v_cmp_eq_u32_e32 vcc, 0, %[cnt]")
                 e(f"v_cndmask_b32_e32 %[gc], %[gc], {OG_(u)}, vcc")
                 e("v_cndmask_b32_e32 %[ec], %[ec], %[e], vcc")
                 if r2:
-                    # (row A's F-down is row B's F-in: only B's is kept)
-                    e(f"v_cndmask_b32_e32 %[gcb], %[gcb], {OGB_(u)}, vcc")
-                    e("v_cndmask_b32_e32 %[ecb], %[ecb], %[eb], vcc")
-                    e(f"v_cndmask_b32_e32 %[fc], %[fc], {OFB_(u)}, vcc")
+                    # (a row's F-down is the next row's F-in: only the last row's is kept)
+                    for rk in range(1, nrows):
+                        t = ROWTAG[rk]
+                        e(f"v_cndmask_b32_e32 %[gc{t}], %[gc{t}], {OGk_(rk, u)}, vcc")
+                        e(f"v_cndmask_b32_e32 %[ec{t}], %[ec{t}], %[e{t}], vcc")
+                    e(f"v_cndmask_b32_e32 %[fc], %[fc], {OFk_(last, u)}, vcc")
                 else:
                     e(f"v_cndmask_b32_e32 %[fc], %[fc], {OF_(u)}, vcc")
                 e("v_add_u32_e32 %[cnt], -1, %[cnt]")
@@ -836,8 +855,9 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, r2=False):
     lean_regs = [("%[dg]", TG_(30)), ("%[tfg]", TG_(31)), ("%[tff]", TF_(31))]
     if pub == "none":
         lean_regs += [("%[cur]", OGP(31)), ("%[fd]", OFP(31))]
-    if r2:
-        lean_regs += [("%[ga]", OG_(31))]   # row A's cell of the previous step: B's diagonal
+    for k in range(nrows - 1):
+        # row k's cell of the previous step: row k+1's diagonal at step 0
+        lean_regs += [("%[g" + "ab"[k] + "]", OGk_(k, 31))]
     if LEAN:
         for named, reg in lean_regs:
             e(f"v_mov_b32_e32 {reg}, {named}")
@@ -930,22 +950,25 @@ def main():
                             for ln in gen_aff2(kind, border, pub, lut, ts, epi, cap):
                                 lines.append(f'    "{ln}\\n" \\')
                             lines.append("")
-    # two rows per lane (no diagnostic-stamp variants)
-    for kind in ("G", "L"):
-        for border in (0, 1):
-            for pub in ("none", "lds", "glob"):
-                for lut in (0, 1):
-                    for epi, cap, tag in ((False, True, ""), (True, True, "E"), (True, False, "F")):
-                        name = f"ANYSEQ_AF2R{tag}_{kind}_B{border}_{pub.upper()}_U{lut}"
-                        lines.append(f"#define {name} \\")
-                        for ln in gen_aff2(kind, border, pub, lut, False, epi, cap, r2=True):
-                            lines.append(f'    "{ln}\\n" \\')
-                        lines.append("")
+    # two and three rows per lane (no diagnostic-stamp variants)
+    for nrows, pre in ((2, "AF2R"), (3, "AF2R3")):
+        for kind in ("G", "L"):
+            for border in (0, 1):
+                for pub in ("none", "lds", "glob"):
+                    for lut in (0, 1):
+                        for epi, cap, tag in ((False, True, ""), (True, True, "E"), (True, False, "F")):
+                            name = f"ANYSEQ_{pre}{tag}_{kind}_B{border}_{pub.upper()}_U{lut}"
+                            lines.append(f"#define {name} \\")
+                            for ln in gen_aff2(kind, border, pub, lut, False, epi, cap, nrows=nrows):
+                                lines.append(f'    "{ln}\\n" \\')
+                            lines.append("")
     sclob = ", ".join(f'"s{n}"' for n in range(TA, TB + 2))
     clob = ", ".join(f'"v{n}"' for n in range(AT0, B_WB + 1))
     lines.append(f"#define ANYSEQ_AF2_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
     clob = ", ".join(f'"v{n}"' for n in range(AT0, B_WBB + 1))
     lines.append(f"#define ANYSEQ_AF2R_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
+    clob = ", ".join(f'"v{n}"' for n in range(AT0, BR0 + 20))
+    lines.append(f"#define ANYSEQ_AF2R3_ASM_CLOBBERS {clob}, {sclob}, \"vcc\", \"scc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, A + 1))
     lines.append(f"#define ANYSEQ_BLOCK_ASM_CLOBBERS {clob}, \"vcc\"")
     clob = ", ".join(f'"v{n}"' for n in range(T0, SKB_ + 8))

@@ -115,36 +115,46 @@ SUBST = {
 }
 
 
-def r2_transform(body):
-    """Two rows per lane (round 5 projection, G space): after each step's cell A (row 2l)
-    the lane computes cell B (row 2l+1) from A without a lane shift -- B's own E chain,
-    its LUT (the other query code, the same subject byte), its diagonal from A's previous
-    step, F and H from A's new cell -- and the lane shifts, the shift register and the
-    publish carry B's cells (the band's bottom row).  A's rotation v128..v135 is mirrored
-    by B's v168..v175; v176 / v177 are B's diagonal sum and weight bytes."""
-    def bmap(r):
+def rn_transform(body, nrows=2):
+    """nrows rows per lane (round 5 projection, G space): after each step's cell A (row
+    nrows*l) the lane computes the cells below it (rows nrows*l+1 ..) from the cell above
+    without a lane shift -- each its own E chain, its LUT (another query code, the same
+    subject byte), its diagonal from the row above's previous cell, F and H from the row
+    above's new cell -- and the lane shifts, the shift register and the publish carry the
+    last row's cells (the band's bottom row).  A's rotation v128..v135 is mirrored by row
+    k's v(128 + 40 + 10 (k-1)) ..; the two registers after each rotation are its diagonal
+    sum and weight bytes.  Named operands of row k: eb/hgb/llb/lhb (k = 1), ec/hgc/llc/lhc."""
+    def base(k):
+        return 40 + 10 * (k - 1)
+
+    def kmap(r, k):
         n = int(r[1:])
-        return f"v{n + 40}" if 128 <= n <= 135 else r
-    out, prev_oga, perm_src, byte, cur_oga = [], "v134", None, 0, None
+        return f"v{n + base(k)}" if k and 128 <= n <= 135 else r
+
+    last = nrows - 1
+    tag = {1: "b", 2: "c", 3: "d"}
+    # each row's cell of the previous step (row k's diagonal: row k-1's; step 0: the last rotation slot)
+    out, prev = [], ["v134"] + [f"v{134 + base(k)}" for k in range(1, nrows - 1)]
+    perm_src, byte, cur_oga = None, 0, None
     for l in body:
         m = re.match(r"v_mov_b32_dpp (v\d+), (\S+) (wave_shr|wave_shl)(.*)", l)
         if m:
             dst, src = m.group(1), m.group(2)
             if m.group(3) == "wave_shl":
-                dst = bmap(dst)
-            src = bmap(src) if src.startswith("v") else src
+                dst = kmap(dst, last)
+            src = kmap(src, last) if src.startswith("v") else src
             out.append(f"v_mov_b32_dpp {dst}, {src} {m.group(3)}{m.group(4)}")
             continue
         m = re.match(r"ds_write_b64 (v\d+), v\[(\d+):(\d+)\](.*)", l)
         if m:
             a0, a1 = int(m.group(2)), int(m.group(3))
             if 128 <= a0 <= 135:
-                a0, a1 = a0 + 40, a1 + 40
+                a0, a1 = a0 + base(last), a1 + base(last)
             out.append(f"ds_write_b64 {m.group(1)}, v[{a0}:{a1}]{m.group(4)}")
             continue
         m = re.match(r"v_mov_b32_e32 (%\[(?:cur|fd)\]), (v\d+)$", l)
         if m:
-            out.append(f"v_mov_b32_e32 {m.group(1)}, {bmap(m.group(2))}")
+            out.append(f"v_mov_b32_e32 {m.group(1)}, {kmap(m.group(2), last)}")
             continue
         m = re.match(r"v_perm_b32 v160, %\[lh\], %\[ll\], (v\d+)", l)
         if m:
@@ -158,18 +168,28 @@ def r2_transform(body):
         out.append(l)
         m = re.match(r"v_max_i32_e32 (v\d+), (v\d+), %\[hg\]$", l)
         if m and cur_oga:
-            ofa = m.group(1)
-            out.append("v_max_i32_e32 %[eb], %[eb], %[hgb]")
-            if perm_src:
-                out.append(f"v_perm_b32 v177, %[lhb], %[llb], {perm_src}")
-                perm_src = None
-            out.append(f"v_add_u32_sdwa v176, {prev_oga}, sext(v177) dst_sel:DWORD dst_unused:UNUSED_PAD "
-                       f"src0_sel:DWORD src1_sel:BYTE_{byte}")
-            out.append(f"v_max3_i32 {bmap(cur_oga)}, v176, %[eb], {ofa}")
-            out.append(f"v_add_u32_e32 %[hgb], %[go], {bmap(cur_oga)}")
-            out.append(f"v_max_i32_e32 {bmap(ofa)}, {ofa}, %[hgb]")
-            prev_oga, cur_oga = cur_oga, None
+            above_g, above_f = cur_oga, m.group(1)
+            for k in range(1, nrows):
+                t, bk = tag[k], base(k)
+                og, of = kmap(cur_oga, k), kmap(m.group(1), k)
+                aa, wb = f"v{136 + bk}", f"v{137 + bk}"
+                out.append(f"v_max_i32_e32 %[e{t}], %[e{t}], %[hg{t}]")
+                if perm_src:
+                    out.append(f"v_perm_b32 {wb}, %[lh{t}], %[ll{t}], {perm_src}")
+                out.append(f"v_add_u32_sdwa {aa}, {prev[k - 1]}, sext({wb}) dst_sel:DWORD dst_unused:UNUSED_PAD "
+                           f"src0_sel:DWORD src1_sel:BYTE_{byte}")
+                out.append(f"v_max3_i32 {og}, {aa}, %[e{t}], {above_f}")
+                out.append(f"v_add_u32_e32 %[hg{t}], %[go], {og}")
+                out.append(f"v_max_i32_e32 {of}, {above_f}, %[hg{t}]")
+                prev[k - 1] = above_g
+                above_g, above_f = og, of
+            perm_src = None
+            cur_oga = None
     return out
+
+
+def r2_transform(body):
+    return rn_transform(body, 2)
 
 
 def main():
@@ -189,15 +209,17 @@ def main():
             for l in sel:
                 f.write(f'    "{l}\\n" \\\n')
             f.write('    ""\n')
-        r2 = r2_transform(body)
-        for sub, keep in (("R2FULL", SUBSETS["FULL"]), ("R2VALU", SUBSETS["VALU"])):
-            sel = [l for l in r2 if kind(l) in keep]
-            f.write(f"#define MIX_{sub}_N {len(sel)}\n")
-            f.write(f"#define MIX_{sub} \\\n")
-            for l in sel:
-                f.write(f'    "{l}\\n" \\\n')
-            f.write('    ""\n')
+        for nr in (2, 3):
+            rn = rn_transform(body, nr)
+            for sub, keep in ((f"R{nr}FULL", SUBSETS["FULL"]), (f"R{nr}VALU", SUBSETS["VALU"])):
+                sel = [l for l in rn if kind(l) in keep]
+                f.write(f"#define MIX_{sub}_N {len(sel)}\n")
+                f.write(f"#define MIX_{sub} \\\n")
+                for l in sel:
+                    f.write(f'    "{l}\\n" \\\n')
+                f.write('    ""\n')
         f.write("#define MIX_R2_CLOBBERS " + ", ".join(f'"v{n}"' for n in range(168, 178)) + "\n")
+        f.write("#define MIX_R3_CLOBBERS " + ", ".join(f'"v{n}"' for n in range(168, 188)) + "\n")
         valu = [l for l in body if kind(l) == "valu"]
         for sub, fn in SUBST.items():
             f.write(f"#define MIX_{sub}_N {len(valu)}\n")

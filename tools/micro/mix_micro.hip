@@ -38,8 +38,8 @@ __global__ __launch_bounds__(512) void mix(int nblocks, const uint8_t* codes, un
     __syncthreads();
     auto la = [](void* p) { return (uint32_t)(size_t)(__attribute__((address_space(3))) char*)p; };
     int g = lane, fdn = -5, dg = lane - 1, tfg = 0, tff = -5, e = -100, hg = -2, bx = 0;
-    int eb = -90, hgb = -3;   // (R2 variants: cell B's E chain)
-    const uint32_t llb = 0x00000300u, lhb = 0x00000003u;
+    int eb = -90, hgb = -3, ec = -80, hgc = -4;   // (R2 / R3 variants: cells B / C's E chains)
+    const uint32_t llb = 0x00000300u, lhb = 0x00000003u, llc = 0x00030000u, lhc = 0x00000300u;
     const int q = lane & 3, wm = 3, wx = 0, go = -2, zlp = lane + 3;
     uint32_t ll = 0x00030000u, lh = 0x03000000u;
     const uint32_t rb = RFL(la(sh.ring[wave])), nb = RFL(la(sh.next[wave]));
@@ -80,6 +80,19 @@ __global__ __launch_bounds__(512) void mix(int nblocks, const uint8_t* codes, un
                    [lid8] "v"(lid8), [bvb] "v"(bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp), [pm63] "v"(pm63),   \
                    [pdb] "v"(pdb), [sg] "s"(sg), [llb] "v"(llb), [lhb] "v"(lhb)                              \
                  : ANYSEQ_AF2_ASM_CLOBBERS, MIX_R2_CLOBBERS, "memory")
+#define MIXLOOP3(NAME)                                                                                           \
+    for (int it = 0; it < nblocks / 2; ++it)                                                                    \
+    asm volatile(NAME                                                                                          \
+                 : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
+                   [hg] "+v"(hg), [best] "+v"(bx), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf), [sc] "+s"(sc),     \
+                   [pf] "+s"(pf), [st] "+s"(st), [x0] "+s"(x0), [x1] "+s"(x1), [x2] "+s"(x2), [x3] "+s"(x3),     \
+                   [x4] "+s"(x4), [eb] "+v"(eb), [hgb] "+v"(hgb), [ec] "+v"(ec), [hgc] "+v"(hgc)               \
+                 : [be] "s"(be), [q] "v"(q), [wm] "v"(wm), [wx] "v"(wx), [ll] "v"(ll), [lh] "v"(lh), [go] "v"(go), \
+                   [ge] "s"(ge), [zlp] "v"(zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(apr), [acn] "v"(acn),     \
+                   [anp] "v"(anp), [anc] "v"(anc), [asf] "v"(asf), [atl] "v"(atl), [skb] "v"(skb), [lo] "v"(lo),  \
+                   [lid8] "v"(lid8), [bvb] "v"(bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp), [pm63] "v"(pm63),   \
+                   [pdb] "v"(pdb), [sg] "s"(sg), [llb] "v"(llb), [lhb] "v"(lhb), [llc] "v"(llc), [lhc] "v"(lhc) \
+                 : ANYSEQ_AF2_ASM_CLOBBERS, MIX_R3_CLOBBERS, "memory")
     if constexpr (V == 0) MIXLOOP(MIX_FULL);
     if constexpr (V == 1) MIXLOOP(MIX_VALU);
     if constexpr (V == 2) MIXLOOP(MIX_VALU_LDS);
@@ -93,17 +106,20 @@ __global__ __launch_bounds__(512) void mix(int nblocks, const uint8_t* codes, un
     if constexpr (V == 10) MIXLOOP(MIX_PLAIN64);
     if constexpr (V == 11) MIXLOOP2(MIX_R2FULL);
     if constexpr (V == 12) MIXLOOP2(MIX_R2VALU);
+    if constexpr (V == 13) MIXLOOP3(MIX_R3FULL);
+    if constexpr (V == 14) MIXLOOP3(MIX_R3VALU);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
-    sink[blockIdx.x * blockDim.x + threadIdx.x] = g + fdn + dg + e + hg + bx + tfg + tff + (int)st + eb + hgb;
+    sink[blockIdx.x * blockDim.x + threadIdx.x] = g + fdn + dg + e + hg + bx + tfg + tff + (int)st + eb + hgb + ec + hgc;
     if (lane == 0) out[blockIdx.x * kMaxW + wave] = c1 - c0;
 }
 
 static const char* kNames[] = {"FULL", "VALU", "VALU+LDS", "VALU+SALU", "VALU+WAIT", "VALU+GLOB",
-                               "NODPP", "NOSDWA", "NOMAX3", "PLAIN", "PLAIN64", "R2FULL", "R2VALU"};
+                               "NODPP", "NOSDWA", "NOMAX3", "PLAIN", "PLAIN64", "R2FULL", "R2VALU",
+                               "R3FULL", "R3VALU"};
 static const int kN[] = {MIX_FULL_N, MIX_VALU_N, MIX_VALU_LDS_N, MIX_VALU_SALU_N, MIX_VALU_WAIT_N, MIX_VALU_GLOB_N,
                          MIX_NODPP_N, MIX_NOSDWA_N, MIX_NOMAX3_N, MIX_PLAIN_N, MIX_PLAIN64_N, MIX_R2FULL_N,
-                         MIX_R2VALU_N};
+                         MIX_R2VALU_N, MIX_R3FULL_N, MIX_R3VALU_N};
 
 template <int V>
 double run(int waves, int wgs, const uint8_t* codes, int nblocks) {
@@ -155,6 +171,9 @@ int main() {
     // two rows per lane (128 cells per wave step: compare cycles per step / 2 with FULL)
     all<11>(codes, nblocks);
     all<12>(codes, nblocks);
+    // three rows per lane (192 cells per wave step)
+    all<13>(codes, nblocks);
+    all<14>(codes, nblocks);
     // the instruction fetch: one busy CU against all of them
     for (int wgs : {1, 8, 64, 128}) {
         all<1>(codes, nblocks, wgs);
