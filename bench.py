@@ -61,6 +61,11 @@ VALU_DESIGN_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
 # (profiles/r04z_pmc.json: 859.2 M per 65536^2 local score launch); G space = 9.25 +
 # the same 2.15 of block overhead.
 VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.4, "affine_local": 12.8}
+# Affine fill with R rows per lane (round 5): VALU per 64 cells.  R = 2
+# measured (SQ_INSTS_VALU / (cells / 64), configs[4], profiles/r05fin_pmc.json); R = 3 the
+# generated loop's count (tools/micro/gen_mix_micro.py R3VALU 19.92 per 192 cells) x the
+# same loop-to-kernel ratio as R = 2 (7.67 / 7.34); X space (local) scaled as R = 1's 12.8 / 11.4
+VALU_PER_64_ROWS = {2: 7.67, 3: 6.93}
 
 AFFINE = dict(match=2, mismatch=-1, gap_open=-2, gap_extend=-1)
 METRIC = "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; % of HBM roofline"
@@ -178,7 +183,8 @@ def cpu_baseline(what: str, work, cells: int, sample: str, runs: int):
     return out
 
 
-def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: str, traffic_tag: str):
+def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: str, traffic_tag: str,
+             rows: int = 1):
     """The dominant kernel's roofline.  The PMC counters (profiles/) show
     the fill bound by VALU issue along the band chain, not by HBM: it keeps every cell in
     VGPRs and moves ~1 % of the 4 B/cell model's bytes.  So `bound` is "valu" (GCUPS
@@ -189,6 +195,8 @@ def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: s
     traffic, traffic_src = load_traffic(traffic_tag)
     gcups = cells_per_launch / (kernel_ms * 1e-3) / 1e9 if ok else None
     v = VALU_PER_STEP[valu_key]
+    if rows > 1 and valu_key.startswith("affine"):
+        v = VALU_PER_64_ROWS[rows] * (VALU_PER_STEP[valu_key] / VALU_PER_STEP["affine"])
     peak = VALU_PEAK_WAVE_INSTR * 64 / v / 1e9
     design = VALU_DESIGN_WAVE_INSTR * 64 / v / 1e9
     return {
@@ -197,7 +205,7 @@ def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: s
         "traffic": traffic, "traffic_source": traffic_src,
         "binding": "band-chain latency: per-step VALU issue x (steps + bands x per-hop lag), DESIGN.md 3.5",
         "kernel": kernel, "kernel_ms": round(kernel_ms, 4), "cells_per_launch": int(cells_per_launch),
-        "valu_model": {"instr_per_wave_step": v, "cells_per_wave_step": 64,
+        "valu_model": {"instr_per_wave_step": round(v, 3), "cells_per_wave_step": 64, "rows_per_lane": rows,
                        "chip_peak": "256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU",
                        "design_ceiling_gcups": round(design, 1),
                        "design_frac": round(gcups / design, 4) if gcups else None,
@@ -366,7 +374,7 @@ def construct_bench(args):
                    "fill_gcups": round(fill_cells / (fill_ms * 1e-3) / 1e9, 2) if fill_ms > 0 else None},
         "roofline": roofline("fill_affine_kernel", fill_cells / max(launches, 1), kernel_ms,
                              "affine_local" if kind == "local" else "affine",
-                             f"fill_affine_kernel<{kind}> construct {n}x{m}"),
+                             f"fill_affine_kernel<{kind}> construct {n}x{m}", rows_max),
     }
     out["roofline"]["kernel_timing"] = kernel_timing
     if args.config == 2:
@@ -578,7 +586,7 @@ def score_bench(args, world, rank, local_rank):
                        "transport": ("RCCL send/recv (host-polled chunk trigger), unmeasured on hardware "
                                      "(no multi-GPU run before this one)" if world > 1 else None)},
             "roofline": roofline("fill_affine_kernel" if aff else "fill_kernel", cells_per_launch, kernel_ms,
-                                 valu_key, tag),
+                                 valu_key, tag, rows_max if aff else 1),
         }
         out["roofline"]["kernel_timing"] = kernel_timing
         if world == 1 and not args.no_cpu_baseline:
