@@ -61,11 +61,10 @@ VALU_DESIGN_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
 # (profiles/r04z_pmc.json: 859.2 M per 65536^2 local score launch); G space = 9.25 +
 # the same 2.15 of block overhead.
 VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.4, "affine_local": 12.8}
-# Affine fill with R rows per lane (round 5): VALU per 64 cells.  R = 2
-# measured (SQ_INSTS_VALU / (cells / 64), configs[4], profiles/r05fin_pmc.json); R = 3 the
-# generated loop's count (tools/micro/gen_mix_micro.py R3VALU 19.92 per 192 cells) x the
-# same loop-to-kernel ratio as R = 2 (7.67 / 7.34); X space (local) scaled as R = 1's 12.8 / 11.4
-VALU_PER_64_ROWS = {2: 7.67, 3: 6.93}
+# Affine fill with R rows per lane (round 5): VALU per 64 cells, measured
+# (SQ_INSTS_VALU / (cells / 64), configs[4]: profiles/r05fin_pmc.json for R = 2,
+# r05fin3_pmc.json for R = 3); X space (local) scaled as R = 1's 12.8 / 11.4
+VALU_PER_64_ROWS = {2: 7.67, 3: 7.00}
 
 AFFINE = dict(match=2, mismatch=-1, gap_open=-2, gap_extend=-1)
 METRIC = "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; % of HBM roofline"
