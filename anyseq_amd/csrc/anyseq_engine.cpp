@@ -303,6 +303,7 @@ void init_tuning_locked() {
     g_tuning.thr = env_int("ANYSEQ_THROTTLE", g_tuning.thr);
     g_tuning.NWa = env_int("ANYSEQ_NWA", g_tuning.NWa);
     g_tuning.arows = env_int("ANYSEQ_AFF_ROWS", g_tuning.arows);
+    g_tuning.selffwd = env_int("ANYSEQ_SELF_FWD", g_tuning.selffwd);
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
@@ -369,12 +370,15 @@ int aff_waves_per_group() {
 // (measured, tools/micro/aff_loop_micro.hip, profiles/r04_ab_nw_st.json).  Chain-bound
 // launches (every configs[2] Hirschberg level) keep 4; throughput-bound ones (the
 // genome-length fills, bands >> waves) take 7.  An explicit affine_waves_per_group wins.
+// Round 5: the throughput-bound launches run 8 compute waves and no I/O wave when
+// `affine_self_forward` is on (each group's first band forwards its own input row), so no
+// compute wave runs alone beside the I/O wave on its SIMD.
 int aff_waves_for(int64_t chain_steps, int64_t wave_steps, int grid) {
-    if (g_tuning.NWa == 3 || g_tuning.NWa == 4 || g_tuning.NWa == 7) return g_tuning.NWa;
+    if (g_tuning.NWa == 3 || g_tuning.NWa == 4 || g_tuning.NWa == 7 || g_tuning.NWa == 8) return g_tuning.NWa;
     const double g = (double)std::max(grid, 1);
     const double t4 = std::max((double)chain_steps, (double)wave_steps / (4.0 * g));
     const double t7 = 1.55 * std::max((double)chain_steps, (double)wave_steps / (7.0 * g));
-    return t7 < 0.9 * t4 ? 7 : 4;
+    return t7 < 0.9 * t4 ? (g_tuning.selffwd ? 8 : 7) : 4;
 }
 
 // Affine fill, rows per lane of one launch (round 5): R rows per lane share
@@ -387,11 +391,12 @@ int aff_waves_for(int64_t chain_steps, int64_t wave_steps, int grid) {
 // least model time when it gains >= 10 % over one row; an explicit affine_rows_per_lane wins
 // (2 and 3 need NW 4 or 7).
 int aff_rows_for(int NW, const int64_t (&chain)[3], int64_t work, int grid) {
-    if (g_tuning.arows >= 1 && g_tuning.arows <= 3) return g_tuning.arows == 1 || NW == 4 || NW == 7 ? g_tuning.arows : 1;
-    if (NW != 7) return 1;
+    if (g_tuning.arows >= 1 && g_tuning.arows <= 3)
+        return g_tuning.arows == 1 || NW == 4 || NW == 7 || NW == 8 ? g_tuning.arows : 1;
+    if (NW != 7 && NW != 8) return 1;
     const double g = (double)std::max(grid, 1), s[3] = {1.0, 1.5, 2.13};
     double t[3];
-    for (int r = 0; r < 3; ++r) t[r] = s[r] * std::max((double)chain[r], (double)work / (7.0 * (r + 1) * g));
+    for (int r = 0; r < 3; ++r) t[r] = s[r] * std::max((double)chain[r], (double)work / ((double)NW * (r + 1) * g));
     const int best = t[2] < t[1] ? 3 : 2;
     return t[best - 1] < 0.9 * t[0] ? best : 1;
 }
@@ -2303,6 +2308,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "fronts") g_tuning.fronts = value;
     else if (n == "affine_waves_per_group") g_tuning.NWa = value;
     else if (n == "affine_rows_per_lane") g_tuning.arows = value;
+    else if (n == "affine_self_forward") g_tuning.selffwd = value;
     else if (n == "affine_grid") g_tuning.grida = value;
     else if (n == "affine_asm") g_tuning.affasm = value;
     else if (n == "ring_slots") g_tuning.ring_slots = value;

@@ -84,6 +84,7 @@ struct Tuning {
     int fronts = 2;
     int NWa = 0;     // affine fill: compute waves per workgroup (3, 4 or 7; 0 = chosen per launch)
     int arows = 0;   // affine fill: rows per lane (1, 2, 3; 0 = chosen per launch, aff_rows_for)
+    int selffwd = 1; // affine fill: throughput-bound launches with 8 compute waves, no I/O wave
     int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
     int affasm = 1;  // affine fill: bit 0 asm steady state; bit 1 no asm epilogue; bits 2/3 none for best-all / other;
                      // bit 5 the round-3 band end (capturing epilogue), bit 6 its start (C++ spin) (A/B; round 5:

@@ -1487,6 +1487,73 @@ struct AffIO {
     uint32_t* s_filled;
     uint32_t* tail;
     int2* gout;   // last band of a group: HBM destination of the bottom row (G, F)
+    // Self-forwarding (round 5, no I/O wave): the group's first band copies the previous
+    // group's bottom row from this HBM hand-off row into its own ring, a segment ahead
+    const int2* g_in;
+    bool reset_in;   // put the sentinel back (the row is reused)
+};
+
+// Self-forwarding first band of a group (round 5): io_forward's protocol run by the band
+// itself between its asm segments -- granules of 16 columns are in when none of their
+// columns < w holds the sentinel; the ring gets them, the HBM row gets the sentinel back.
+// Brings the ring (and *my_prod, in half chunks) up to chunk `cend` (exclusive), never
+// more than kSlots - 1 chunks past the band's current block `b`.  false on timeout.
+struct SelfFwd {
+    int gran = 0;   // granules forwarded
+    __device__ bool forward_to(const AffIO& io, int lane, int w, int b, int cend, uint32_t* err) {
+        constexpr int CH = 32, GR = 16, IRM = kSlots * CH - 1;
+        const int nchunks = (w + CH - 1) / CH, ngran = (w + GR - 1) / GR;
+        const int tg = min(2 * min(cend, b + kSlots - 1), ngran);
+        if (gran >= tg) return true;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t idle = 0;
+        while (gran < tg) {
+            const int lim = min(gran + 8, tg);
+            int2 pv[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int col = gran * GR + i * 64 + lane;
+                pv[i] = col < lim * GR && col < w ? HandOff<int2>::load(io.g_in + col) : HandOff<int2>::zero();
+            }
+            int ready = 0;
+            bool stop = false;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint64_t bad = __ballot(HandOff<int2>::pending(pv[i]));
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    if (!stop && gran + 4 * i + g < lim && ((bad >> (16 * g)) & 0xffffu) == 0u) ++ready;
+                    else stop = true;
+                }
+            }
+            if (ready == 0) {
+                __builtin_amdgcn_s_sleep(1);
+                if ((++idle & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || err_set(err))) {
+                    atomicOr(err, ERR_SPIN_TIMEOUT | 8u);
+                    return false;
+                }
+                continue;
+            }
+            const int c0 = gran * GR, c2 = (gran + ready) * GR;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int col = c0 + i * 64 + lane;
+                if (col < c2) io.my_ring[col & IRM] = pv[i];
+                if (io.reset_in && col < c2) HandOff<int2>::store(const_cast<int2*>(io.g_in) + col, HandOff<int2>::sentinel());
+            }
+            gran += ready;
+            if (gran >= ngran) {   // "minus infinity" past the last granule; the producer's last chunk past w
+                const int c = ngran * GR + lane;
+                if (c < nchunks * CH) {
+                    io.my_ring[c & IRM] = HandOff<int2>::neg();
+                    if (io.reset_in) HandOff<int2>::store(const_cast<int2*>(io.g_in) + c, HandOff<int2>::sentinel());
+                }
+            }
+            idle = 0;
+        }
+        lds_st(io.my_prod, gran >= ngran ? (uint32_t)(2 * nchunks) : (uint32_t)gran);
+        return true;
+    }
 };
 
 // 32 steps in C++ (prologue / epilogue / partial bands; the steady state is the asm
@@ -1954,6 +2021,11 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
     const int nblocks = nchunks + LAG;
     const int fe = w >= CH - 1 ? (w - (CH - 1)) / CH + 1 : 0;   // full blocks: 32b + 30 < w
     uint32_t seen_prod = 0, seen_sfill = 0, seen_cons = 0;
+    // self-forwarding first band (no I/O wave): asm segments of kFwdSeg blocks, the ring
+    // brought up to the segment's end before each
+    const bool self_fwd = io.g_in != nullptr;
+    constexpr int kFwdSeg = kSlots - 4;
+    SelfFwd fw;
     uint64_t ts_v = 0, te_v = 0;   // diagnostic build: steady-state start / end (s_memrealtime)
     uint32_t ts_f = 0, nmiss = 0;  // diagnostic build: + hand-off waits
     // diagnostic build: hand-off event record of the band (tools/probes/_aff_timeline.py)
@@ -2031,6 +2103,11 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
         const int t0 = b * CH;
         if constexpr (ASM_OK) {
             if ((virt || t0 >= 64) && b < fe && !(k.flags & 1)) {
+                // self-forwarding: the fused end once the band's remaining chunks fit the ring,
+                // else a main-loop segment of kFwdSeg blocks
+                const bool fwd_end = !self_fwd || nblocks - b <= kFwdSeg + 1;
+                const int seg_end = self_fwd ? min(fe, b + kFwdSeg) : fe;
+                if (self_fwd && !fw.forward_to(io, lane, w, b, fwd_end ? nchunks : seg_end, err)) return;
                 // one block of slack: block b starts once chunk b+1 is published, so in the
                 // steady state the loop's poll (step 16) already sees the next chunk and
                 // prefetches its top row -- no wait on the band chain's critical path
@@ -2092,7 +2169,7 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                 const bool top_safe = !io.in_border || (B.tfree ? clamp : B.tg == kAffNeg);
                 const bool best_safe = bestmode == 0 || (bestmode == 1 && ff_loses && top_safe);
                 const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || !best_safe || (k.flags & 32);
-                if (epi && !need_cap) {
+                if (epi && !need_cap && fwd_end) {
 #define AF2_CALL(LV, BD, PB, LU)                                                                                  \
     if constexpr (RR > 1)                                                                                         \
         st = aff2n_loop_asm<RR, LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, \
@@ -2121,20 +2198,21 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                 }
 #define AF2_CALL(LV, BD, PB, LU)                                                                               \
     if constexpr (RR > 1)                                                                                      \
-        st = aff2n_loop_asm<RR, LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, \
-                                                g, fdn, dg, tf, e, hg, bx, gu, eu, hgu, bxu);                    \
+        st = aff2n_loop_asm<RR, LV, BD, PB, LU>(bb, (uint32_t)seg_end, seen_prod, seen_sfill, seen_cons, la, go, \
+                                                nge, g, fdn, dg, tf, e, hg, bx, gu, eu, hgu, bxu);               \
     else                                                                                                       \
-        st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)fe, seen_prod, seen_sfill, seen_cons, la, go, nge, g, fdn, \
-                                           dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, nullptr, dbp)
+        st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)seg_end, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
+                                           fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, nullptr, dbp)
                 if (xs) {
                     if (k.lut) { AF2_ROLES(true, true) } else { AF2_ROLES(true, false) }
                 } else {
                     if (k.lut) { AF2_ROLES(false, true) } else { AF2_ROLES(false, false) }
                 }
 #undef AF2_CALL
-                if (!st && epi) {
+                if (!st && epi && (int)bb >= fe) {
                     // the band's last blocks in the loop too: every lane runs on past column
                     // w-1 (subject code 0xFF there) and keeps its column-(w-1) state
+                    if (self_fwd && !fw.forward_to(io, lane, w, (int)bb, nchunks, err)) return;
 #ifdef ANYSEQ_STAMPS
                     ev_store(7, te_v);                               // main loop end
                     ev_store(8, __builtin_amdgcn_s_memrealtime());   // epilogue entry
@@ -2242,6 +2320,7 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                 const int bvr = xs ? to_x(bv, t0 + lane) : bv;   // rings hold the loop's space
                 io.my_ring[(t0 + lane) & IRM] = make_int2(bvr, bvr + go);
             } else if (seen_prod < (uint32_t)(2 * b + 2)) {
+                if (self_fwd && !fw.forward_to(io, lane, w, b, b + 4, err)) return;
                 if (!(seen_prod = spin_lds_ge(io.my_prod, (uint32_t)(2 * b + 2), err))) return;
             }
             const int4* src = reinterpret_cast<const int4*>(io.my_ring + (t0 & IRM));
@@ -2401,8 +2480,10 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
     }
 }
 
+// NW 8 (round 5): eight compute waves and no I/O wave -- each group's first band forwards
+// its own input row (SelfFwd), so every SIMD runs two compute waves
 template <int NW, int RR>
-__global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProblem* __restrict__ probs,
+__global__ __launch_bounds__(NW == 8 ? 512 : 64 * (NW + 1)) void fill_affine_kernel(const DPProblem* __restrict__ probs,
                                                                      const GroupRef* __restrict__ groups,
                                                                      int ngroups_total, uint32_t* dq, uint32_t* err,
                                                                      FillParams fp) {
@@ -2481,7 +2562,10 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
             g_out = reinterpret_cast<int2*>(P.out_row);
         // (GS: always the forwarder -- the I/O wave has no subject work; io_wave, a called
         // function, would give the kernel a stack and every launch a scratch setup)
-        if (wave == NW && (kAffGS || fp.io_fwd)) {
+        constexpr bool kSelfFwd = NW == 8;
+        static_assert(!kSelfFwd || kAffGS, "self-forwarding needs the code rows");
+        if (kSelfFwd && wave == NW) {
+        } else if (wave == NW && (kAffGS || fp.io_fwd)) {
             const int2* g_in = gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad : nullptr;
             io_forward<int2>(lane, P.w, g_in, sh.in_ring[0], &sh.prod[0], &sh.cons[0], err,
                              P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc, 2, 2, fp.prio == 3,
@@ -2517,6 +2601,9 @@ __global__ __launch_bounds__(64 * (NW + 1)) void fill_affine_kernel(const DPProb
                 io.next_prod = band < last ? &sh.prod[wave + 1] : nullptr;
                 io.next_cons = band < last ? &sh.cons[wave + 1] : nullptr;
                 io.gout = band < last ? nullptr : g_out;
+                io.g_in = kSelfFwd && wave == 0 && gr.group > 0 ? rows + (size_t)((gr.group - 1) % P.nslots) * P.wpad
+                                                                : nullptr;
+                io.reset_in = P.nslots < P.ngroups - 1 || P.pad_ == kPlannedDesc;
                 if ((band + 1) * 64 * RR > P.h) run_band_aff<true, RR>(P, band, lane, io, err, k, fp.dbg);
                 else run_band_aff<false, RR>(P, band, lane, io, err, k, fp.dbg);
             }
@@ -4308,8 +4395,8 @@ static hipError_t launch_fill_c(int R, int NW, const DPProblem* probs, const Gro
 template <int NW, int RR>
 static hipError_t launch_fill_aff_n(const DPProblem* probs, const GroupRef* groups, int ngroups, uint32_t* dq,
                                     uint32_t* err, const FillParams& fp, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((fill_affine_kernel<NW, RR>), dim3(grid), dim3(64 * (NW + 1)), 0, st, probs, groups, ngroups,
-                       dq, err, fp);
+    hipLaunchKernelGGL((fill_affine_kernel<NW, RR>), dim3(grid), dim3(NW == 8 ? 512 : 64 * (NW + 1)), 0, st, probs,
+                       groups, ngroups, dq, err, fp);
     return hipGetLastError();
 }
 #endif  // ANYSEQ_MICRO
@@ -4540,13 +4627,17 @@ hipError_t anyseq_launch_fill_affine(int NW, const anyseq::DPProblem* probs, con
     using namespace anyseq;
     // (the asm steady state holds ~150 fixed VGPRs: at most 2 waves per SIMD, NW <= 7)
     // fp->arows 2 / 3: rows per lane (NW 4 or 7; the descriptors' nbands count 64 arows-row bands)
+    // NW 8: eight compute waves, the groups' first bands forwarding their own input rows
     if (fp->arows == 2 || fp->arows == 3) {
         if (NW == 7 && fp->arows == 2) return launch_fill_aff_n<7, 2>(probs, groups, ngroups, dq, err, *fp, grid, st);
         if (NW == 4 && fp->arows == 2) return launch_fill_aff_n<4, 2>(probs, groups, ngroups, dq, err, *fp, grid, st);
+        if (NW == 8 && fp->arows == 2) return launch_fill_aff_n<8, 2>(probs, groups, ngroups, dq, err, *fp, grid, st);
         if (NW == 7) return launch_fill_aff_n<7, 3>(probs, groups, ngroups, dq, err, *fp, grid, st);
         if (NW == 4) return launch_fill_aff_n<4, 3>(probs, groups, ngroups, dq, err, *fp, grid, st);
+        if (NW == 8) return launch_fill_aff_n<8, 3>(probs, groups, ngroups, dq, err, *fp, grid, st);
         return hipErrorInvalidValue;
     }
+    if (NW == 8) return launch_fill_aff_n<8, 1>(probs, groups, ngroups, dq, err, *fp, grid, st);
     if (NW == 3) return launch_fill_aff_n<3, 1>(probs, groups, ngroups, dq, err, *fp, grid, st);
     if (NW == 7) return launch_fill_aff_n<7, 1>(probs, groups, ngroups, dq, err, *fp, grid, st);
     return launch_fill_aff_n<4, 1>(probs, groups, ngroups, dq, err, *fp, grid, st);

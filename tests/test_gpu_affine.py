@@ -93,9 +93,10 @@ def test_affine_bytes_and_similar(anyseq, oracle, kind):
     assert gpu(anyseq, kind, base, s2, sc) == ora(oracle, kind, base, s2, sc)
 
 
-@pytest.mark.parametrize("nw", [3, 4, 7])
+@pytest.mark.parametrize("nw", [3, 4, 7, 8])
 def test_affine_waves_per_group(anyseq, oracle, nw):
-    """Forced compute waves per workgroup (7: two per SIMD beside the I/O wave) give the
+    """Forced compute waves per workgroup (7: two per SIMD beside the I/O wave; 8: two per
+    SIMD and no I/O wave, the groups' first bands forwarding their own input rows) give the
     same scores and constructs; 0 (the default) chooses per launch."""
     rng = random.Random(27)
     anyseq.set_option("affine_waves_per_group", nw)
