@@ -144,3 +144,25 @@ def test_r2_shards(anyseq, oracle, r2):
             got = anyseq.shard_score_local(kind, q, s, ns, match=sc[0], mismatch=sc[1], gap_open=sc[2],
                                            gap_extend=sc[3])
             assert got == ora(oracle, kind, q, s, sc), (kind, n, m, ns)
+
+
+def test_self_forward_rows_stay_clean(anyseq, oracle, monkeypatch):
+    """Eight compute waves without the I/O wave (the groups' first bands forward their own
+    input rows): with a small grid every hand-off ring is reused within the launch, so the
+    first bands must put the sentinel back exactly as the forwarder did -- checked after
+    each host-built fill by ANYSEQ_CHECK_ROWS, at one to three rows per lane."""
+    rng = random.Random(48)
+    q, s = rnd(rng, 80000), rnd(rng, 700)   # (>= 53 groups of 8 bands at three rows: rings reused)
+    sc = (2, -1, -2, -1)
+    anyseq.set_option("affine_grid", 8)
+    anyseq.set_option("affine_waves_per_group", 8)
+    monkeypatch.setenv("ANYSEQ_CHECK_ROWS", "1")
+    try:
+        for rows in (1, 2, 3):
+            anyseq.set_option("affine_rows_per_lane", rows)
+            for kind in KINDS:
+                assert gpu(anyseq, kind, q, s, sc) == ora(oracle, kind, q, s, sc), (kind, rows)
+    finally:
+        anyseq.set_option("affine_rows_per_lane", 0)
+        anyseq.set_option("affine_waves_per_group", 0)
+        anyseq.set_option("affine_grid", 0)
