@@ -90,6 +90,7 @@ thread_local double g_fill_ms = 0.0;
 thread_local int g_fill_launches = 0;
 thread_local int g_fill_r2 = 0;     // affine launches with >= 2 rows per lane (anyseq_last_fill_multi_row_launches)
 thread_local int g_fill_rmax = 1;   // the most rows per lane among them
+thread_local int g_fill_stages = 0;
 thread_local int g_shard_blocked_levels = 0;   // anyseq_last_shard_plan
 thread_local int64_t g_fill_cells = 0;
 
@@ -387,16 +388,20 @@ int aff_waves_for(int64_t chain_steps, int64_t wave_steps, int grid) {
 // mix_micro.hip R2FULL / FULL, profiles/r05aa_mix_micro_r2.txt), s_3 = 2.13 (the projection
 // says 2.01, R3FULL 167.6; the product measures 1.054x over two rows at configs[4], 1.063x at
 // configs[3], gpurun_out/r05af / r05ag).  The throughput gains, but the band chain steps at
-// s_R for a hop over 64 R rows (chain_R = w + 1.28 h / R).  NW 7 launches take the R with the
-// least model time when it gains >= 10 % over one row; an explicit affine_rows_per_lane wins
-// (2 and 3 need NW 4 or 7).
-int aff_rows_for(int NW, const int64_t (&chain)[3], int64_t work, int grid) {
+// s_R for a hop over 64 R rows (chain_R = w + 1.28 h / R), and a column-block pipeline's
+// ranks start one band sweep of the block (w steps) after each other (g_fill_stages: the
+// pipeline's stages).  NW 7 / 8 launches take the R
+// with the least model time when it gains >= 10 % over one row; an explicit
+// affine_rows_per_lane wins (2 and 3 need NW 4, 7 or 8).
+int aff_rows_for(int NW, const int64_t (&chain)[3], int64_t work, int grid, int64_t wmax) {
     if (g_tuning.arows >= 1 && g_tuning.arows <= 3)
         return g_tuning.arows == 1 || NW == 4 || NW == 7 || NW == 8 ? g_tuning.arows : 1;
     if (NW != 7 && NW != 8) return 1;
     const double g = (double)std::max(grid, 1), s[3] = {1.0, 1.5, 2.13};
     double t[3];
-    for (int r = 0; r < 3; ++r) t[r] = s[r] * std::max((double)chain[r], (double)work / ((double)NW * (r + 1) * g));
+    for (int r = 0; r < 3; ++r)
+        t[r] = s[r] * (std::max((double)chain[r], (double)work / ((double)NW * (r + 1) * g)) +
+                       (double)g_fill_stages * (double)wmax);
     const int best = t[2] < t[1] ? 3 : 2;
     return t[best - 1] < 0.9 * t[0] ? best : 1;
 }
@@ -404,11 +409,13 @@ int aff_rows_for(int NW, const int64_t (&chain)[3], int64_t work, int grid) {
 namespace {
 // chain[r]: the longest band chain with r+1 rows per lane, w + 1.28 h / (r+1) steps; work:
 // one-row wave steps of the launch
-void aff_launch_model(const std::vector<DPProblem>& probs, int64_t (&chain)[3], int64_t& work) {
+void aff_launch_model(const std::vector<DPProblem>& probs, int64_t (&chain)[3], int64_t& work, int64_t& wmax) {
     chain[0] = chain[1] = chain[2] = 0;
     work = 0;
+    wmax = 0;
     for (const DPProblem& P : probs) {
         if (P.h <= 0 || P.w <= 0) continue;
+        wmax = std::max<int64_t>(wmax, P.w);
         for (int r = 0; r < 3; ++r) chain[r] = std::max(chain[r], (int64_t)P.w + (int64_t)P.h * 128 / (100 * (r + 1)));
         work += (int64_t)((P.h + 63) / 64) * ((int64_t)P.w + 64);
     }
@@ -463,11 +470,11 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     int NW = waves_per_group();
     int R = aff ? 1 : rows_per_lane();
     if (aff) {
-        int64_t chain[3], work;
-        aff_launch_model(probs, chain, work);
+        int64_t chain[3], work, wmax;
+        aff_launch_model(probs, chain, work, wmax);
         const int g0 = grid_req > 0 ? grid_req : (g_tuning.grida > 0 ? g_tuning.grida : E.num_cus);
         NW = aff_waves_for(chain[0], work, g0);
-        R = aff_rows_for(NW, chain, work, g0);   // (affine bands: 64 R rows)
+        R = aff_rows_for(NW, chain, work, g0, wmax);   // (affine bands: 64 R rows)
     }
     const int vpc = aff ? 2 : 1;
     // Persistent grid: at most `grid` groups are in flight, and a group finishes only after

@@ -195,6 +195,14 @@ int aff_waves_per_group();
 // the issue-priority mode of a fill launch (g_tuning.prio, per kind when -1)
 inline int fill_prio(bool affine) { return g_tuning.prio >= 0 ? g_tuning.prio : (affine ? 1 : 0); }
 int aff_waves_for(int64_t chain_steps, int64_t wave_steps, int grid);
+// Column-block pipelines (round 5): stages ahead of the last one for the fills prepared
+// while it is set (a rank starts one band sweep of its block after its left neighbour;
+// aff_rows_for weighs that start against the throughput of more rows per lane)
+extern thread_local int g_fill_stages;
+struct FillStages {
+    explicit FillStages(int s) { g_fill_stages = s > 0 ? s : 0; }
+    ~FillStages() { g_fill_stages = 0; }
+};
 
 FillParams make_params(int kind, const anyseq_scoring& sc);
 // An affine problem of kind `kind` over the whole matrix (or a shard of it): its

@@ -1956,7 +1956,10 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
     }
     // settle the query loads here: a vmcnt wait inside the step loop would also wait
     // for lane 63's HBM row stores
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(q), "+v"(qu[0]), "+v"(qu[NU - 1])::"memory");
+    if constexpr (NU > 1)
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(q), "+v"(qu[0]), "+v"(qu[1])::"memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(q), "+v"(qu[0])::"memory");
     if (kAffGS && !P.scode) {   // (a planned level whose code rows did not fit: its bound check fails too)
         if (lane == 0) atomicOr(err, ERR_BAD_DESC);
         return;

@@ -618,7 +618,10 @@ int64_t shard_score_local(int kind, const anyseq_scoring& sc, const char* q, int
     }
     const int grid = grid_per_shard(E, N);
     // every shard's allocations and uploads first: the fills wait for each other once launched
-    for (int g = 0; g < N; ++g) fill_prepare(E, shards[g].fc, probs[g], fp, shards[g].st, grid);
+    {
+        const FillStages stages(N - 1);
+        for (int g = 0; g < N; ++g) fill_prepare(E, shards[g].fc, probs[g], fp, shards[g].st, grid);
+    }
     for (int g = 0; g < N; ++g) fill_launch(shards[g].fc);
     std::vector<Xfer> xs = direct ? std::vector<Xfer>() : local_xfers(shards, N, E.device);
     std::vector<std::thread> th = start_xfers(xs);
@@ -737,7 +740,10 @@ int64_t shard_score_rccl(int kind, const anyseq_scoring& sc) {
         probs[0].best = res;
         probs[1].best = res;
     }
-    fill_async(E, S.fc, probs, fp, S.st, grid_per_shard(E, 1));
+    {
+        const FillStages stages(R.world - 1);
+        fill_async(E, S.fc, probs, fp, S.st, grid_per_shard(E, 1));
+    }
     std::vector<Xfer> xs = rccl_xfers(R, E.device);
     std::vector<std::thread> th = start_xfers(xs);
     bool ok = true;
