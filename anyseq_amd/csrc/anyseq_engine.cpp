@@ -305,6 +305,8 @@ void init_tuning_locked() {
     g_tuning.NWa = env_int("ANYSEQ_NWA", g_tuning.NWa);
     g_tuning.arows = env_int("ANYSEQ_AFF_ROWS", g_tuning.arows);
     g_tuning.selffwd = env_int("ANYSEQ_SELF_FWD", g_tuning.selffwd);
+    g_tuning.linaff = env_int("ANYSEQ_LIN_AFF", g_tuning.linaff);
+    g_tuning.linloop = env_int("ANYSEQ_LIN_LOOP", g_tuning.linloop);
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
@@ -858,6 +860,8 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     // bit 4: a NORMAL-border best of every cell may run the virtual prologue (its column
     // -1 border cells, at most go + ge, never exceed cell (0,0) >= min(match, mismatch))
     if (g_tuning.virtbest && std::min(sc.match, sc.mismatch) >= sc.gap_open + sc.gap_extend) fp.pad |= 16;
+    // bit 7: gap open 0 through the affine loop, not the linear one (A/B)
+    if (!g_tuning.linloop) fp.pad |= 128;
     fp.alpha = nullptr;
     fp.io_stage = g_tuning.io_stage;
     fp.io_skew = g_tuning.io_skew;
@@ -916,7 +920,13 @@ int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const ui
 int64_t score_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds, int m,
                   hipStream_t st) {
     if (n <= 0 || m <= 0) return empty_score(kind, n, m, sc);
-    if (sc.gap_open != 0) return score_dev_affine(E, kind, sc, dq, n, ds, m, st);
+    // a linear global / local score runs through the affine fill with gap open 0 (round 5,
+    // DESIGN.md §3.1b): its linear loop on the affine kernel's code rows, lean blocks and
+    // half-chunk hand-off.  (Semiglobal stays: its zero-open left border has no virtual
+    // prologue, so every band would start with two C++ blocks on the chain -- 21 % slower.
+    // linear_via_affine 2 takes it too, for the tests.)
+    const bool via_aff = g_tuning.linaff == 2 || (g_tuning.linaff == 1 && kind != KIND_SEMIGLOBAL);
+    if (sc.gap_open != 0 || via_aff) return score_dev_affine(E, kind, sc, dq, n, ds, m, st);
     const FillParams fp = make_params(kind, sc);
     const int wpad = (m + 63) & ~63;
     int32_t* res = (int32_t*)E.fc.ctr.get(128) + 4;
@@ -983,6 +993,7 @@ int64_t score_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* 
 int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq_raw, int n,
                          const uint8_t* ds_raw, int m, hipStream_t st) {
     FillParams fp = make_params(kind, sc);
+    fp.affine = 1;   // (also a linear score: gap open 0)
     const SeqCodes cd = prepare_codes(E, dq_raw, n, ds_raw, m, st);
     fp.alpha = cd.alpha;
     const uint8_t *dq = cd.q, *ds = cd.s;
@@ -2316,6 +2327,8 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_waves_per_group") g_tuning.NWa = value;
     else if (n == "affine_rows_per_lane") g_tuning.arows = value;
     else if (n == "affine_self_forward") g_tuning.selffwd = value;
+    else if (n == "linear_via_affine") g_tuning.linaff = value;
+    else if (n == "linear_affine_loop") g_tuning.linloop = value;
     else if (n == "affine_grid") g_tuning.grida = value;
     else if (n == "affine_asm") g_tuning.affasm = value;
     else if (n == "ring_slots") g_tuning.ring_slots = value;

@@ -1439,6 +1439,7 @@ struct AffK {
     bool codes;   // q / s hold alphabet codes (0xFF never a code): the virtual prologue may clamp
     bool lut;     // codes 0..7 and int8 weights: the v_perm weight table
     int slack;    // FillParams::slack
+    bool lin;     // gap open 0 (a linear score through this kernel): the linear asm loop (gen_aff2 lin)
 };
 
 // Borders of a problem in G space (H border values by border mode, see
@@ -1659,8 +1660,9 @@ struct Aff2Args {
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
                    [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr), [neg] "s"(negp), [sg] "s"(sg)    \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
-// EPI: 0 the steady state, 1 the band's last blocks with the capture, 2 without it
-template <bool L, bool BORDER, int PUB, bool LUT, int EPI = 0>
+// EPI: 0 the steady state, 1 the band's last blocks with the capture, 2 without it.
+// LIN: the linear loop (gen_aff2 lin: kinds N = G space, M = X space)
+template <bool L, bool BORDER, int PUB, bool LUT, int EPI = 0, bool LIN = false>
 __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                   const Aff2Args& a, int go, int nge, int& g, int& fdn, int& dg,
                                                   int2& tf, int& e, int& hg, int& bx, uint64_t& ts_v, uint64_t& te_v,
@@ -1696,29 +1698,39 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
     if constexpr (!BORDER && PUB == 0) A(AF2_NAME(ANYSEQ_##V##_##K##_B0_NONE_U##U));         \
     if constexpr (!BORDER && PUB == 1) A(AF2_NAME(ANYSEQ_##V##_##K##_B0_LDS_U##U));          \
     if constexpr (!BORDER && PUB == 2) A(AF2_NAME(ANYSEQ_##V##_##K##_B0_GLOB_U##U));
+// (the linear loops have no diagnostic-stamp variants: their names stay plain)
+#define AF2_SELN(A, V, K, U)                                                                  \
+    if constexpr (BORDER && PUB == 0) A(ANYSEQ_##V##_##K##_B1_NONE_U##U);                    \
+    if constexpr (BORDER && PUB == 1) A(ANYSEQ_##V##_##K##_B1_LDS_U##U);                     \
+    if constexpr (BORDER && PUB == 2) A(ANYSEQ_##V##_##K##_B1_GLOB_U##U);                    \
+    if constexpr (!BORDER && PUB == 0) A(ANYSEQ_##V##_##K##_B0_NONE_U##U);                   \
+    if constexpr (!BORDER && PUB == 1) A(ANYSEQ_##V##_##K##_B0_LDS_U##U);                    \
+    if constexpr (!BORDER && PUB == 2) A(ANYSEQ_##V##_##K##_B0_GLOB_U##U);
+#define AF2_KINDS(A, V)                                          \
+    if constexpr (!LIN && L && LUT) { AF2_SEL(A, V, L, 1) }       \
+    if constexpr (!LIN && L && !LUT) { AF2_SEL(A, V, L, 0) }      \
+    if constexpr (!LIN && !L && LUT) { AF2_SEL(A, V, G, 1) }      \
+    if constexpr (!LIN && !L && !LUT) { AF2_SEL(A, V, G, 0) }     \
+    if constexpr (LIN && L && LUT) { AF2_SELN(A, V, M, 1) }       \
+    if constexpr (LIN && L && !LUT) { AF2_SELN(A, V, M, 0) }      \
+    if constexpr (LIN && !L && LUT) { AF2_SELN(A, V, N, 1) }      \
+    if constexpr (LIN && !L && !LUT) { AF2_SELN(A, V, N, 0) }
     if constexpr (EPI == 1) {
         nch = __builtin_amdgcn_readfirstlane(nch);
         int cnt = cap[0], gc = cap[1], ec = cap[2], fc = cap[3];
-        if constexpr (L && LUT) { AF2_SEL(AF2E_ASM, AF2E, L, 1) }
-        if constexpr (L && !LUT) { AF2_SEL(AF2E_ASM, AF2E, L, 0) }
-        if constexpr (!L && LUT) { AF2_SEL(AF2E_ASM, AF2E, G, 1) }
-        if constexpr (!L && !LUT) { AF2_SEL(AF2E_ASM, AF2E, G, 0) }
+        AF2_KINDS(AF2E_ASM, AF2E)
         cap[0] = cnt, cap[1] = gc, cap[2] = ec, cap[3] = fc;
     } else if constexpr (EPI == 2) {
         nch = __builtin_amdgcn_readfirstlane(nch);
         const uint32_t negp = __builtin_amdgcn_readfirstlane(a.neg);
         (void)cap;
-        if constexpr (L && LUT) { AF2_SEL(AF2F_ASM, AF2F, L, 1) }
-        if constexpr (L && !LUT) { AF2_SEL(AF2F_ASM, AF2F, L, 0) }
-        if constexpr (!L && LUT) { AF2_SEL(AF2F_ASM, AF2F, G, 1) }
-        if constexpr (!L && !LUT) { AF2_SEL(AF2F_ASM, AF2F, G, 0) }
+        AF2_KINDS(AF2F_ASM, AF2F)
     } else {
         (void)nch, (void)cap;
-        if constexpr (L && LUT) { AF2_SEL(AF2_ASM, AF2, L, 1) }
-        if constexpr (L && !LUT) { AF2_SEL(AF2_ASM, AF2, L, 0) }
-        if constexpr (!L && LUT) { AF2_SEL(AF2_ASM, AF2, G, 1) }
-        if constexpr (!L && !LUT) { AF2_SEL(AF2_ASM, AF2, G, 0) }
+        AF2_KINDS(AF2_ASM, AF2)
     }
+#undef AF2_KINDS
+#undef AF2_SELN
 #undef AF2_SEL
     tf = make_int2(tfg, tff);
     return st;
@@ -2049,6 +2061,8 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
     // codes (0xFF beyond w) and not a last-row best (the last row's cells are read per
     // column); the loop's best takes real cells only
     const bool epi = k.codes && !(k.flags & 3) && bestmode != 2 && !(k.flags & (bestmode == 1 ? 4 : 8));
+    // gap open 0: the linear loop (one row per lane; its band end keeps no exact E for out_col_e)
+    const bool lin = RR == 1 && k.lin && !P.out_col_e;
     Aff2Args la;
     if constexpr (ASM_OK) {
         la.rb = lds_addr(io.my_ring);
@@ -2178,6 +2192,10 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
         st = aff2n_loop_asm<RR, LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, \
                                                    nge, g, fdn, dg, tf, e, hg, bx, gu, eu, hgu, bxu,             \
                                                    (uint32_t)(2 * nchunks));                                     \
+    else if (lin)                                                                                                 \
+        st = aff2_loop_asm<LV, BD, PB, LU, 2, true>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, \
+                                                    nge, g, fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss,        \
+                                                    (uint32_t)(2 * nchunks), nullptr, dbp);                         \
     else                                                                                                          \
         st = aff2_loop_asm<LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
                                               fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), \
@@ -2203,6 +2221,10 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
     if constexpr (RR > 1)                                                                                      \
         st = aff2n_loop_asm<RR, LV, BD, PB, LU>(bb, (uint32_t)seg_end, seen_prod, seen_sfill, seen_cons, la, go, \
                                                 nge, g, fdn, dg, tf, e, hg, bx, gu, eu, hgu, bxu);               \
+    else if (lin)                                                                                              \
+        st = aff2_loop_asm<LV, BD, PB, LU, 0, true>(bb, (uint32_t)seg_end, seen_prod, seen_sfill, seen_cons, la, go, \
+                                                    nge, g, fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u,     \
+                                                    nullptr, dbp);                                                   \
     else                                                                                                       \
         st = aff2_loop_asm<LV, BD, PB, LU>(bb, (uint32_t)seg_end, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
                                            fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, nullptr, dbp)
@@ -2237,6 +2259,10 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
         st = aff2n_loop_asm<RR, LV, BD, PB, LU, 1>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, \
                                                    nge, g, fdn, dg, tf, e, hg, bx, gu, eu, hgu, bxu,             \
                                                    (uint32_t)(2 * nchunks), cap);                                \
+    else if (lin)                                                                                              \
+        st = aff2_loop_asm<LV, BD, PB, LU, 1, true>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, \
+                                                    nge, g, fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss,        \
+                                                    (uint32_t)(2 * nchunks), cap, dbp);                             \
     else                                                                                                       \
         st = aff2_loop_asm<LV, BD, PB, LU, 1>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, nge, g, \
                                               fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, (uint32_t)(2 * nchunks), \
@@ -2505,6 +2531,7 @@ __global__ __launch_bounds__(NW == 8 ? 512 : 64 * (NW + 1)) void fill_affine_ker
     k.codes = nsym > 0 && nsym < 255;
     k.lut = nsym > 0 && nsym <= 8 && fp.lut_ok;
     k.slack = fp.slack;
+    k.lin = fp.gap_open == 0 && !(fp.pad & 128);
     // issue priority: 1 = compute waves before the I/O wave, 2 = the I/O wave first (it
     // sleeps when idle; its hand-off polls sit on the band chain)
     if (fp.prio == 1 && wave < NW) __builtin_amdgcn_s_setprio(3);

@@ -60,7 +60,10 @@ VALU_DESIGN_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
 # wave step (profiles/r03a_pmc.json: SQ_INSTS_VALU / (cells / 64)), 12.8 in round 4
 # (profiles/r04z_pmc.json: 859.2 M per 65536^2 local score launch); G space = 9.25 +
 # the same 2.15 of block overhead.
-VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.4, "affine_local": 12.8}
+VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.4, "affine_local": 12.8,
+                 # linear global / local scores through the affine fill's linear loop (round 5:
+                 # gen_aff2 lin, 4.25 / 6.75 VALU per step in the loop + the block's ~1)
+                 "linear_aff": 5.25, "linear_aff_local": 7.75}
 # Affine fill with R rows per lane (round 5): VALU per 64 cells, measured
 # (SQ_INSTS_VALU / (cells / 64), configs[4]: profiles/r05fin_pmc.json for R = 2,
 # r05fin3_pmc.json for R = 3); X space (local) scaled as R = 1's 12.8 / 11.4
@@ -557,8 +560,12 @@ def score_bench(args, world, rank, local_rank):
     gcups = cells_per_step * args.steps / elapsed / 1e9
     kernel_ms = fill_ms / max(launches, 1)
     aff = bool(args.gap_open)
-    valu_key = ("affine" if aff else "linear") + ("_local" if kind == "local" else "")
-    tag = f"fill_affine_kernel<{kind}> {n}x{m}" if aff else f"fill_kernel<{kind}> {n}x{m}"
+    # linear global / local scores run on fill_affine_kernel's linear loop (the library's
+    # linear_via_affine 1 default), linear semiglobal and the sharded linear
+    # fills on fill_kernel
+    lin_aff = not aff and kind in ("global", "local") and not dist
+    valu_key = ("affine" if aff else "linear_aff" if lin_aff else "linear") + ("_local" if kind == "local" else "")
+    tag = f"fill_affine_kernel<{kind}> {n}x{m}" if aff or lin_aff else f"fill_kernel<{kind}> {n}x{m}"
 
     if rank == 0:
         st = step_stats(ts)
@@ -584,8 +591,8 @@ def score_bench(args, world, rank, local_rank):
                    "fill_rows_per_lane_max": rows_max,
                        "transport": ("RCCL send/recv (host-polled chunk trigger), unmeasured on hardware "
                                      "(no multi-GPU run before this one)" if world > 1 else None)},
-            "roofline": roofline("fill_affine_kernel" if aff else "fill_kernel", cells_per_launch, kernel_ms,
-                                 valu_key, tag, rows_max if aff else 1),
+            "roofline": roofline("fill_affine_kernel" if aff or lin_aff else "fill_kernel", cells_per_launch,
+                                 kernel_ms, valu_key, tag, rows_max if aff else 1),
         }
         out["roofline"]["kernel_timing"] = kernel_timing
         if world == 1 and not args.no_cpu_baseline:

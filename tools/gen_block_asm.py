@@ -366,7 +366,7 @@ def OFB_(u):
     return OFk_(1, u)
 
 
-def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1):
+def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin=False):
     """Affine steady-state loop, round 3: full blocks b .. be-1.
     kind G: G space (X_G = X + (r+c+2)|ge|), no clamp, no best (amode 0).
     kind L: X space (X = H + (r+2)|ge|, a per-ROW shift): the local clamp H >= 0 is
@@ -408,9 +408,17 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1):
     row), so the hand-off is the one-row kernel's.  The DPP moves are shared by two cells:
     16.4 instead of 2 x 11.2 instructions per step (tools/micro/gen_mix_micro.py).
     nrows 3: rows 3l, 3l+1, 3l+2 the same way (row k from row k-1; %[gb] carries row B's
-    cell of the previous step into row C's diagonal; %[ex] / %[hgx] / ... row C's)."""
+    cell of the previous step into row C's diagonal; %[ex] / %[hgx] / ... row C's).
+    lin (round 5): the LINEAR gap recurrence in the same loop (the affine one with gap open
+    0, where E = the left cell and F = the cell above): G space G = max3(G_diag + w,
+    G_left, G_up); X space (kind L, local) X = max3(X_diag + w, max(X_left, zl') - |ge|,
+    X_up) with zl' = %[zlp] = the clamp bound + |ge|.  One DPP and one shift-register move
+    per step; the published pairs carry (G, G) (F-down = G), and at loop exit %[fd], %[e]
+    and %[hg] get the last cell (the C++ blocks' affine step with open 0 then continues
+    exactly: E and F of the next cell are the left and upper cells)."""
     L = kind == "L"
     r2 = nrows > 1
+    assert not (lin and r2)
     last = nrows - 1
     assert not r2 or (REORDER and LEAN and SLIM and GS and not ts)
     OGP, OFP = (lambda u: OGk_(last, u)), (lambda u: OFk_(last, u))   # the published / lane-shifted cells
@@ -536,7 +544,10 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1):
     def publish(k, half, reg):
         """Lanes 48..63 of the (G, F) pair `reg` hold 16 columns of chunk b-2: half
         `half` of the next band's top row (LDS: always written -- a dummy slot and
-        counter 0 while b < 2 -- so the counted lgkmcnt waits stay fixed)."""
+        counter 0 while b < 2 -- so the counted lgkmcnt waits stay fixed).  Linear: the
+        pair's F register gets the cell first (F-down = G)."""
+        if lin:
+            e(f"v_mov_b32_e32 v{reg + 1}, v{reg}")
         if pub == "lds" and SLIM:
             # round 4: the slot address once per block (half 1 reuses it through the
             # offset field), the counter written by the same 16 lanes inside the exec
@@ -705,12 +716,45 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1):
             # Instruction order (round 4): no VALU reads the result of the instruction
             # right before it -- E's max3 first, the DPP moves between the E pair, the
             # shift-register moves between OG -> hg -> F-down, the best after hg.
-            if REORDER:
+            if lin:
+                # linear step: weight, the cell above by DPP (2 wait states after the left
+                # cell's max3: s_nop where the weight and the shift register leave fewer)
+                sr = u >= 2 and pub != "none"
+                # VALU since the left cell's max3: the previous step's shift-register move (the
+                # block's first step follows the block start's moves, waits and reads)
+                nv = 2 if u == 0 else (1 if u - 1 >= 2 and pub != "none" else 0)
+                if lut:
+                    if u % 4 == 0:
+                        e(f"v_perm_b32 v{B_WB}, %[lh], %[ll], {sw}")
+                        nv += 1
+                    e(f"v_add_u32_sdwa v{B_AA}, {dg}, sext(v{B_WB}) dst_sel:DWORD dst_unused:UNUSED_PAD "
+                      f"src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+                    nv += 1
+                else:
+                    e(f"v_cmp_eq_u32_sdwa vcc, %[q], {sw} src0_sel:DWORD src1_sel:BYTE_{u % 4}")
+                    e(f"v_cndmask_b32_e32 v{B_AW}, %[wx], %[wm], vcc")
+                    e(f"v_add_u32_e32 v{B_AA}, {dg}, v{B_AW}")
+                    nv += 3
+                if L:
+                    e(f"v_max_i32_e32 v{B_AT}, {g}, %[zlp]")
+                    e(f"v_add_u32_e32 v{B_AT}, %[ge], v{B_AT}")
+                    nv += 2
+                if nv < 2:
+                    e(f"s_nop {1 - nv}")
+                e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_max3_i32 {OG_(u)}, v{B_AA}, {'v' + str(B_AT) if L else g}, {tg}")
+                if L and u % 2 == 1 and not (epi and cap):
+                    e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
+                if sr:
+                    e(f"v_mov_b32_dpp {OG_(u - 1)}, {OG_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            elif REORDER:
                 if L:
                     e("v_max3_i32 %[e], %[e], %[hg], %[zlp]")
                 else:
                     e("v_max_i32_e32 %[e], %[e], %[hg]")
-            if lut:
+            if lin:
+                pass
+            elif lut:
                 if u % 4 == 0:
                     e(f"v_perm_b32 v{B_WB}, %[lh], %[ll], {sw}")
                 e(f"v_add_u32_sdwa v{B_AA}, {dg}, sext(v{B_WB}) dst_sel:DWORD dst_unused:UNUSED_PAD "
@@ -720,7 +764,9 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1):
                 e(f"v_cndmask_b32_e32 v{B_AW}, %[wx], %[wm], vcc")
                 e(f"v_add_u32_e32 v{B_AA}, {dg}, v{B_AW}")
             sr = u >= 2 and pub != "none"
-            if REORDER:
+            if lin:
+                pass
+            elif REORDER:
                 e(f"v_mov_b32_dpp {tf}, {f} wave_shr:1 row_mask:0xf bank_mask:0xf")
                 if L:
                     e("v_add_u32_e32 %[e], %[ge], %[e]")
@@ -786,8 +832,16 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1):
                 # the lane whose cell is column w-1 at this step keeps its state
                 e("v_cmp_eq_u32_e32 vcc, 0, %[cnt]")
                 e(f"v_cndmask_b32_e32 %[gc], %[gc], {OG_(u)}, vcc")
-                e("v_cndmask_b32_e32 %[ec], %[ec], %[e], vcc")
-                if r2:
+                if lin:
+                    # (linear: F-down = the cell; E = the left cell, G space -- the kernel
+                    # never asks a linear band for out_col_e)
+                    e(f"v_cndmask_b32_e32 %[ec], %[ec], {g}, vcc")
+                    e(f"v_cndmask_b32_e32 %[fc], %[fc], {OG_(u)}, vcc")
+                else:
+                    e("v_cndmask_b32_e32 %[ec], %[ec], %[e], vcc")
+                if lin:
+                    pass
+                elif r2:
                     # (a row's F-down is the next row's F-in: only the last row's is kept)
                     for rk in range(1, nrows):
                         t = ROWTAG[rk]
@@ -809,12 +863,14 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1):
             g, f, dg = OGP(u), OFP(u), tg
         if not LEAN or pub != "none":
             e(f"v_mov_b32_e32 %[cur], {OGP(31)}")
-            e(f"v_mov_b32_e32 %[fd], {OFP(31)}")
+            # (linear: F-down = the cell; also the shift move's second wait state)
+            e(f"v_mov_b32_e32 %[fd], {OGP(31) if lin else OFP(31)}")
         if not LEAN:
             e(f"v_mov_b32_e32 %[dg], {TG_(30)}")
         if pub != "none":
             e(f"v_mov_b32_dpp {OGP(31)}, {OGP(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
-            e(f"v_mov_b32_dpp {OFP(31)}, {OFP(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            if not lin:
+                e(f"v_mov_b32_dpp {OFP(31)}, {OFP(30)} wave_shl:1 row_mask:0xf bank_mask:0xf")
         if not LEAN:
             e(f"v_mov_b32_e32 %[tfg], {TG_(31)}")
             e(f"v_mov_b32_e32 %[tff], {TF_(31)}")
@@ -889,6 +945,10 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1):
     if LEAN:
         for named, reg in lean_regs:
             e(f"v_mov_b32_e32 {named}, {reg}")
+    if lin:
+        # the C++ blocks' open-0 affine step: F-down, E and G + go of the last cell
+        for named in ("%[fd]", "%[e]", "%[hg]"):
+            e(f"v_mov_b32_e32 {named}, %[cur]")
     return out
 
 
@@ -950,6 +1010,18 @@ def main():
                             for ln in gen_aff2(kind, border, pub, lut, ts, epi, cap):
                                 lines.append(f'    "{ln}\\n" \\')
                             lines.append("")
+    # linear gap in the affine loop (one row per lane, no diagnostic-stamp variants):
+    # kinds N (G space) and M (X space: local)
+    for kind, lk in (("G", "N"), ("L", "M")):
+        for border in (0, 1):
+            for pub in ("none", "lds", "glob"):
+                for lut in (0, 1):
+                    for epi, cap, tag in ((False, True, ""), (True, True, "E"), (True, False, "F")):
+                        name = f"ANYSEQ_AF2{tag}_{lk}_B{border}_{pub.upper()}_U{lut}"
+                        lines.append(f"#define {name} \\")
+                        for ln in gen_aff2(kind, border, pub, lut, False, epi, cap, lin=True):
+                            lines.append(f'    "{ln}\\n" \\')
+                        lines.append("")
     # two and three rows per lane (no diagnostic-stamp variants)
     for nrows, pre in ((2, "AF2R"), (3, "AF2R3")):
         for kind in ("G", "L"):
