@@ -61,9 +61,10 @@ VALU_DESIGN_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
 # (profiles/r04z_pmc.json: 859.2 M per 65536^2 local score launch); G space = 9.25 +
 # the same 2.15 of block overhead.
 VALU_PER_STEP = {"linear": 6.0, "linear_local": 8.0, "affine": 11.4, "affine_local": 12.8,
-                 # linear global / local scores through the affine fill's linear loop (round 5:
-                 # gen_aff2 lin, 4.25 / 6.75 VALU per step in the loop + the block's ~1)
-                 "linear_aff": 5.25, "linear_aff_local": 7.75}
+                 # linear global / local scores through the affine fill's linear loop (round 5,
+                 # gen_aff2 lin: G space measured, SQ_INSTS_VALU per wave step of configs[1],
+                 # profiles/r05fin6_pmc.json; local: the loop's 6.75 + the block's ~1)
+                 "linear_aff": 5.18, "linear_aff_local": 7.75}
 # Affine fill with R rows per lane (round 5): VALU per 64 cells, measured
 # (SQ_INSTS_VALU / (cells / 64), configs[4]: profiles/r05fin_pmc.json for R = 2,
 # r05fin3_pmc.json for R = 3); X space (local) scaled as R = 1's 12.8 / 11.4
