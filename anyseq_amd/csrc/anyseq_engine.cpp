@@ -307,6 +307,7 @@ void init_tuning_locked() {
     g_tuning.selffwd = env_int("ANYSEQ_SELF_FWD", g_tuning.selffwd);
     g_tuning.linaff = env_int("ANYSEQ_LIN_AFF", g_tuning.linaff);
     g_tuning.linloop = env_int("ANYSEQ_LIN_LOOP", g_tuning.linloop);
+    g_tuning.iofirst = env_int("ANYSEQ_IO_FIRST", g_tuning.iofirst);
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
@@ -862,6 +863,8 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     if (g_tuning.virtbest && std::min(sc.match, sc.mismatch) >= sc.gap_open + sc.gap_extend) fp.pad |= 16;
     // bit 7: gap open 0 through the affine loop, not the linear one (A/B)
     if (!g_tuning.linloop) fp.pad |= 128;
+    // bit 8: the affine I/O wave on the first hardware wave (A/B)
+    if (g_tuning.iofirst) fp.pad |= 256;
     fp.alpha = nullptr;
     fp.io_stage = g_tuning.io_stage;
     fp.io_skew = g_tuning.io_skew;
@@ -2329,6 +2332,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_self_forward") g_tuning.selffwd = value;
     else if (n == "linear_via_affine") g_tuning.linaff = value;
     else if (n == "linear_affine_loop") g_tuning.linloop = value;
+    else if (n == "affine_io_first") g_tuning.iofirst = value;
     else if (n == "affine_grid") g_tuning.grida = value;
     else if (n == "affine_asm") g_tuning.affasm = value;
     else if (n == "ring_slots") g_tuning.ring_slots = value;

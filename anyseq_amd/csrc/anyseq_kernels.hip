@@ -2517,7 +2517,11 @@ __global__ __launch_bounds__(NW == 8 ? 512 : 64 * (NW + 1)) void fill_affine_ker
                                                                      int ngroups_total, uint32_t* dq, uint32_t* err,
                                                                      FillParams fp) {
     __shared__ __attribute__((aligned(16))) AffShared<NW> sh;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    // logical wave: compute waves 0 .. NW-1, the I/O wave NW.  FillParams::pad bit 8: the
+    // I/O wave is the workgroup's first hardware wave, so it shares its SIMD with the
+    // group's last band instead of its first (waves are dealt to the SIMDs in order)
+    const int hw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int wave = (fp.pad & 256) && NW != 8 ? (hw == 0 ? NW : hw - 1) : hw;
     AffK k;
     k.go = fp.gap_open;
     k.nge = -fp.gap_extend;
