@@ -15,6 +15,8 @@ the loop branches are cut out) and writes one macro per instruction subset:
   NOMAX3      VALU with v_max3 as v_max of its first two sources
   PLAIN       all three substitutions
   PLAIN64     PLAIN in 64-bit encodings (v_*_e64)
+  R2FULL / R2VALU, R3FULL / R3VALU   two / three rows per lane (rn_transform: the projection
+              that preceded the product's gen_aff2 nrows; its whole loop / its VALU)
 
 tools/micro/mix_micro.hip times each at one and two compute waves per SIMD.
 Diagnostic tool, not part of the product.
