@@ -103,9 +103,10 @@ void anyseq_set_tuning(int rows_per_lane, int waves_per_group, int grid);
 
 /* Named tuning option: "rows_per_lane" (1,2,4), "chunk" (16,32 steps per block),
  * "waves_per_group" (3,4,7,8), "grid", "fronts" (1 or 2: score fill as one
- * front or two meeting fronts), "affine_waves_per_group" (3,4,7), "affine_grid",
- * "ring_slots" (group hand-off rows kept per sub-problem; 0 = 4*grid+4, never
- * fewer than 2*grid+2).
+ * front or two meeting fronts), "affine_waves_per_group" (3,4,7,8),
+ * "affine_rows_per_lane" (0,1,2,3), "affine_self_forward", "linear_via_affine",
+ * "affine_grid", "ring_slots" (group hand-off rows kept per sub-problem; 0 = 4*grid+4,
+ * never fewer than 2*grid+2), and the others INTEGRATION.md lists.
  * Returns 0, or -1 for an unknown name. */
 int anyseq_set_option(const char* name, int value);
 
