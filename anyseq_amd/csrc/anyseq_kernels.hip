@@ -4659,7 +4659,8 @@ hipError_t anyseq_launch_fill_affine(int NW, const anyseq::DPProblem* probs, con
                                      int ngroups, uint32_t* dq, uint32_t* err, const anyseq::FillParams* fp, int grid,
                                      hipStream_t st) {
     using namespace anyseq;
-    // (the asm steady state holds ~150 fixed VGPRs: at most 2 waves per SIMD, NW <= 7)
+    // (the asm steady state holds ~150 fixed VGPRs: at most 2 waves per SIMD -- NW <= 7 beside
+    // the I/O wave, or NW 8 without it)
     // fp->arows 2 / 3: rows per lane (NW 4 or 7; the descriptors' nbands count 64 arows-row bands)
     // NW 8: eight compute waves, the groups' first bands forwarding their own input rows
     if (fp->arows == 2 || fp->arows == 3) {
