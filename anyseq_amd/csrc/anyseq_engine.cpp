@@ -308,6 +308,7 @@ void init_tuning_locked() {
     g_tuning.linaff = env_int("ANYSEQ_LIN_AFF", g_tuning.linaff);
     g_tuning.linloop = env_int("ANYSEQ_LIN_LOOP", g_tuning.linloop);
     g_tuning.iofirst = env_int("ANYSEQ_IO_FIRST", g_tuning.iofirst);
+    g_tuning.forcelb = env_int("ANYSEQ_FORCE_LB", g_tuning.forcelb);
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
@@ -865,6 +866,8 @@ FillParams make_params(int kind, const anyseq_scoring& sc) {
     if (!g_tuning.linloop) fp.pad |= 128;
     // bit 8: the affine I/O wave on the first hardware wave (A/B)
     if (g_tuning.iofirst) fp.pad |= 256;
+    // bit 9: a zero-open left border through the C++ blocks, not the forcing prologue (A/B)
+    if (!g_tuning.forcelb) fp.pad |= 512;
     fp.alpha = nullptr;
     fp.io_stage = g_tuning.io_stage;
     fp.io_skew = g_tuning.io_skew;
@@ -923,12 +926,10 @@ int64_t score_dev_affine(Engine& E, int kind, const anyseq_scoring& sc, const ui
 int64_t score_dev(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds, int m,
                   hipStream_t st) {
     if (n <= 0 || m <= 0) return empty_score(kind, n, m, sc);
-    // a linear global / local score runs through the affine fill with gap open 0 (round 5,
-    // DESIGN.md §3.1b): its linear loop on the affine kernel's code rows, lean blocks and
-    // half-chunk hand-off.  (Semiglobal stays: its zero-open left border has no virtual
-    // prologue, so every band would start with two C++ blocks on the chain -- 21 % slower.
-    // linear_via_affine 2 takes it too, for the tests.)
-    const bool via_aff = g_tuning.linaff == 2 || (g_tuning.linaff == 1 && kind != KIND_SEMIGLOBAL);
+    // a linear score runs through the affine fill with gap open 0 (round 5):
+    // its linear loop on the affine kernel's code rows, lean blocks and half-chunk hand-off
+    // (semiglobal with its zero-open left border forced at column -1, the `pro` prologue)
+    const bool via_aff = g_tuning.linaff != 0;
     if (sc.gap_open != 0 || via_aff) return score_dev_affine(E, kind, sc, dq, n, ds, m, st);
     const FillParams fp = make_params(kind, sc);
     const int wpad = (m + 63) & ~63;
@@ -2333,6 +2334,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "linear_via_affine") g_tuning.linaff = value;
     else if (n == "linear_affine_loop") g_tuning.linloop = value;
     else if (n == "affine_io_first") g_tuning.iofirst = value;
+    else if (n == "affine_force_border") g_tuning.forcelb = value;
     else if (n == "affine_grid") g_tuning.grida = value;
     else if (n == "affine_asm") g_tuning.affasm = value;
     else if (n == "ring_slots") g_tuning.ring_slots = value;

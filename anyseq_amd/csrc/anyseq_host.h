@@ -85,9 +85,10 @@ struct Tuning {
     int NWa = 0;     // affine fill: compute waves per workgroup (3, 4 or 7; 0 = chosen per launch)
     int arows = 0;   // affine fill: rows per lane (1, 2, 3; 0 = chosen per launch, aff_rows_for)
     int selffwd = 1; // affine fill: throughput-bound launches with 8 compute waves, no I/O wave
-    int linaff = 1;  // linear scores through the affine fill with gap open 0 (1: global / local, 2: all)
+    int linaff = 1;  // linear scores through the affine fill with gap open 0 (every kind; 0: fill_kernel)
     int linloop = 1; // ... with its linear asm loop (0: the affine loop with open 0)
     int iofirst = 0; // affine fill: the I/O wave on the workgroup's first hardware wave
+    int forcelb = 1; // affine fill: a zero-open left border forced at column -1 (virtual prologue)
     int grida = 0;   // affine fill: persistent grid (0 = one workgroup per CU)
     int affasm = 1;  // affine fill: bit 0 asm steady state; bit 1 no asm epilogue; bits 2/3 none for best-all / other;
                      // bit 5 the round-3 band end (capturing epilogue), bit 6 its start (C++ spin) (A/B; round 5:

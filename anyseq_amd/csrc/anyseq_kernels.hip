@@ -1564,10 +1564,11 @@ struct SelfFwd {
 // MASK: some lanes are outside [0, w).  PARTIAL: rows >= h pass the row above
 // through (so lane 63 publishes the last row's G and F-down).  og/of: this lane's
 // (G, F-down) after each step (lane 63's are the band's bottom row).
+// lbrd: a zero-open left border (semiglobal) forced at column -1 (VIRT; kAffNeg: none)
 template <bool MASK, bool PARTIAL, bool VIRT>
 __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&rv)[32], const uint32_t (&sw)[8], int q,
                                           bool dead, int zc, int zb, int& g, int& e, int& hg, int& fdn, int& dg,
-                                          int& best, int (&og)[32], int (&of)[32], const AffK k) {
+                                          int& best, int (&og)[32], int (&of)[32], const AffK k, int lbrd = kAffNeg) {
 #pragma unroll
     for (int u = 0; u < 32; ++u) {
         const int2 top = u == 0 ? tf : rv[u - 1];
@@ -1582,6 +1583,7 @@ __device__ __forceinline__ void aff_block(int c0, int w, int2 tf, const int2 (&r
         const int en = max(e, hg);
         int v = max(max(dg + wgt, en), fin);
         v = max(v, zc + u * k.nge);
+        if (VIRT && c0 + u == -1 && lbrd != kAffNeg) v = lbrd;
         const int hn = v + k.go;
         int fn = max(fin, hn);
         if (PARTIAL && dead) {
@@ -1647,6 +1649,19 @@ struct Aff2Args {
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
                    [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr), [sg] "s"(sg)                    \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
+// the band's first blocks with the zero-open left border forced (gen_aff2 pro)
+#define AF2P_ASM(NAME)                                                                                          \
+    asm volatile(NAME                                                                                          \
+                 : [cur] "+v"(g), [fd] "+v"(fdn), [dg] "+v"(dg), [tfg] "+v"(tfg), [tff] "+v"(tff), [e] "+v"(e),  \
+                   [hg] "+v"(hg), [best] "+v"(bx), [b] "+s"(b), [sp] "+s"(sp), [sf] "+s"(sf), [sc] "+s"(sc),     \
+                   [pf] "+s"(pf), [st] "=&s"(st), [x0] "=&s"(x0), [x1] "=&s"(x1), [x2] "=&s"(x2), [x3] "=&s"(x3), \
+                   [x4] "=&s"(x4), [pcnt] "+v"(pcnt) AF2_TS_OUT                                                \
+                 : [be] "s"(be), [q] "v"(a.q), [wm] "v"(a.wm), [wx] "v"(a.wx), [ll] "v"(a.ll), [lh] "v"(a.lh),   \
+                   [go] "v"(go), [ge] "s"(ge), [zlp] "v"(a.zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(a.apr),   \
+                   [acn] "v"(a.acn), [anp] "v"(a.anp), [anc] "v"(a.anc), [asf] "v"(a.asf), [atl] "v"(a.atl),     \
+                   [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
+                   [hm] "s"(hm), [gp] "s"(gp), [thr] "s"(thr), [sg] "s"(sg), [pbrd] "v"(pbrd)                  \
+                 : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
 // the band's last blocks without the column-(w-1) capture (gen_aff2 cap=False)
 #define AF2F_ASM(NAME)                                                                                          \
     asm volatile(NAME                                                                                          \
@@ -1660,8 +1675,10 @@ struct Aff2Args {
                    [skb] "v"(a.skb), [lo] "v"(a.lo), [lid8] "v"(a.lid8), [bvb] "v"(a.bvb), [bvs] "s"(bvs),        \
                    [hm] "s"(hm), [gp] "s"(gp), [nch] "s"(nch), [thr] "s"(thr), [neg] "s"(negp), [sg] "s"(sg)    \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
-// EPI: 0 the steady state, 1 the band's last blocks with the capture, 2 without it.
-// LIN: the linear loop (gen_aff2 lin: kinds N = G space, M = X space)
+// EPI: 0 the steady state, 1 the band's last blocks with the capture, 2 without it, 3 the
+// band's first blocks with the zero-open left border forced (cap = {steps to column -1,
+// the border in the loop's space}).  LIN: the linear loop (gen_aff2 lin: kinds N = G space,
+// M = X space)
 template <bool L, bool BORDER, int PUB, bool LUT, int EPI = 0, bool LIN = false>
 __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint32_t& sp, uint32_t& sf, uint32_t& sc,
                                                   const Aff2Args& a, int go, int nge, int& g, int& fdn, int& dg,
@@ -1725,6 +1742,19 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
         const uint32_t negp = __builtin_amdgcn_readfirstlane(a.neg);
         (void)cap;
         AF2_KINDS(AF2F_ASM, AF2F)
+    } else if constexpr (EPI == 3) {
+        (void)nch;
+        int pcnt = cap[0];
+        const int pbrd = cap[1];
+        if constexpr (!LIN && L && LUT) { AF2_SELN(AF2P_ASM, AF2P, L, 1) }
+        if constexpr (!LIN && L && !LUT) { AF2_SELN(AF2P_ASM, AF2P, L, 0) }
+        if constexpr (!LIN && !L && LUT) { AF2_SELN(AF2P_ASM, AF2P, G, 1) }
+        if constexpr (!LIN && !L && !LUT) { AF2_SELN(AF2P_ASM, AF2P, G, 0) }
+        if constexpr (LIN && L && LUT) { AF2_SELN(AF2P_ASM, AF2P, M, 1) }
+        if constexpr (LIN && L && !LUT) { AF2_SELN(AF2P_ASM, AF2P, M, 0) }
+        if constexpr (LIN && !L && LUT) { AF2_SELN(AF2P_ASM, AF2P, N, 1) }
+        if constexpr (LIN && !L && !LUT) { AF2_SELN(AF2P_ASM, AF2P, N, 0) }
+        cap[0] = pcnt;
     } else {
         (void)nch, (void)cap;
         AF2_KINDS(AF2_ASM, AF2)
@@ -1738,6 +1768,7 @@ __device__ __forceinline__ uint32_t aff2_loop_asm(uint32_t& b, uint32_t be, uint
 #undef AF2_ASM
 #undef AF2E_ASM
 #undef AF2F_ASM
+#undef AF2P_ASM
 
 // Two or three rows per lane (gen_aff2 nrows): the upper rows' state in gu / eu / hgu / bxu
 // (row 0: %[ga] / %[e] / %[hg] / %[best], row 1 of three: %[gb] / %[eb] / %[hgb] / %[bestb]),
@@ -1951,8 +1982,13 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
     // weights give it the mismatch -- a positive mismatch would lift column -1 above the
     // local left border (round 5: local scores too high with > 8 symbols and mismatch > 0)
     const bool ff_loses = k.lut || k.wx <= 2 * nge;
-    const bool virt = ASM_OK && !shard_left && !zero_open && !(bestmode == 2 && finite_left) && best_border_ok &&
-                      (!clamp || (k.codes && ff_loses)) && !(k.flags & 1);
+    // A zero-open left border (semiglobal) is forced at column -1 instead: the asm
+    // prologue variant (gen_aff2 pro) and the C++ blocks' lbrd (one row per lane; round 5)
+    // (not with a best of the last row or of every cell: the forced border cell, H = 0, would
+    // become a candidate the C++ path never offers)
+    const bool force_lb = zero_open && RR == 1 && !(k.flags & 512) && (bestmode == 0 || bestmode == 3);
+    const bool virt = ASM_OK && !shard_left && (!zero_open || force_lb) && !(bestmode == 2 && finite_left) &&
+                      best_border_ok && (!clamp || (k.codes && ff_loses)) && !(k.flags & 1);
     const int rb = band * 64 * RR;
     const int row = rb + RR * lane + (RR - 1);   // the lane's bottom row
     const int rowt = row - (RR - 1);             // its top row
@@ -2119,11 +2155,15 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
     for (int b = 0; b < nblocks; ++b) {
         const int t0 = b * CH;
         if constexpr (ASM_OK) {
-            if ((virt || t0 >= 64) && b < fe && !(k.flags & 1)) {
+            // (a forced left border needs both prologue blocks in the forcing loop: with fewer
+            // full blocks the band's first blocks stay in C++, where lbrd forces it)
+            if ((virt || t0 >= 64) && b < fe && !(k.flags & 1) && !(force_lb && b < 2 && fe < 2)) {
                 // self-forwarding: the fused end once the band's remaining chunks fit the ring,
                 // else a main-loop segment of kFwdSeg blocks
-                const bool fwd_end = !self_fwd || nblocks - b <= kFwdSeg + 1;
-                const int seg_end = self_fwd ? min(fe, b + kFwdSeg) : fe;
+                // (a zero-open left border: its first two blocks in the forcing prologue variant)
+                const bool pro = force_lb && b < 2;
+                const bool fwd_end = !pro && (!self_fwd || nblocks - b <= kFwdSeg + 1);
+                const int seg_end = pro ? min(2, fe) : self_fwd ? min(fe, b + kFwdSeg) : fe;
                 if (self_fwd && !fw.forward_to(io, lane, w, b, fwd_end ? nchunks : seg_end, err)) return;
                 // one block of slack: block b starts once chunk b+1 is published, so in the
                 // steady state the loop's poll (step 16) already sees the next chunk and
@@ -2186,7 +2226,7 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                 const bool top_safe = !io.in_border || (B.tfree ? clamp : B.tg == kAffNeg);
                 const bool best_safe = bestmode == 0 || (bestmode == 1 && ff_loses && top_safe);
                 const bool need_cap = P.out_col || P.out_col_e || P.out_f_last || !best_safe || (k.flags & 32);
-                if (epi && !need_cap && fwd_end) {
+                if (epi && !need_cap && fwd_end) {   // (never in the prologue: fwd_end is false there)
 #define AF2_CALL(LV, BD, PB, LU)                                                                                  \
     if constexpr (RR > 1)                                                                                         \
         st = aff2n_loop_asm<RR, LV, BD, PB, LU, 2>(bb, (uint32_t)nblocks, seen_prod, seen_sfill, seen_cons, la, go, \
@@ -2217,10 +2257,19 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                     }
                     break;   // band done (g / e / fdn: nobody reads them)
                 }
+                // (the forcing prologue: steps until the lane's column -1, the border there)
+                int pcap[2] = {lane - t0, xs ? to_x(B.left(row, nge), -1) : B.left(row, nge)};
 #define AF2_CALL(LV, BD, PB, LU)                                                                               \
     if constexpr (RR > 1)                                                                                      \
         st = aff2n_loop_asm<RR, LV, BD, PB, LU>(bb, (uint32_t)seg_end, seen_prod, seen_sfill, seen_cons, la, go, \
                                                 nge, g, fdn, dg, tf, e, hg, bx, gu, eu, hgu, bxu);               \
+    else if (pro && lin)                                                                                       \
+        st = aff2_loop_asm<LV, BD, PB, LU, 3, true>(bb, (uint32_t)seg_end, seen_prod, seen_sfill, seen_cons, la, go, \
+                                                    nge, g, fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u,     \
+                                                    pcap, dbp);                                                      \
+    else if (pro)                                                                                              \
+        st = aff2_loop_asm<LV, BD, PB, LU, 3>(bb, (uint32_t)seg_end, seen_prod, seen_sfill, seen_cons, la, go, nge, \
+                                              g, fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u, pcap, dbp);  \
     else if (lin)                                                                                              \
         st = aff2_loop_asm<LV, BD, PB, LU, 0, true>(bb, (uint32_t)seg_end, seen_prod, seen_sfill, seen_cons, la, go, \
                                                     nge, g, fdn, dg, tf, e, hg, bx, ts_v, te_v, ts_f, nmiss, 0u,     \
@@ -2402,13 +2451,13 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
         } else if (full) {
             if (virt)
                 aff_block<false, PARTIAL, true>(c0, w, tf, rv, sw, q, dead, zc, zb, g, e, hg, fdn,
-                                                        dg, best, og, of, k);
+                                                        dg, best, og, of, k, force_lb ? B.left(row, nge) : kAffNeg);
             else
                 aff_block<false, PARTIAL, false>(c0, w, tf, rv, sw, q, dead, zc, zb, g, e, hg, fdn,
                                                          dg, best, og, of, k);
         } else if (virt) {
             aff_block<true, PARTIAL, true>(c0, w, tf, rv, sw, q, dead, zc, zb, g, e, hg, fdn, dg,
-                                                   best, og, of, k);
+                                                   best, og, of, k, force_lb ? B.left(row, nge) : kAffNeg);
         } else {   // masked prologue / epilogue (also a shard's received border column)
             aff_block<true, PARTIAL, false>(c0, w, tf, rv, sw, q, dead, zc, zb, g, e, hg, fdn, dg,
                                                     best, og, of, k);

@@ -561,10 +561,9 @@ def score_bench(args, world, rank, local_rank):
     gcups = cells_per_step * args.steps / elapsed / 1e9
     kernel_ms = fill_ms / max(launches, 1)
     aff = bool(args.gap_open)
-    # linear global / local scores run on fill_affine_kernel's linear loop (the library's
-    # linear_via_affine 1 default), linear semiglobal and the sharded linear
-    # fills on fill_kernel
-    lin_aff = not aff and kind in ("global", "local") and not dist
+    # linear scores run on fill_affine_kernel's linear loop (the library's linear_via_affine 1
+    # default), the sharded linear fills on fill_kernel
+    lin_aff = not aff and not dist
     valu_key = ("affine" if aff else "linear_aff" if lin_aff else "linear") + ("_local" if kind == "local" else "")
     tag = f"fill_affine_kernel<{kind}> {n}x{m}" if aff or lin_aff else f"fill_kernel<{kind}> {n}x{m}"
 

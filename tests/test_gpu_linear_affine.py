@@ -1,6 +1,6 @@
 """GPU parity of LINEAR scores through the affine fill (round 5): with
-`linear_via_affine` (default 1: global and local; 2, here: every kind) a linear-gap score
-(gap open 0) runs on fill_affine_kernel -- its code
+`linear_via_affine` (default 1) a linear-gap score of every kind (gap open 0) runs on
+fill_affine_kernel -- its code
 rows, lean blocks, half-chunk hand-offs and, with `linear_affine_loop` (default), the linear
 asm loop (gen_aff2 lin: one DPP and one shift move per step; X space for local) -- against
 the reference-semantics linear oracle (oracle.score), bit-exact: every kind, shapes around
@@ -22,7 +22,7 @@ def rnd(rng, n, alphabet="ACGT"):
 
 @pytest.fixture(params=[1, 0], ids=["linear-loop", "affine-loop"])
 def linaff(anyseq, request):
-    anyseq.set_option("linear_via_affine", 2)   # (every kind; the default 1 keeps semiglobal linear)
+    anyseq.set_option("linear_via_affine", 1)
     anyseq.set_option("linear_affine_loop", request.param)
     try:
         yield request.param
@@ -88,3 +88,22 @@ def test_linear_kernel_still_covered(anyseq, oracle):
                 assert anyseq.score(kind, q, s) == oracle.score(kind, q, s), (kind, n, m)
     finally:
         anyseq.set_option("linear_via_affine", 1)
+
+
+@pytest.mark.parametrize("force", [1, 0])
+def test_semiglobal_zero_open_border(anyseq, oracle, force):
+    """The zero-open left border of semiglobal fills (round 5): forced at column -1 in the
+    virtual prologue (`affine_force_border` 1, the asm `pro` loop and the C++ blocks' lbrd)
+    or, with 0, the masked C++ prologue as before -- affine and linear scores, one- and
+    multi-group bands, bands with fewer than two full blocks (the prologue stays in C++)."""
+    rng = random.Random(65)
+    anyseq.set_option("affine_force_border", force)
+    try:
+        for n, m in [(230, 50), (700, 31), (64, 64), (3000, 2500), (9000, 300), (129, 1000)]:
+            q, s = rnd(rng, n), rnd(rng, m)
+            for sc in [(2, -1, -2, -1), (1, -3, -5, -2), (3, 1, -2, -1)]:
+                got = anyseq.score("semiglobal", q, s, match=sc[0], mismatch=sc[1], gap_open=sc[2], gap_extend=sc[3])
+                assert got == oracle.affine_score("semiglobal", q, s, *sc), (n, m, sc)
+            assert anyseq.score("semiglobal", q, s) == oracle.score("semiglobal", q, s), (n, m)
+    finally:
+        anyseq.set_option("affine_force_border", 1)

@@ -366,7 +366,7 @@ def OFB_(u):
     return OFk_(1, u)
 
 
-def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin=False):
+def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin=False, pro=False):
     """Affine steady-state loop, round 3: full blocks b .. be-1.
     kind G: G space (X_G = X + (r+c+2)|ge|), no clamp, no best (amode 0).
     kind L: X space (X = H + (r+2)|ge|, a per-ROW shift): the local clamp H >= 0 is
@@ -415,10 +415,19 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin
     X_up) with zl' = %[zlp] = the clamp bound + |ge|.  One DPP and one shift-register move
     per step; the published pairs carry (G, G) (F-down = G), and at loop exit %[fd], %[e]
     and %[hg] get the last cell (the C++ blocks' affine step with open 0 then continues
-    exactly: E and F of the next cell are the left and upper cells)."""
+    exactly: E and F of the next cell are the left and upper cells).
+    pro (round 5): the band's first blocks with a zero-open left border (semiglobal), which
+    the virtual prologue cannot reproduce: the lane's cell at column -1 (after %[pcnt]
+    steps) is forced to the border %[pbrd] right after its max3, before anything reads it."""
     L = kind == "L"
     r2 = nrows > 1
-    assert not (lin and r2)
+    assert not (lin and r2) and not (pro and (r2 or epi))
+
+    def force(u):
+        if pro:
+            e("v_cmp_eq_u32_e32 vcc, 0, %[pcnt]")
+            e(f"v_cndmask_b32_e32 {OG_(u)}, {OG_(u)}, %[pbrd], vcc")
+            e("v_add_u32_e32 %[pcnt], -1, %[pcnt]")
     last = nrows - 1
     assert not r2 or (REORDER and LEAN and SLIM and GS and not ts)
     OGP, OFP = (lambda u: OGk_(last, u)), (lambda u: OFk_(last, u))   # the published / lane-shifted cells
@@ -743,6 +752,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin
                     e(f"s_nop {1 - nv}")
                 e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_max3_i32 {OG_(u)}, v{B_AA}, {'v' + str(B_AT) if L else g}, {tg}")
+                force(u)
                 if L and u % 2 == 1 and not (epi and cap):
                     e(f"v_max3_i32 %[best], %[best], {OG_(u - 1)}, {OG_(u)}")
                 if sr:
@@ -772,6 +782,7 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin
                     e("v_add_u32_e32 %[e], %[ge], %[e]")
                 e(f"v_mov_b32_dpp {tg}, {g} wave_shr:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_max3_i32 {OG_(u)}, v{B_AA}, %[e], {tf}")
+                force(u)
                 if sr and not r2:
                     e(f"v_mov_b32_dpp {OF_(u - 1)}, {OF_(u - 2)} wave_shl:1 row_mask:0xf bank_mask:0xf")
                 e(f"v_add_u32_e32 %[hg], %[go], {OG_(u)}")
@@ -1010,6 +1021,16 @@ def main():
                             for ln in gen_aff2(kind, border, pub, lut, ts, epi, cap):
                                 lines.append(f'    "{ln}\\n" \\')
                             lines.append("")
+    # zero-open left border prologue (one row per lane, affine G / L and linear N / M kinds)
+    for kind, lk, lin in (("G", "G", False), ("L", "L", False), ("G", "N", True), ("L", "M", True)):
+        for border in (0, 1):
+            for pub in ("none", "lds", "glob"):
+                for lut in (0, 1):
+                    name = f"ANYSEQ_AF2P_{lk}_B{border}_{pub.upper()}_U{lut}"
+                    lines.append(f"#define {name} \\")
+                    for ln in gen_aff2(kind, border, pub, lut, False, False, True, lin=lin, pro=True):
+                        lines.append(f'    "{ln}\\n" \\')
+                    lines.append("")
     # linear gap in the affine loop (one row per lane, no diagnostic-stamp variants):
     # kinds N (G space) and M (X space: local)
     for kind, lk in (("G", "N"), ("L", "M")):
