@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 5 final evidence (round-5 final build) on one fresh box, for the committed build: the whole GPU suite
+# with test ids and the in-tree libraries it loaded, smoke, the profile set (bench lines,
+# kernel traces, PMC passes: tools/profile.sh), configs[3] and configs[4] at N=1.
+set -o pipefail
+O=gpurun_out/r05fin8; mkdir -p $O   # (rerun: the final build)
+ANYSEQ_MAPS_OUT=$O/loaded_libs.txt timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rA --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || exit 1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); import sys; sys.path.insert(0, 'tests'); import conftest; [print('loaded', r, d) for r, d in conftest.loaded_libraries()]" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 1500 bash tools/profile.sh r05fin8 > $O/profile.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --config 3 --steps 1 --warmup 1 --no-cpu-baseline > $O/c3.json 2> $O/c3.err || exit 1
+timeout -k 10 300 python -u bench.py --config 4 --steps 1 --warmup 1 --no-cpu-baseline > $O/c4.json 2> $O/c4.err || exit 1
+tail -2 $O/pytest.log; cat $O/loaded_libs.txt; tail -3 $O/smoke.log
