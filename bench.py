@@ -588,7 +588,7 @@ def score_bench(args, world, rank, local_rank):
                        "parallelism": parallelism, "score": int(score),
                        "fill_launches_per_step": launches // max(args.steps, 1),
                        "fill_multi_row_launches_per_step": multi_row // max(args.steps, 1),
-                   "fill_rows_per_lane_max": rows_max,
+                       "fill_rows_per_lane_max": rows_max,
                        "transport": ("RCCL send/recv (host-polled chunk trigger), unmeasured on hardware "
                                      "(no multi-GPU run before this one)" if world > 1 else None)},
             "roofline": roofline("fill_affine_kernel" if aff or lin_aff else "fill_kernel", cells_per_launch,
