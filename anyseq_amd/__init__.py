@@ -79,6 +79,10 @@ _lib.anyseq_construct_local_sharded.argtypes = [_c_int, ctypes.POINTER(Scoring),
 _lib.anyseq_shard_construct.restype = _c_int
 _lib.anyseq_shard_construct.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _vp, _vp,
                                         ctypes.POINTER(_c_i64)]
+HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(_c_int, _vp, _c_i64, _c_int, _c_int, _vp)
+_lib.anyseq_shard_construct_hostcoll.restype = _c_int
+_lib.anyseq_shard_construct_hostcoll.argtypes = [_c_int, ctypes.POINTER(Scoring), _c_p, _c_int, _c_p, _c_int, _c_int,
+                                                 _c_int, HOST_ALLREDUCE_FN, _vp, _vp, _vp, ctypes.POINTER(_c_i64)]
 _lib.anyseq_shard_unique_ids.restype = _c_int
 _lib.anyseq_shard_unique_ids.argtypes = [_vp, _c_int]
 _lib.anyseq_shard_init.restype = _c_int

@@ -321,6 +321,7 @@ void init_tuning_locked() {
     g_tuning.devplan = env_int("ANYSEQ_AFF_DEVPLAN", g_tuning.devplan);
     g_tuning.devfinal = env_int("ANYSEQ_AFF_DEVFINAL", g_tuning.devfinal);
     g_tuning.xcdq = env_int("ANYSEQ_XCD_GROUPS", g_tuning.xcdq);
+    g_tuning.ctrue = env_int("ANYSEQ_CONSTRUCT_TRUE", g_tuning.ctrue);
     g_tuning_init = true;
 }
 
@@ -1714,15 +1715,15 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             const uint32_t* c = h_tail + 9 * nlev + 8 * li;
             if (c[0])
                 fail("hand-off row invariant broken after planned level %d: %u non-sentinel word(s), the first at "
-                     "word %u = half %d, ring slot %d, column %d (half width %d)", li + 1, c[0], c[1], (int)c[2],
+                     "word %u = half %d, ring slot %d, column %d (half width %d)", lev0 + li + 1, c[0], c[1], (int)c[2],
                      (int)c[3], (int)c[4], (int)c[5]);
         }
         for (int li = 0; li < nlev; ++li) {
             const uint32_t err = h_tail[8 * nlev + li];
             g_stage_level = lev0 + li + 1;
-            if (err & ERR_BAD_DESC) fail("fill kernel read a corrupt problem descriptor (error %u; planned level %d)", err, li + 1);
-            if (err) fail("fill kernel reported error %u (spin timeout; planned level %d)", err, li + 1);
-            if (h_tail[8 * li + 1]) fail("internal: planned level %d: a half exceeds its group slots", li + 1);
+            if (err & ERR_BAD_DESC) fail("fill kernel read a corrupt problem descriptor (error %u; planned level %d)", err, lev0 + li + 1);
+            if (err) fail("fill kernel reported error %u (spin timeout; planned level %d)", err, lev0 + li + 1);
+            if (h_tail[8 * li + 1]) fail("internal: planned level %d: a half exceeds its group slots", lev0 + li + 1);
             float ms = 0.f;
             if (timed) HIPCHECK(hipEventElapsedTime(&ms, E.pl_ev[2 * li], E.pl_ev[2 * li + 1]));
             g_fill_ms += ms;
@@ -2250,13 +2251,23 @@ int anyseq_score_device(int kind, const anyseq_scoring* sc, const uint8_t* d_que
     }
 }
 
+// The extended API's construct: the build-defined true global / semiglobal / local
+// construct for affine gaps, and for linear gaps under construct_mode 1 (the affine
+// construct with gap open 0); else the reference's compat construct.
+static bool true_construct(const anyseq_scoring& s) {
+    if (s.gap_open != 0) return true;
+    std::lock_guard<std::mutex> lk(g_engines_mu);
+    init_tuning_locked();
+    return g_tuning.ctrue != 0;
+}
+
 int anyseq_construct(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject, int lens,
                      char* alQuery, char* alSubject, int64_t* score) {
     try {
         const anyseq_scoring s = sc ? *sc : kAbiScoring;
         check_scoring(kind, s);
         check_value_range(s, lenq, lens);
-        if (s.gap_open != 0) {   // build-defined affine construct (true global / semiglobal / local)
+        if (true_construct(s)) {   // build-defined affine construct (true global / semiglobal / local)
             const int64_t v = construct_affine_host(kind, s, query, lenq, subject, lens, alQuery, alSubject);
             if (score) *score = v;
             return 0;
@@ -2285,7 +2296,7 @@ int anyseq_construct_device(int kind, const anyseq_scoring* sc, const uint8_t* d
         ExternRanges xr({{d_query, (size_t)std::max(lenq, 0)}, {d_subject, (size_t)std::max(lens, 0)},
                          {d_alQuery, L}, {d_alSubject, L}});
         int64_t v;
-        if (s.gap_open != 0) {
+        if (true_construct(s)) {
             v = construct_affine_dev(E, kind, s, d_query, lenq, d_subject, lens, d_alQuery, d_alSubject, st);
         } else {
             construct_dev(E, kind, s, d_query, lenq, d_subject, lens, d_alQuery, d_alSubject, st);
@@ -2353,6 +2364,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "affine_device_final") g_tuning.devfinal = value;
     else if (n == "plan_hw_queues") g_tuning.plan_queues = value;
     else if (n == "xcd_groups") g_tuning.xcdq = value;
+    else if (n == "construct_mode") g_tuning.ctrue = value;
     else return -1;
     return 0;
 }

@@ -112,7 +112,17 @@ struct Tuning {
     int devfinal = 1;    // affine construct, device-planned: the final level's blocks built on the device too
     int virtbest = 1;    // affine fill: virtual prologue for NORMAL-border best-of-every-cell problems when safe
     int plan_queues = 0; // sharded construct plan: hardware queues to plan for (0 = the process's, below)
-    int xcdq = 0;        // affine fill: XCD-local groups on whole-chip launches (FillParams::xq)
+    // affine fill: XCD-local groups on whole-chip launches (FillParams::xq).  Diagnostic
+    // only, never a default: a worker takes from another XCD's queue only when its own is
+    // empty, so an XCD with no resident workgroup (CUs held by another stream's kernels)
+    // leaves its queue's groups undequeued and their successors spin to the timeout.
+    int xcdq = 0;
+    // extended API (anyseq_construct / anyseq_construct_device) with gap open 0: 0 = the
+    // reference's compat construct (align.impala:292-311, per-block walk to the first
+    // PRED_NONE), 1 = the true optimal alignment from the affine construct with open 0,
+    // which is the linear recurrence.  The six import.h symbols
+    // always keep the compat semantics.
+    int ctrue = 0;
 };
 extern Tuning g_tuning;
 

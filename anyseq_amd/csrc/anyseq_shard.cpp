@@ -1182,6 +1182,39 @@ int anyseq_shard_construct(int kind, const anyseq_scoring* sc, const char* query
     }
 }
 
+int anyseq_shard_construct_hostcoll(int kind, const anyseq_scoring* sc, const char* query, int lenq,
+                                    const char* subject, int lens, int rank, int world,
+                                    anyseq_host_allreduce_fn reduce, void* user, char* alQuery, char* alSubject,
+                                    int64_t* score) {
+    try {
+        if (world < 2 || rank < 0 || rank >= world) fail("host-collective construct: rank %d of world %d", rank, world);
+        if (!reduce) fail("host-collective construct: no reduce callback");
+        // each reduction: the stream drained, the device buffer down, the ranks' host
+        // all-reduce, the result back up -- the RCCL branch's data flow, host transport
+        auto red = [reduce, user](void* p, size_t count, size_t esz, int dtype, int op, hipStream_t st) {
+            std::vector<uint8_t> h(std::max<size_t>(count * esz, 1));
+            HIPCHECK(hipMemcpyAsync(h.data(), p, count * esz, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            if (reduce(h.data(), (int64_t)count, dtype, op, user) != 0) fail("host all-reduce callback failed");
+            HIPCHECK(hipMemcpyAsync(p, h.data(), count * esz, hipMemcpyHostToDevice, st));
+            HIPCHECK(hipStreamSynchronize(st));
+        };
+        ConstructShards cs;
+        cs.rank = rank;
+        cs.world = world;
+        cs.sum_i32 = [red](int32_t* p, size_t n, hipStream_t st) { red(p, n, 4, 0, 0, st); };
+        cs.max_i32 = [red](int32_t* p, size_t n, hipStream_t st) { red(p, n, 4, 0, 1, st); };
+        cs.max_u8 = [red](uint8_t* p, size_t n, hipStream_t st) { red(p, n, 1, 1, 1, st); };
+        const int64_t v = sharded_construct(kind, sc ? *sc : anyseq_scoring{2, -1, -2, -1}, query, lenq, subject,
+                                            lens, alQuery, alSubject, cs);
+        if (score) *score = v;
+        return 0;
+    } catch (const Failure& f) {
+        set_last_error(f.msg);
+        return -1;
+    }
+}
+
 int anyseq_shard_score_local(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
                              int lens, int nshards, int64_t* score) {
     try {

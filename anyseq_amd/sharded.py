@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import ctypes
 
-from . import AnySeqError, _b, _err, _kind, _lib, _scoring, main_random_pair
+from . import HOST_ALLREDUCE_FN, AnySeqError, _b, _err, _kind, _lib, _scoring, main_random_pair
 from . import shard_plan
 
 _ID_BYTES = 128
@@ -61,6 +61,43 @@ def construct(kind, query, subject, match=2, mismatch=-1, gap_open=-2, gap_exten
     sc = _scoring(match, mismatch, gap_open, gap_extend)
     if _lib.anyseq_shard_construct(_kind(kind), ctypes.byref(sc), q, len(q), s, len(s), aq, as_,
                                    ctypes.byref(out)) != 0:
+        raise AnySeqError(_err())
+    return out.value, aq.raw[:L], as_.raw[:L]
+
+
+def construct_hostcoll(dist, rank: int, world: int, kind, query, subject, match=2, mismatch=-1, gap_open=-2,
+                       gap_extend=-1):
+    """The one-rank-per-process sharded construct (rank >= 0: this process fills only its
+    own halves and final blocks) with the level reductions over `dist` (torch.distributed,
+    gloo is enough) on host copies instead of RCCL (anyseq_shard_construct_hostcoll).
+    Several ranks may share one device: the 1-GPU test of the plan RCCL runs per GPU."""
+    import numpy as np
+    import torch
+
+    def reduce(buf, count, dtype, op, _user):
+        try:
+            n = int(count)
+            if dtype == 0:
+                a = np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(ctypes.c_int32)), shape=(n,))
+                t = torch.from_numpy(a.copy())
+            else:
+                a = np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(ctypes.c_uint8)), shape=(n,))
+                t = torch.from_numpy(a.astype(np.int32))
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
+            a[:] = t.numpy().astype(a.dtype)
+            return 0
+        except Exception:   # (a C callback must not raise)
+            return 1
+
+    cb = HOST_ALLREDUCE_FN(reduce)
+    q, s = _b(query), _b(subject)
+    L = len(q) + len(s)
+    aq = ctypes.create_string_buffer(max(L, 1))
+    as_ = ctypes.create_string_buffer(max(L, 1))
+    out = ctypes.c_int64(0)
+    sc = _scoring(match, mismatch, gap_open, gap_extend)
+    if _lib.anyseq_shard_construct_hostcoll(_kind(kind), ctypes.byref(sc), q, len(q), s, len(s), int(rank),
+                                            int(world), cb, None, aq, as_, ctypes.byref(out)) != 0:
         raise AnySeqError(_err())
     return out.value, aq.raw[:L], as_.raw[:L]
 

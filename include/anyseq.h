@@ -168,6 +168,19 @@ int anyseq_construct_local_sharded(int kind, const anyseq_scoring* sc, const cha
                                    int64_t* score);
 int anyseq_shard_score_local(int kind, const anyseq_scoring* sc, const char* query, int lenq, const char* subject,
                              int lens, int nshards, int64_t* score);
+/* The one-rank-per-process plan of anyseq_shard_construct (this process is `rank` of
+ * `world`: it fills only its own halves and final blocks), with the level reductions
+ * through a host callback instead of RCCL: `reduce(buf, count, dtype, op, user)` must
+ * all-reduce `count` elements of the host buffer in place over the ranks (dtype 0 int32,
+ * 1 uint8; op 0 SUM, 1 MAX) and return 0.  No column-blocked levels (they need the
+ * send/recv transport): every level is dealt round-robin.  Test transport: it runs the
+ * rank >= 0 branch of the sharded construct (several processes may share one device,
+ * which RCCL refuses) against the single-GPU construct. */
+typedef int (*anyseq_host_allreduce_fn)(void* buf, int64_t count, int dtype, int op, void* user);
+int anyseq_shard_construct_hostcoll(int kind, const anyseq_scoring* sc, const char* query, int lenq,
+                                    const char* subject, int lens, int rank, int world,
+                                    anyseq_host_allreduce_fn reduce, void* user, char* alQuery, char* alSubject,
+                                    int64_t* score);
 
 /* ---- alignment-output adapters (host only) ----
  * The sparse i+j+1 layout of construct_* / anyseq_construct (len = lenq+lens):

@@ -14,7 +14,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "liboracle.so")
+# ORACLE_LIB: another build of the same restatement (tests/test_oracle_asan.py: the sanitizer build)
+_LIB = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 
 GLOBAL, SEMIGLOBAL, LOCAL = 0, 1, 2
 KINDS = {"global": GLOBAL, "semiglobal": SEMIGLOBAL, "local": LOCAL}

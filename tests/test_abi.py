@@ -16,6 +16,7 @@ LIB = os.path.join(ROOT, "anyseq_amd", "libanyseq.so")
 def declared_functions():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    txt = re.sub(r"typedef[^;{]*\([^;]*;", "", txt)   # function-pointer typedefs declare no symbol
     return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", txt)) - {"if", "sizeof"})
 
 

@@ -1,0 +1,112 @@
+"""GPU parity of the linear TRUE local / semiglobal / global traceback (round 6, verdict
+round 5 item 5; SURVEY §7 "hard parts", §8(f) rank 4).
+
+The reference's linear construct_* is the compat traceback: a per-128-column-block walk to
+the first PRED_NONE (align.impala:292-311, traceback.impala:47-80), not an optimal local
+alignment.  With `construct_mode` 1 the extended API (anyseq_construct /
+anyseq_construct_device) sends gap open 0 to the affine construct, whose
+recurrence with open 0 is the linear one (§3.1b): the result must equal
+oracle.affine_construct(..., gap_open=0) bit for bit (score and both sparse strings), the
+score the textbook linear DP's, and the strings must re-score to it.  The compat path
+(mode 0, and the six import.h symbols in every mode) is unchanged."""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ("global", "semiglobal", "local")
+# shapes >= 65 columns, the m <= 128 edge (no Hirschberg level) and one-block parts
+SHAPES = [(65, 65), (100, 70), (64, 128), (128, 129), (200, 127), (257, 300), (300, 1000), (1000, 257),
+          (1, 300), (300, 1), (513, 4000), (3000, 2500)]
+
+
+def rnd(rng, n, alphabet="ACGT"):
+    return "".join(rng.choice(alphabet) for _ in range(n))
+
+
+def linear_rescore(aq, as_, match, mismatch, gap):
+    """Score of a sparse i+j+1 alignment under the linear scheme."""
+    v = 0
+    for a, b in zip(aq, as_):
+        if a == 0x20 and b == 0x20:
+            continue
+        if a == ord("_") or b == ord("_"):
+            v += gap
+        else:
+            v += match if a == b else mismatch
+    return v
+
+
+@pytest.fixture
+def true_mode(anyseq):
+    anyseq.set_option("construct_mode", 1)
+    try:
+        yield
+    finally:
+        anyseq.set_option("construct_mode", 0)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_linear_true_construct_matches_oracle(anyseq, oracle, true_mode, kind):
+    rng = random.Random(606)
+    for n, m in SHAPES:
+        q, s = rnd(rng, n).encode(), rnd(rng, m).encode()
+        for sc in ((2, -1, -1), (1, -3, -2)):
+            got = anyseq.construct(kind, q, s, match=sc[0], mismatch=sc[1], gap_open=0, gap_extend=sc[2])
+            exp = oracle.affine_construct(kind, q, s, sc[0], sc[1], 0, sc[2])
+            assert got == exp, (kind, n, m, sc)
+            assert got[0] == oracle.textbook_score(kind, q, s, *sc), (kind, n, m, sc)
+            if got[0] > 0 or kind == "global":
+                assert linear_rescore(got[1], got[2], *sc) == got[0], (kind, n, m, sc)
+
+
+def test_linear_true_construct_device_api(anyseq, oracle, true_mode):
+    import torch
+    rng = random.Random(607)
+    dev = torch.device("cuda", 0)
+    for kind in KINDS:
+        n, m = 1500, 2200
+        q, s = rnd(rng, n).encode(), rnd(rng, m).encode()
+        dq = torch.frombuffer(bytearray(q), dtype=torch.uint8).to(dev)
+        ds = torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev)
+        aq = torch.empty(n + m, dtype=torch.uint8, device=dev)
+        as_ = torch.empty(n + m, dtype=torch.uint8, device=dev)
+        v = anyseq.construct_device(kind, dq.data_ptr(), n, ds.data_ptr(), m, aq.data_ptr(), as_.data_ptr(),
+                                    gap_open=0, gap_extend=-1)
+        exp = oracle.affine_construct(kind, q, s, 2, -1, 0, -1)
+        assert (v, aq.cpu().numpy().tobytes(), as_.cpu().numpy().tobytes()) == exp, kind
+
+
+def test_linear_true_local_differs_from_compat(anyseq, oracle):
+    """A pair where the compat local walk stops early: the two modes must disagree, each
+    equal to its own oracle (so the mode switch really routes the call)."""
+    rng = random.Random(608)
+    q = (rnd(rng, 300) + "ACGTACGTAC" * 30 + rnd(rng, 300)).encode()
+    s = (rnd(rng, 200) + "ACGTACGTAC" * 30 + rnd(rng, 400)).encode()
+    anyseq.set_option("construct_mode", 0)
+    compat = anyseq.construct("local", q, s, gap_open=0, gap_extend=-1)
+    assert compat[1:] == oracle.construct("local", q, s)[1:]
+    anyseq.set_option("construct_mode", 1)
+    try:
+        true = anyseq.construct("local", q, s, gap_open=0, gap_extend=-1)
+    finally:
+        anyseq.set_option("construct_mode", 0)
+    assert true == oracle.affine_construct("local", q, s, 2, -1, 0, -1)
+    assert true[0] == oracle.textbook_score("local", q, s)
+    # the ABI symbol keeps the compat semantics in every mode
+    anyseq.set_option("construct_mode", 1)
+    try:
+        abi = anyseq.construct_local_alignment(q, s)
+    finally:
+        anyseq.set_option("construct_mode", 0)
+    assert abi == oracle.construct("local", q, s)
+
+
+def test_linear_true_construct_config2_shape(anyseq, oracle, true_mode):
+    """configs[2]'s inputs under the linear scheme at a 16384 x 16384 prefix (the oracle
+    finishes in seconds): local, bit-exact."""
+    Q, S = anyseq.main_random_pair(65536, 65536)
+    q, s = Q[:16384], S[:16384]
+    got = anyseq.construct("local", q, s, gap_open=0, gap_extend=-1)
+    assert got == oracle.affine_construct("local", q, s, 2, -1, 0, -1)

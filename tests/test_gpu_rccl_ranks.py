@@ -1,11 +1,16 @@
-"""Multi-process GPU test of the RCCL transport (advisor round 1).
+"""Multi-process GPU test of the RCCL transport (advisor round 1, verdict
+round 5 item 1).
 
-Two ranks, one process per GPU, launched with torch.distributed.run as a child
-process: the sharded score (linear and affine, all three kinds) and the sharded
-affine construct must equal the single-GPU path bit for bit (tools/rccl_ranks.py).
-RCCL refuses two ranks on one device, so the test needs >= 2 GPUs and skips on
-the 1-GPU box; in-process virtual ranks cover the same plans there
-(test_gpu_shard*.py)."""
+World 2, 4 and 8 (capped at the node's GPU count), one process per GPU, launched with
+torch.distributed.run as a child process: the sharded score (linear and affine, all three
+kinds) and the sharded affine construct must equal the single-GPU path bit for bit
+(tools/rccl_ranks.py), every construct's plan is asserted (level 1 column-blocked when the
+query gives every rank a column; levels 2 and 3 too at world >= 4 / 8), and the largest
+world also runs the configs[2] fixture (score and SHA-256 of both strings, with exactly the
+expected number of column-blocked levels: 1 / 2 / 3).  RCCL refuses two ranks on one
+device, so every case needs >= world GPUs and skips otherwise; on one GPU the same plans
+run as in-process virtual ranks (test_gpu_shard*.py) and the rank >= 0 branch over host
+reductions (test_gpu_shard_hostcoll.py)."""
 import os
 import subprocess
 import sys
@@ -14,6 +19,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORLDS = (2, 4, 8)
 
 
 def _gpus():
@@ -21,10 +27,16 @@ def _gpus():
     return torch.cuda.device_count()
 
 
-@pytest.mark.skipif(_gpus() < 2, reason="RCCL needs one device per rank (Duplicate GPU detected on one device)")
-def test_rccl_two_ranks_match_single_gpu():
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29537", os.path.join(ROOT, "tools", "rccl_ranks.py")]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+@pytest.mark.parametrize("world", WORLDS)
+def test_rccl_ranks_match_single_gpu(world):
+    ngpu = _gpus()
+    if ngpu < world:
+        pytest.skip(f"RCCL needs one device per rank ({ngpu} GPU(s), world {world})")
+    largest = max(w for w in WORLDS if w <= ngpu)
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", RCCL_FIXTURE="1" if world == largest else "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(29537 + world),
+           os.path.join(ROOT, "tools", "rccl_ranks.py")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=110 + 30 * world + (60 if world == largest else 0))
     assert r.returncode == 0 and "ALL_MATCH" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

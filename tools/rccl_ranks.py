@@ -35,6 +35,15 @@ CONSTRUCT_CASES = [("semiglobal", 8000, 16384), ("local", 8000, 16500), ("local"
                    ("semiglobal", 16384, 16384), ("global", 12000, 9000), ("local", 100, 120)]
 
 
+def expected_blocked_levels(world: int, nb: int) -> int:
+    """Leading column-blocked levels of a construct with nb 128-column blocks: P = 1, 2, 4 ..
+    parts while 2P <= world and P < nb (shard_plan.blocked_level; rows to spare)."""
+    k, P = 0, 1
+    while 2 * P <= world and P < nb:
+        k, P = k + 1, 2 * P
+    return k
+
+
 def main():
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     sys.path.insert(0, ROOT)
@@ -46,6 +55,9 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    if torch.cuda.device_count() < world:
+        raise SystemExit(f"rccl_ranks: {world} ranks need {world} GPUs (RCCL refuses two ranks on one device)")
     A.set_device(local_rank)
     n, m = int(os.environ.get("PROBE_N", "8192")), int(os.environ.get("PROBE_M", "16384"))
     L = max(n, m, max(c[1] for c in CONSTRUCT_CASES), max(c[2] for c in CONSTRUCT_CASES))
@@ -76,6 +88,9 @@ def main():
         exp = ref_c[c]
         good = got[0] == exp[0] and got[1] == exp[1] and got[2] == exp[2]
         plan_ok = (plan >= 1) == level1_blocked(cn, cm, world)
+        if level1_blocked(cn, cm, world) and min(cn, cm) >= 8 * world:
+            # (levels 2 / 3 too at world >= 4 / 8, when their parts keep a column per rank)
+            plan_ok &= plan >= min(expected_blocked_levels(world, (cm + 127) // 128), 2 if world >= 4 else 1)
         ok &= good and plan_ok
         if rank == 0:
             print(json.dumps({"op": "construct", "kind": k, "n": cn, "m": cm, "gap_open": -2, "world": world,
@@ -92,11 +107,15 @@ def main():
         plan = A.last_shard_plan()
         dt = time.time() - t
         h = [hashlib.sha256(x).hexdigest() for x in got[1:]]
-        good = got[0] == fx["score"] and h[0] == fx["sha_alq"] and h[1] == fx["sha_als"] and plan >= 1
+        # every level with 2P <= world is column-blocked at 65536^2 (512 blocks): 1 at two
+        # ranks, 2 at four, 3 at eight (verdict round 5, item 1)
+        want = expected_blocked_levels(world, (len(Sf) + 127) // 128)
+        good = got[0] == fx["score"] and h[0] == fx["sha_alq"] and h[1] == fx["sha_als"] and plan == want
         ok &= good
         if rank == 0:
             print(json.dumps({"op": "fixture", "name": "config2_65536", "world": world, "score": got[0],
-                              "match": good, "blocked_levels": plan, "s": round(dt, 4)}), flush=True)
+                              "match": good, "blocked_levels": plan, "want_blocked": want, "s": round(dt, 4)}),
+                  flush=True)
     dist.barrier()
     sharded.finalize()
     dist.destroy_process_group()
