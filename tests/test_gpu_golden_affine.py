@@ -72,3 +72,9 @@ def test_config3_genome_length_construct(anyseq):
         assert len(res) > 0.9 * len(seq) and seq.find(res) >= 0
     assert anyseq.score("semiglobal", q, s, gap_open=-2, gap_extend=-1) == v
     assert anyseq.shard_score_local("semiglobal", q, s, 2, gap_open=-2, gap_extend=-1) == v
+    # the bench gate's anchor (tests/golden/config4_synthetic.json, round 6): same score
+    # and, for the construct, the same strings as the single-GPU run that wrote it
+    g = json.load(open(os.path.join(GOLD, "config4_synthetic.json")))
+    assert (g["lq"], g["ls"], g["sha_q"], g["sha_s"]) == (len(q), len(s), sha(q), sha(s))
+    assert v == g["score"] == g["construct_score"]
+    assert (sha(aq), sha(as_)) == (g["construct_sha_alq"], g["construct_sha_als"])
