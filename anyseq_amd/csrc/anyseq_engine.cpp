@@ -312,6 +312,7 @@ void init_tuning_locked() {
     g_tuning.grida = env_int("ANYSEQ_GRIDA", g_tuning.grida);
     g_tuning.afflut = env_int("ANYSEQ_AFFINE_LUT", g_tuning.afflut);
     g_tuning.slack = env_int("ANYSEQ_SLACK", g_tuning.slack);
+    g_tuning.slack_io = env_int("ANYSEQ_SLACK_IO", g_tuning.slack_io);
     g_tuning.io_stage = env_int("ANYSEQ_IO_STAGE", g_tuning.io_stage);
     g_tuning.io_skew = env_int("ANYSEQ_IO_SKEW", g_tuning.io_skew);
     g_tuning.io_poll2 = env_int("ANYSEQ_IO_POLL2", g_tuning.io_poll2);
@@ -621,6 +622,7 @@ void fill_prepare(Engine& E, FillCtx& C, std::vector<DPProblem>& probs, const Fi
     fpl.prio = fill_prio(aff);
     fpl.throttle = g_tuning.thr;
     fpl.slack = g_tuning.slack;
+    fpl.slack_io = g_tuning.slack_io;
     unsigned long long* dbg = nullptr;
     static DevBuf stamp_buf;
     if (getenv("ANYSEQ_STAMPS")) {
@@ -1588,6 +1590,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             fpl.prio = fill_prio(true);
             fpl.throttle = g_tuning.thr;
             fpl.slack = g_tuning.slack;
+            fpl.slack_io = g_tuning.slack_io;
             fpl.dbg = nullptr;
             fpl.xq = A.xrun > 0 ? A.xq : nullptr;
             // the level's subject-code rows, from the descriptors its plan just wrote
@@ -2354,6 +2357,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "throttle") g_tuning.thr = value;
     else if (n == "affine_lut") g_tuning.afflut = value;
     else if (n == "slack") g_tuning.slack = value;
+    else if (n == "slack_io") g_tuning.slack_io = value;
     else if (n == "io_stage") g_tuning.io_stage = value;
     else if (n == "io_skew") g_tuning.io_skew = value;
     else if (n == "io_poll2") g_tuning.io_poll2 = value;

@@ -100,6 +100,7 @@ struct Tuning {
     int thr = 0;         // band 0 of every problem sleeps thr s_sleep-1 units per block (chain pace)
     int afflut = 1;      // affine fill: v_perm weight table when the pair has <= 8 symbols
     int slack = 0;       // affine fill: half chunks a band starts behind the structural minimum
+    int slack_io = 0;    // ... the extra for the band fed through the I/O wave (HBM hop)
     int io_stage = 3;    // affine fill: the I/O wave's subject staging mode (io_wave; 0..3, r04o A/B)
     int io_skew = 0;     // affine fill: the I/O wave's skewed blocks per pass while a poll is out (0: 8)
     int io_poll2 = 0;    // affine fill: the I/O wave keeps two hand-off polls in flight

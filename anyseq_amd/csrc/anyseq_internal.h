@@ -156,6 +156,9 @@ struct FillParams {
     // groups of XCD x in k-major order, dequeued by that XCD's workgroups through the
     // counter dq[kXcdCtr + x] (a workgroup whose queue is empty takes from the others)
     const uint32_t* xq;
+    // affine (round 6): half chunks of extra start slack for the band fed through the
+    // I/O wave (a group's first band after the HBM hand-off)
+    int32_t slack_io;
 };
 
 // XCD-local group placement: the workgroups of a launch of `grid` >= 8 are dealt to the 8

@@ -1439,6 +1439,7 @@ struct AffK {
     bool codes;   // q / s hold alphabet codes (0xFF never a code): the virtual prologue may clamp
     bool lut;     // codes 0..7 and int8 weights: the v_perm weight table
     int slack;    // FillParams::slack
+    int slack_io; // FillParams::slack_io
     bool lin;     // gap open 0 (a linear score through this kernel): the linear asm loop (gen_aff2 lin)
 };
 
@@ -1476,6 +1477,7 @@ struct AffShared {
 
 struct AffIO {
     bool in_border, trailing, out_lds;
+    bool io_fed = false;   // the group's first band behind the HBM hand-off, fed by the I/O wave
     int2* my_ring;
     uint32_t* my_prod;
     uint32_t* my_cons;
@@ -2171,8 +2173,9 @@ __device__ __forceinline__ void run_band_aff(const DPProblem& P, int band, int l
                 // (without slack the loop's own block-start poll waits for the same half
                 // 2b: entering it right away overlaps the conversions and the loop's
                 // prologue with that wait -- round 4)
-                if (!io.in_border && (k.slack > 0 || (k.flags & 64))) {
-                    const uint32_t need = (uint32_t)min(2 * b + 1 + k.slack, 2 * nchunks);
+                const int slk = k.slack + (io.io_fed ? k.slack_io : 0);
+                if (!io.in_border && (slk > 0 || (k.flags & 64))) {
+                    const uint32_t need = (uint32_t)min(2 * b + 1 + slk, 2 * nchunks);
                     if (seen_prod < need && !(seen_prod = spin_lds_ge(io.my_prod, need, err))) return;
                 }
                 // state into the loop's space: the lane's cell of step t0-1 is column t0-2-lane
@@ -2584,6 +2587,7 @@ __global__ __launch_bounds__(NW == 8 ? 512 : 64 * (NW + 1)) void fill_affine_ker
     k.codes = nsym > 0 && nsym < 255;
     k.lut = nsym > 0 && nsym <= 8 && fp.lut_ok;
     k.slack = fp.slack;
+    k.slack_io = fp.slack_io;
     k.lin = fp.gap_open == 0 && !(fp.pad & 128);
     // issue priority: 1 = compute waves before the I/O wave, 2 = the I/O wave first (it
     // sleeps when idle; its hand-off polls sit on the band chain)
@@ -2670,6 +2674,7 @@ __global__ __launch_bounds__(NW == 8 ? 512 : 64 * (NW + 1)) void fill_affine_ker
             if (band <= last) {
                 AffIO io;
                 io.in_border = band == 0;
+                io.io_fed = !kSelfFwd && wave == 0 && gr.group > 0;
                 io.trailing = band == last;
                 io.my_ring = sh.in_ring[wave];
                 io.my_prod = &sh.prod[wave];

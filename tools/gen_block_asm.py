@@ -338,6 +338,21 @@ LEAN = int(os.environ.get("ANYSEQ_GEN_LEAN", "2"))
 # problem's code rows in HBM (DPProblem::scode; kernel ANYSEQ_AFF_GS 1), issued one block
 # ahead; 0 = the I/O wave's pre-skewed LDS copy (ds_read2st64 at step 8, an s_filled wait)
 GS = int(os.environ.get("ANYSEQ_GEN_GS", "1"))
+# gen_aff2 hand-off reads (round 6): 1 = a consumer band issues the producer's counter
+# read and the half's top-row reads back to back and checks the counter afterwards (the
+# LDS serves one wave's requests in order and the producer writes the data before the
+# counter, so a satisfied counter read validates the data reads issued after it); a failed
+# check falls back to the poll loop and reads again.  The first half at the block start
+# (one LDS round trip instead of a poll round trip followed by the reads), the second half
+# issued at SPEC_B_ISSUE and checked at SPEC_B_CHECK (0: the round-5 counter poll at step
+# 10, checked at 14, then the reads).
+SPEC = int(os.environ.get("ANYSEQ_GEN_SPEC", "1"))
+# 2 = as 1, but the first half of block b+1 is read (counter + data) at step SPEC_A of
+# block b (and at the loop's entry for its first block) and only checked at b+1's start:
+# the counter's round trip leaves the block start when the producer is a few steps ahead
+SPEC_A = int(os.environ.get("ANYSEQ_GEN_SPEC_A", "29"))
+SPEC_B_ISSUE = int(os.environ.get("ANYSEQ_GEN_SPEC_BI", "14"))
+SPEC_B_CHECK = int(os.environ.get("ANYSEQ_GEN_SPEC_BC", "16"))
 # diagnostic build (ts variants): 1 = only the steady-state start / end stamps, no per-block
 # event checks (a step close to the product's: band lags in product steps)
 TSLIGHT = int(os.environ.get("ANYSEQ_GEN_TSLIGHT", "0"))
@@ -484,6 +499,60 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin
 
     # lean (non-border variants, where x0 is free): 2b in x0, set at the block start
     b2 = LEAN and not border
+    spec = SPEC and not border and (not ts or TSLIGHT) and LEAN
+    assert not SPEC or (SPEC_B_ISSUE < SPEC_B_CHECK <= 16 and 18 <= SPEC_A <= 31)
+
+    def spec_prefetch(breg):
+        """SPEC 2: the counter, then the first half of block `breg`'s top row (VB)."""
+        ring_addr(breg)
+        e(f"ds_read_b32 v{B_AP}, %[apr]")
+        top_reads(0)
+
+    def spec_first2(k):
+        """SPEC 2, block start: the prefetched counter covers half 2b (x4) -> the reads
+        issued after it are valid; else poll and read again."""
+        e("s_waitcnt lgkmcnt(8)")
+        e(f"v_readfirstlane_b32 %[x2], v{B_AP}")
+        e("s_max_u32 %[sp], %[sp], %[x2]")
+        e("s_cmp_ge_u32 %[sp], %[x4]")
+        e(f"s_cbranch_scc1 L_sad{k}_%=")
+        wait(e, f"pa{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
+        top_reads(0)
+        e(f"L_sad{k}_%=:")
+
+    def spec_first(k):
+        """First half of the block's top row (half 2b, target in x4): the cached counter
+        suffices -> read; else counter + reads together, check, poll loop on a miss."""
+        e("s_cmp_ge_u32 %[sp], %[x4]")
+        e(f"s_cbranch_scc1 L_sar{k}_%=")
+        e(f"ds_read_b32 v{B_AP}, %[apr]")
+        top_reads(0)
+        e("s_waitcnt lgkmcnt(8)")
+        e(f"v_readfirstlane_b32 %[x2], v{B_AP}")
+        e("s_max_u32 %[sp], %[sp], %[x2]")
+        e("s_cmp_ge_u32 %[sp], %[x4]")
+        e(f"s_cbranch_scc1 L_sad{k}_%=")
+        wait(e, f"pa{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
+        e(f"L_sar{k}_%=:")
+        top_reads(0)
+        e(f"L_sad{k}_%=:")
+
+    def spec_second_issue():
+        e(f"ds_read_b32 v{B_AP}, %[apr]")
+        top_reads(1)
+
+    def spec_second_check(k):
+        """Second half (2b+1, needed at step 17): the reads issued at SPEC_B_ISSUE after the
+        counter read are valid if that counter read covers the half."""
+        half_target(2)
+        e("s_waitcnt lgkmcnt(8)")
+        e(f"v_readfirstlane_b32 %[x2], v{B_AP}")
+        e("s_max_u32 %[sp], %[sp], %[x2]")
+        e("s_cmp_ge_u32 %[sp], %[x4]")
+        e(f"s_cbranch_scc1 L_sbd{k}_%=")
+        wait(e, f"pb{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
+        top_reads(1)
+        e(f"L_sbd{k}_%=:")
 
     def half_target(add):
         # x4 = 2b + add (clamped to the last half in the epilogue)
@@ -608,12 +677,20 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin
         event(k, 3, EVB)              # consumer: block EVB starts
         # ---- first half of this block's top row (half 2b)
         if not border:
+            if spec and SPEC < 2:
+                ring_addr("%[b]")     # (before the target: the band-end variant's uses x4)
             half_target(1)
             count_miss(k, "a")
-            wait(e, f"pa{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
+            if spec and SPEC >= 2:
+                spec_first2(k)
+            elif spec:
+                spec_first(k)
+            else:
+                wait(e, f"pa{k}", "%[sp]", "%[x4]", "%[apr]", tmp=B_VT2)
         event(k, 4, EVB)              # consumer: first half of chunk EVB seen
-        ring_addr("%[b]")
-        top_reads(0)
+        if not spec:
+            ring_addr("%[b]")
+            top_reads(0)
         if GS:
             # this block's codes (loaded one block ago), then the next block's.  The glob
             # publisher stores its halves from block 2 on: blocks 0..2 wait for all.
@@ -683,10 +760,16 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin
                     e(f"ds_read2st64_b32 v[{ns + 2 * i}:{ns + 2 * i + 1}], v{B_VA} offset0:{2 * i} offset1:{2 * i + 1}")
                 if border:
                     border_write("%[x1]")
-            if u == 10 and not border:
+            if spec and SPEC >= 2 and u == SPEC_A:
+                spec_prefetch("%[x1]")
+            if spec and u == SPEC_B_ISSUE:
+                spec_second_issue()
+            if spec and u == SPEC_B_CHECK:
+                spec_second_check(k)
+            if u == 10 and not border and not spec:
                 # poll the producer's counter for the second half (used at step 14)
                 e(f"ds_read_b32 v{B_AP}, %[apr]")
-            if u == 14:
+            if u == 14 and not spec:
                 e("s_waitcnt lgkmcnt(0)")
                 if not border:
                     e(f"v_readfirstlane_b32 %[x2], v{B_AP}")
@@ -935,6 +1018,8 @@ def gen_aff2(kind, border, pub, lut, ts=False, epi=False, cap=True, nrows=1, lin
         if pub == "lds":
             e("s_sub_u32 %[x4], %[b], 17")
             wait(e, "bpe", "%[sc]", "%[x4]", "%[anc]", tmp=B_VT2, signed=True)
+    if SPEC >= 2 and not border and (not ts or TSLIGHT) and LEAN:
+        spec_prefetch("%[b]")     # (the loop's first block)
     e("L_top_%=:")
     body(0)
     e("s_cmp_lt_u32 %[b], %[be]")
