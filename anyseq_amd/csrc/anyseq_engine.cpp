@@ -61,7 +61,8 @@ hipError_t anyseq_launch_view_reduce_i32(int32_t* base, size_t stride, int nview
 hipError_t anyseq_launch_view_max_u8(uint8_t* dst, const uint8_t* others, size_t stride, int nothers, size_t n,
                                      hipStream_t st);
 hipError_t anyseq_launch_seq_codes(const uint8_t* q, int n, const uint8_t* s, int m, uint32_t* mask, uint8_t* table,
-                                   int32_t* alpha, uint8_t* out, hipStream_t st);
+                                   int32_t* alpha, uint8_t* out, uint8_t* fill0, uint8_t* fill1, size_t fill_len,
+                                   hipStream_t st);
 hipError_t anyseq_launch_aff_predwalk(void* blocks, int nblocks, const uint8_t* Q, const uint8_t* S, uint8_t* pred,
                                       int match, int mismatch, int go, int ge, uint8_t* alq, uint8_t* als, int lds_rows,
                                       hipStream_t st);
@@ -73,9 +74,6 @@ hipError_t anyseq_launch_aff_level_tail(const void* tail, int fill_groups, hipSt
 hipError_t anyseq_launch_rows_check(const void* rows, size_t nwords, uint32_t sentinel, const void* probs, int nprobs,
                                     uint32_t* out, int inject, hipStream_t st);
 hipError_t anyseq_launch_aff_scode(const void* probs, int nprobs, int64_t max_w, hipStream_t st);
-hipError_t anyseq_launch_fill_prep_planned(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
-                                           void* sent, size_t sent_max_bytes, uint32_t sent_value,
-                                           const uint32_t* sent_n16, hipStream_t st);
 }
 
 namespace anyseq {
@@ -94,7 +92,28 @@ thread_local int g_fill_stages = 0;
 thread_local int g_shard_blocked_levels = 0;   // anyseq_last_shard_plan
 thread_local int64_t g_fill_cells = 0;
 
+int env_int_early(const char* name) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : 0;
+}
 void set_last_error(const std::string& m) { g_last_error = m; }
+// diagnostics (ANYSEQ_HOST_STAMPS=1): host-side phase stamps of one construct call,
+// printed to stderr at its end (where the host, not the GPU, sits on the critical path)
+const int g_host_stamps = env_int_early("ANYSEQ_HOST_STAMPS");
+thread_local std::vector<std::pair<const char*, double>> g_hs;
+double host_now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+inline void hstamp(const char* what) {
+    if (g_host_stamps) g_hs.emplace_back(what, host_now_us());
+}
+void hstamp_print() {
+    if (!g_host_stamps || g_hs.empty()) return;
+    fprintf(stderr, "host stamps:");
+    for (size_t i = 1; i < g_hs.size(); ++i) fprintf(stderr, " %s %.1f", g_hs[i].first, g_hs[i].second - g_hs[i - 1].second);
+    fprintf(stderr, " | total %.1f us\n", g_hs.back().second - g_hs.front().second);
+    g_hs.clear();
+}
 
 [[noreturn]] void fail(const char* fmt, ...) {
     char buf[512];
@@ -831,15 +850,17 @@ void run_fill(Engine& E, std::vector<DPProblem>& probs, const FillParams& fp, hi
 // Alphabet codes of the pair: q ++ s recoded into E.codes (n + m
 // bytes), the symbol count in device memory.  The affine fills compare codes; the
 // kernel reads the count itself (no host synchronisation).
-SeqCodes prepare_codes(Engine& E, const uint8_t* dq, int n, const uint8_t* ds, int m, hipStream_t st) {
+SeqCodes prepare_codes(Engine& E, const uint8_t* dq, int n, const uint8_t* ds, int m, hipStream_t st,
+                       uint8_t* fill0, uint8_t* fill1, size_t fill_len) {
     const bool fresh = E.codemeta.p == nullptr;
     char* meta = (char*)E.codemeta.get(512);
-    uint32_t* mask = (uint32_t*)meta;
+    uint32_t* mask = (uint32_t*)meta;   // (+ the recode kernel's block counter at word 8)
     uint8_t* table = (uint8_t*)(meta + 64);
     int32_t* alpha = (int32_t*)(meta + 320);
-    if (fresh) HIPCHECK(hipMemsetAsync(mask, 0, 32, st));   // (the recode kernel clears it after each use)
+    if (fresh) HIPCHECK(hipMemsetAsync(mask, 0, 64, st));   // (the recode kernel clears them after each use)
     uint8_t* out = (uint8_t*)E.codes.get((size_t)std::max(n, 0) + (size_t)std::max(m, 0) + 16);
-    HIPCHECK(anyseq_launch_seq_codes(dq, std::max(n, 0), ds, std::max(m, 0), mask, table, alpha, out, st));
+    HIPCHECK(anyseq_launch_seq_codes(dq, std::max(n, 0), ds, std::max(m, 0), mask, table, alpha, out, fill0, fill1,
+                                     fill_len, st));
     return SeqCodes{out, out + std::max(n, 0), alpha};
 }
 
@@ -1283,11 +1304,18 @@ void add_half(std::vector<DPProblem>& probs, std::vector<RowToColJob>& jobs, int
 // RCCL path holds one rank view per process and reduces with RCCL; local mode holds
 // all `world` views in this process (each with its own columns, best cells and
 // strings) and reduces them with device kernels -- the same data flow on one GPU.
+// `clear`: the strings' ' ' prefill (n+m bytes each) is this call's job (it rides in the
+// alphabet-coding launch: one launch fewer in front of level 1's fill)
 int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const uint8_t* dq, int n, const uint8_t* ds,
-                         int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st, const ConstructShards* shards) {
+                         int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st, const ConstructShards* shards,
+                         bool clear) {
     FillParams fp = make_params(KIND_GLOBAL, sc);
-    // the level fills compare alphabet codes; the final blocks emit the raw bytes
-    const SeqCodes cd = prepare_codes(E, dq, n, ds, m, st);
+    hstamp("enter");
+    // the level fills compare alphabet codes; the final blocks emit the raw bytes (the
+    // strings' prefill rides in the coding launch)
+    const SeqCodes cd = prepare_codes(E, dq, n, ds, m, st, clear ? d_alq : nullptr, clear ? d_als : nullptr,
+                                      (size_t)n + (size_t)m);
+    hstamp("codes");
     fp.alpha = cd.alpha;
     const uint8_t *cq = cd.q, *cs = cd.s;
     const int world = shards ? shards->world : 1;
@@ -1315,11 +1343,13 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     // one device status block per construct: splits | types | level-1 score, downloaded
     // in one copy per level into pinned memory (the level's only synchronisation)
     const size_t nsv = sp.v.size();
-    int32_t* d_status = (int32_t*)E.status.get((2 * nsv + 4) * 4);
+    // (+ the device-planned levels' tail words at tail_off, downloaded in the same copy)
+    const size_t tail_off = (2 * nsv + 4 + 3) & ~(size_t)3, tail_cap = 32 * 17 + 1 + 3;
+    int32_t* d_status = (int32_t*)E.status.get((tail_off + tail_cap) * 4);
     int32_t* d_spl = d_status;
     int32_t* d_typ = d_status + nsv;
     int32_t* d_score = d_status + 2 * nsv;
-    int32_t* h_status = (int32_t*)E.pin_down.get((2 * nsv + 4) * 4);
+    int32_t* h_status = (int32_t*)E.pin_down.get((tail_off + tail_cap) * 4);
     // the initial split table: uploaded by the host-built levels below; the device-planned
     // levels set its two ends in level 1's plan launch (the rest is written level by level)
     auto upload_status = [&]() {
@@ -1469,10 +1499,12 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         const int check_rows = env_int("ANYSEQ_CHECK_ROWS", 0);   // (read per call: tests toggle it)
         // + one word: the final level's split-table check (aff_final_blocks_kernel)
         const size_t tail_words = (size_t)std::max(nlev, 1) * (check_rows ? 17 : 9) + 1;
-        uint32_t* d_tail = (uint32_t*)E.pl_hdr.get(tail_words * 4 + 16);
+        if (tail_words > tail_cap) fail("internal: %d planned levels", nlev);
+        // (in the status block, so one download carries the splits, the score and these)
+        uint32_t* d_tail = reinterpret_cast<uint32_t*>(d_status + tail_off);
         uint32_t* d_hdr = d_tail;
         uint32_t* d_err = d_tail + 8 * nlev;
-        uint32_t* h_tail = (uint32_t*)E.pl_pin.get(tail_words * 4 + 16);
+        uint32_t* h_tail = reinterpret_cast<uint32_t*>(h_status + tail_off);
         // the final level on the device too, right behind the levels (no host round trip):
         // its block table, list of tall blocks and (worst case) HBM slab
         const int64_t slab_bound = ((int64_t)n + 127 * (int64_t)sp.nb) * 128;
@@ -1567,13 +1599,19 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         // level 1: plan + prep; every level: fill, then one tail launch (join, next level's
         // sentinel rows, counters, best cells and plan)
         if (nlev == 0) upload_status();   // (no level: the table's ends come from the host)
+        hstamp("plan setup");
         if (nlev > 0) {
             plans[0].zero_init = d_tail;
             plans[0].nzero_init = 9 * nlev;
             plans[0].init_ends = 1;
+            // (the fill prep's work too: level 1's counters and best cells; the hand-off
+            // rows are all sentinel already)
+            plans[0].zero2 = ctr;
+            plans[0].nzero2 = 32 + lv[0].slots;
+            plans[0].init2 = pbest;
+            plans[0].ninit2 = ninit_best;
+            plans[0].init2_value = kAffNegH;
             HIPCHECK(anyseq_launch_aff_level_plan(&plans[0], st));
-            HIPCHECK(anyseq_launch_fill_prep_planned(ctr, 32 + lv[0].slots, pbest, ninit_best, kAffNegH, rowbuf,
-                                                     0, 0x80808080u, d_hdr, st));
         }
         for (int li = 0; li < nlev; ++li) {
             const Lev& L = lv[li];
@@ -1597,6 +1635,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             HIPCHECK(anyseq_launch_aff_scode(d_probs, L.nh, std::max(n, m), st));
             if (timed) HIPCHECK(hipEventRecord(E.pl_ev[2 * li], st));
             HIPCHECK(anyseq_launch_fill_affine(L.nw, d_probs, d_groups, L.slots, ctr, d_err + li, &fpl, L.grid, st));
+            if (li == 0) hstamp("first fill");
             if (timed) HIPCHECK(hipEventRecord(E.pl_ev[2 * li + 1], st));
             if (check_rows) {
                 // the invariant the next launch relies on: every hand-off row word is the
@@ -1692,10 +1731,11 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                 }
             }
         }
-        HIPCHECK(hipMemcpyAsync(h_status, d_status, (2 * nsv + 1) * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipMemcpyAsync(h_tail, d_tail, tail_words * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipMemcpyAsync(h_status, d_status, (tail_off + tail_words) * 4, hipMemcpyDeviceToHost, st));
+        hstamp("enqueued");
         {
             const hipError_t e = stream_wait_spin(st);
+            hstamp("wait");
             if (e != hipSuccess) fail("affine construct levels failed: %s", hipGetErrorString(e));
         }
         if (d_tst) {
@@ -1748,6 +1788,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             score = kind == KIND_SEMIGLOBAL ? std::max(s32, 0) : s32;
         }
         planned = true;   // (the host loop has nothing left)
+        hstamp("checks");
     };
     if (!sharded && plan_ok) run_planned(1);
     if (planned && kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
@@ -2039,6 +2080,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     return score;
 }
 
+
 // Affine construct on device-resident sequences into device strings (n+m bytes);
 // returns the optimal score.
 }  // namespace
@@ -2048,9 +2090,13 @@ int64_t construct_affine_dev(Engine& E, int kind, const anyseq_scoring& sc, cons
                              const ConstructShards* shards) {
     const size_t L = (size_t)n + (size_t)m;
     if (L == 0) return empty_score(kind, n, m, sc);
-    HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
-    HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
+    // the strings' ' ' prefill: here for the degenerate shapes, else inside the construct
+    // (in its alphabet-coding launch)
+    bool clear = true;
     if (n <= 0 || m <= 0) {
+        HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
+        HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
+        clear = false;
         if (kind == KIND_GLOBAL && m <= 0 && n > 0) {   // all query rows against gaps, down the left border
             HIPCHECK(hipMemcpyAsync(d_alq, dq, (size_t)n, hipMemcpyDeviceToDevice, st));
             HIPCHECK(hipMemsetAsync(d_als, '_', (size_t)n, st));
@@ -2059,11 +2105,17 @@ int64_t construct_affine_dev(Engine& E, int kind, const anyseq_scoring& sc, cons
     }
     if (m <= MIN_PART_WIDTH_HB) {   // no Hirschberg level: the score from a (small) fill
         const int64_t score = score_dev(E, kind, sc, dq, n, ds, m, st);
-        if (kind != KIND_GLOBAL && score <= 0) return score;
-        aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st, shards);
+        if (kind != KIND_GLOBAL && score <= 0) {
+            if (clear) {
+                HIPCHECK(hipMemsetAsync(d_alq, ' ', L, st));
+                HIPCHECK(hipMemsetAsync(d_als, ' ', L, st));
+            }
+            return score;
+        }
+        aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st, shards, clear);
         return score;
     }
-    return aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st, shards);
+    return aff_construct_hb(E, kind, sc, dq, n, ds, m, d_alq, d_als, st, shards, clear);
 }
 
 namespace {
@@ -2292,6 +2344,7 @@ int anyseq_construct_device(int kind, const anyseq_scoring* sc, const uint8_t* d
         check_scoring(kind, s);
         check_value_range(s, lenq, lens);
         if (lenq < 0 || lens < 0) fail("negative sequence length");
+        hstamp("entry");
         Engine& E = engine();
         std::lock_guard<std::mutex> lk(E.mu);
         hipStream_t st = caller_stream(E, stream);
@@ -2299,6 +2352,7 @@ int anyseq_construct_device(int kind, const anyseq_scoring* sc, const uint8_t* d
         ExternRanges xr({{d_query, (size_t)std::max(lenq, 0)}, {d_subject, (size_t)std::max(lens, 0)},
                          {d_alQuery, L}, {d_alSubject, L}});
         int64_t v;
+        hstamp("setup");
         if (true_construct(s)) {
             v = construct_affine_dev(E, kind, s, d_query, lenq, d_subject, lens, d_alQuery, d_alSubject, st);
         } else {
@@ -2307,6 +2361,8 @@ int anyseq_construct_device(int kind, const anyseq_scoring* sc, const uint8_t* d
                                      : empty_score(kind, lenq, lens, s);
         }
         HIPCHECK(hipStreamSynchronize(st));
+        hstamp("sync");
+        hstamp_print();
         if (score) *score = v;
         return 0;
     } catch (const Failure& f) {

@@ -185,11 +185,10 @@ struct Engine {
     DevBuf codes, codemeta;    // alphabet codes of the current pair (prepare_codes)
     DevBuf vstr;               // sharded construct, emulated ranks: their ' '-filled strings
     // affine construct, device-planned levels: launch block, hand-off rows, part table,
-    // row-to-column jobs, per-level header and error words (+ their pinned download)
-    DevBuf pl_meta, pl_rowbuf, pl_parts, pl_jobs, pl_hdr;
+    // row-to-column jobs (their per-level header and error words sit in `status`)
+    DevBuf pl_meta, pl_rowbuf, pl_parts, pl_jobs;
     DevBuf pl_scode;           // the planned levels' subject-code rows (DPProblem::scode)
     DevBuf tst;                // diagnostics: tail-launch stamps (ANYSEQ_TAIL_STAMPS)
-    PinBuf pl_pin;
     std::vector<hipEvent_t> pl_ev;
     bool pl_dirty = true;      // pl_rowbuf may hold non-sentinel words (fresh, or a failed call)
     explicit Engine(int dev);
@@ -201,7 +200,9 @@ struct SeqCodes {
     const uint8_t* s;
     const int32_t* alpha;   // device: number of distinct symbols
 };
-SeqCodes prepare_codes(Engine& E, const uint8_t* dq, int n, const uint8_t* ds, int m, hipStream_t st);
+// (fill0 / fill1: optionally fill_len bytes of ' ' each, in the same launches)
+SeqCodes prepare_codes(Engine& E, const uint8_t* dq, int n, const uint8_t* ds, int m, hipStream_t st,
+                       uint8_t* fill0 = nullptr, uint8_t* fill1 = nullptr, size_t fill_len = 0);
 
 Engine& engine();
 int rows_per_lane();

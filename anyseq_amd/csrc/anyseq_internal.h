@@ -271,6 +271,12 @@ struct AffLevelPlan {
     // level's header and error word), and the split table's two ends to set
     uint32_t* zero_init;
     int32_t nzero_init, init_ends;
+    // (and what the level's fill prep did: the launch block's counters zeroed, the best
+    // cells set to init2_value -- one launch fewer in front of level 1's fill)
+    uint32_t* zero2;
+    int32_t nzero2;
+    int32_t* init2;
+    int32_t ninit2, init2_value;
     // XCD-local groups (FillParams::xq): run > 0 -> the group table in XCD order and its
     // 9 offsets at xq (run: consecutive groups per XCD, the grid / 8)
     int32_t xrun;

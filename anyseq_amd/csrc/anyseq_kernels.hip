@@ -3668,9 +3668,11 @@ __device__ void aff_level_plan_body(const AffLevelPlan& a) {
 }
 
 __global__ __launch_bounds__(1024) void aff_level_plan_kernel(const AffLevelPlan a) {
-    // (level 1: what a memset and an upload did before -- two launches fewer)
-    if (a.nzero_init > 0 || a.init_ends) {
+    // (level 1: what a memset, an upload and the fill prep did before -- three launches fewer)
+    if (a.nzero_init > 0 || a.init_ends || a.nzero2 > 0 || a.ninit2 > 0) {
         for (int i = threadIdx.x; i < a.nzero_init; i += blockDim.x) a.zero_init[i] = 0u;
+        for (int i = threadIdx.x; i < a.nzero2; i += blockDim.x) a.zero2[i] = 0u;
+        for (int i = threadIdx.x; i < a.ninit2; i += blockDim.x) a.init2[i] = a.init2_value;
         if (a.init_ends && threadIdx.x == 0) {
             int32_t* spl = const_cast<int32_t*>(a.spl);
             int32_t* typ = const_cast<int32_t*>(a.typ);
@@ -3683,6 +3685,27 @@ __global__ __launch_bounds__(1024) void aff_level_plan_kernel(const AffLevelPlan
         __syncthreads();
     }
     aff_level_plan_body(a);
+}
+
+// Dwords [d0, d1) of problem P's subject-code rows (DPProblem::scode): column c at byte
+// c + 64 of copy 0, copy r shifted left by r bytes, code 0xFF outside [0, w)
+// (aff_scode_kernel).
+__device__ __forceinline__ void aff_scode_dwords(const DPProblem& P, int64_t d0, int64_t d1, int64_t stride) {
+    const int64_t nd = scode_len(P.w) / 4;   // dwords per copy (scode_len is a multiple of 16)
+    const GLOBAL_AS uint8_t* s = gmem(P.s);
+    uint32_t* out = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(P.scode));
+    for (int64_t d = d0; d < d1; d += stride) {
+        const int r = (int)(d / nd);
+        const int64_t c0 = (d % nd) * 4 - 64 + r;   // column of the dword's first byte
+        uint32_t v = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t c = c0 + t;
+            const uint32_t b = (c >= 0 && c < P.w) ? s[P.s_off + (int64_t)P.s_step * c] : 0xffu;
+            v |= b << (8 * t);
+        }
+        out[d] = v;
+    }
 }
 
 constexpr int kTailStage = 8192;   // partials staged in LDS per chunk of parts (64 KiB)
@@ -4531,12 +4554,19 @@ __global__ __launch_bounds__(256) void fill_prep_kernel(uint32_t* zero, int nzer
 // per-lane table with one v_perm_b32.  Code 0xFF is never a code of a pair with fewer
 // than 255 symbols: the virtual prologue's columns left of 0 use it.
 namespace anyseq {
+// (+ optionally the ' ' prefill of a construct's two output strings, fill_len bytes each:
+// one launch fewer in front of the construct's first fill)
 __global__ __launch_bounds__(256) void seq_presence_kernel(const uint8_t* __restrict__ q, int n,
-                                                           const uint8_t* __restrict__ s, int m, uint32_t* mask) {
+                                                           const uint8_t* __restrict__ s, int m, uint32_t* mask,
+                                                           uint8_t* fill0, uint8_t* fill1, size_t fill_len) {
     __shared__ uint32_t sm[8];
     if (threadIdx.x < 8) sm[threadIdx.x] = 0;
     __syncthreads();
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = tid; i < fill_len; i += nth) {
+        fill0[i] = ' ';
+        fill1[i] = ' ';
+    }
     const size_t total = (size_t)n + (size_t)m;
     for (size_t i = tid; i < total; i += nth) {
         const uint32_t b = i < (size_t)n ? q[i] : s[i - n];
@@ -4548,44 +4578,57 @@ __global__ __launch_bounds__(256) void seq_presence_kernel(const uint8_t* __rest
     __syncthreads();
     if (threadIdx.x < 8 && sm[threadIdx.x]) atomicOr(&mask[threadIdx.x], sm[threadIdx.x]);
 }
-// One block of 256: code(byte) = rank of the byte among the present bytes; alpha[0] =
-// number of symbols.
-__global__ __launch_bounds__(256) void seq_code_kernel(const uint32_t* __restrict__ mask, uint8_t* table,
-                                                       int32_t* alpha) {
-    const int t = threadIdx.x;
-    const uint32_t w = mask[t >> 5];
-    int rank = __popc(w & ((1u << (t & 31)) - 1u));
-    for (int k = 0; k < (t >> 5); ++k) rank += __popc(mask[k]);
-    table[t] = ((w >> (t & 31)) & 1u) ? (uint8_t)rank : (uint8_t)0xfe;
-    if (t == 0) {
-        int tot = 0;
-        for (int k = 0; k < 8; ++k) tot += __popc(mask[k]);
-        *alpha = tot;
-    }
-}
-// q ++ s -> their codes (one buffer of n + m bytes); clears the presence mask for the
-// next pair.
+// q ++ s -> their codes (one buffer of n + m bytes): every block builds the code table
+// from the presence mask (code(byte) = rank of the byte among the present bytes, 0xfe
+// for an absent one; block 0 also writes it out and alpha[0] = the number of symbols),
+// then recodes its share; the last block to finish clears the mask for the next pair.
 __global__ __launch_bounds__(256) void seq_recode_kernel(const uint8_t* __restrict__ q, int n,
-                                                         const uint8_t* __restrict__ s, int m,
-                                                         const uint8_t* __restrict__ table, uint8_t* out,
-                                                         uint32_t* mask) {
+                                                         const uint8_t* __restrict__ s, int m, uint8_t* table,
+                                                         int32_t* alpha, uint8_t* out, uint32_t* mask,
+                                                         uint32_t* done) {
     __shared__ uint8_t tb[256];
-    tb[threadIdx.x] = table[threadIdx.x];
+    __shared__ uint32_t sm[8];
+    __shared__ int last;
+    const int t = threadIdx.x;
+    if (t < 8) sm[t] = mask[t];
     __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x < 8) mask[threadIdx.x] = 0u;
+    {
+        const uint32_t w = sm[t >> 5];
+        int rank = __popc(w & ((1u << (t & 31)) - 1u));
+        for (int k = 0; k < (t >> 5); ++k) rank += __popc(sm[k]);
+        tb[t] = ((w >> (t & 31)) & 1u) ? (uint8_t)rank : (uint8_t)0xfe;
+        if (blockIdx.x == 0) {
+            table[t] = tb[t];
+            if (t == 0) {
+                int tot = 0;
+                for (int k = 0; k < 8; ++k) tot += __popc(sm[k]);
+                *alpha = tot;
+            }
+        }
+    }
+    __syncthreads();
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
     const size_t total = (size_t)n + (size_t)m;
     for (size_t i = tid; i < total; i += nth) out[i] = tb[i < (size_t)n ? q[i] : s[i - n]];
+    // (every block has read the mask: the last one clears it, and the counter)
+    __syncthreads();
+    if (t == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (last && t < 8) mask[t] = 0u;
+    if (last && t == 0) *done = 0u;
 }
 }  // namespace anyseq
 
+
 hipError_t anyseq_launch_seq_codes(const uint8_t* q, int n, const uint8_t* s, int m, uint32_t* mask, uint8_t* table,
-                                   int32_t* alpha, uint8_t* out, hipStream_t st) {
+                                   int32_t* alpha, uint8_t* out, uint8_t* fill0, uint8_t* fill1, size_t fill_len,
+                                   hipStream_t st) {
     const size_t total = (size_t)n + (size_t)m;
-    const int blocks = (int)std::max<size_t>(1, std::min<size_t>(1024, (total + 4095) / 4096));
-    hipLaunchKernelGGL(anyseq::seq_presence_kernel, dim3(blocks), dim3(256), 0, st, q, n, s, m, mask);
-    hipLaunchKernelGGL(anyseq::seq_code_kernel, dim3(1), dim3(256), 0, st, mask, table, alpha);
-    hipLaunchKernelGGL(anyseq::seq_recode_kernel, dim3(blocks), dim3(256), 0, st, q, n, s, m, table, out, mask);
+    const int blocks = (int)std::max<size_t>(1, std::min<size_t>(1024, (std::max(total, fill_len) + 4095) / 4096));
+    hipLaunchKernelGGL(anyseq::seq_presence_kernel, dim3(blocks), dim3(256), 0, st, q, n, s, m, mask, fill0, fill1,
+                       fill0 ? fill_len : 0);
+    hipLaunchKernelGGL(anyseq::seq_recode_kernel, dim3(blocks), dim3(256), 0, st, q, n, s, m, table, alpha, out, mask,
+                       mask + 8);
     return hipGetLastError();
 }
 
@@ -4665,24 +4708,11 @@ hipError_t anyseq_launch_fill_prep(uint32_t* zero, int nzero, int32_t* init, int
 // [0, w): the virtual prologue's columns and the asm band end's columns past w.
 namespace anyseq {
 __global__ __launch_bounds__(256) void aff_scode_kernel(const DPProblem* __restrict__ probs, int nprobs) {
+    if ((int)blockIdx.y >= nprobs) return;
     const DPProblem& P = probs[blockIdx.y];
-    if ((int)blockIdx.y >= nprobs || P.h <= 0 || P.w <= 0 || !P.scode) return;
-    const int64_t L = scode_len(P.w);
-    const int64_t nd = L / 4;   // dwords per copy (L is a multiple of 16)
-    const GLOBAL_AS uint8_t* s = gmem(P.s);
-    uint32_t* out = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(P.scode));
-    for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < 4 * nd; d += (int64_t)gridDim.x * blockDim.x) {
-        const int r = (int)(d / nd);
-        const int64_t c0 = (d % nd) * 4 - 64 + r;   // column of the dword's first byte
-        uint32_t v = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int64_t c = c0 + t;
-            const uint32_t b = (c >= 0 && c < P.w) ? s[P.s_off + (int64_t)P.s_step * c] : 0xffu;
-            v |= b << (8 * t);
-        }
-        out[d] = v;
-    }
+    if (P.h <= 0 || P.w <= 0 || !P.scode) return;
+    aff_scode_dwords(P, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, scode_len(P.w),
+                     (int64_t)gridDim.x * blockDim.x);
 }
 }  // namespace anyseq
 
@@ -4692,19 +4722,6 @@ hipError_t anyseq_launch_aff_scode(const void* probs, int nprobs, int64_t max_w,
     const int bx = (int)std::max<int64_t>(1, std::min<int64_t>(per, std::max(1, 2048 / nprobs)));
     hipLaunchKernelGGL(anyseq::aff_scode_kernel, dim3(bx, nprobs), dim3(256), 0, st,
                        (const anyseq::DPProblem*)probs, nprobs);
-    return hipGetLastError();
-}
-
-// The prep of a device-planned level: the hand-off rows' size is read from the plan
-// header (*sent_n16 uint4s, at most sent_max_bytes).
-hipError_t anyseq_launch_fill_prep_planned(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
-                                           void* sent, size_t sent_max_bytes, uint32_t sent_value,
-                                           const uint32_t* sent_n16, hipStream_t st) {
-    const size_t n16 = sent_max_bytes / 16;
-    const size_t work = std::max<size_t>(std::max<size_t>((size_t)nzero, (size_t)ninit), n16);
-    const int blocks = (int)std::max<size_t>(1, std::min<size_t>(2048, (work + 255) / 256));
-    hipLaunchKernelGGL(anyseq::fill_prep_kernel, dim3(blocks), dim3(256), 0, st, zero, nzero, init, ninit, init_value,
-                       (uint4*)sent, n16, sent_value, (const uint4*)nullptr, (uint4*)nullptr, 0, sent_n16);
     return hipGetLastError();
 }
 

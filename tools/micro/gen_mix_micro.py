@@ -194,6 +194,117 @@ def r2_transform(body):
     return rn_transform(body, 2)
 
 
+
+def steady_path(lines):
+    """The loop's executed path in the steady state (every counter satisfied, the cached
+    hand-off counter sufficient): from L_top, conditional branches to the cached-counter
+    read paths (L_sar / L_sbd) and to the poll exits (*_ok) taken, every other conditional
+    branch not taken; ends at the loop's back branch."""
+    labels = {l[:-1]: i for i, l in enumerate(lines) if l.endswith(":")}
+    i, out = labels["L_top_%="] + 1, []
+    while True:
+        l = lines[i]
+        if l.startswith("s_cbranch_scc1 L_top_%="):
+            return out
+        m = re.match(r"s_cbranch_scc[01] (L_\w+_%=)", l)
+        if m:
+            lab = m.group(1)
+            if re.match(r"L_(sar|sbd)\d|L_\w+_ok_", lab):
+                i = labels[lab] + 1
+            else:
+                i += 1
+            continue
+        m = re.match(r"s_branch (L_\w+_%=)", l)
+        if m:
+            i = labels[m.group(1)] + 1
+            continue
+        if not l.endswith(":"):
+            out.append(l)
+        i += 1
+
+
+def lgkm_ops(l):
+    op = l.split()[0]
+    return 1 if op.startswith("ds_") else 0
+
+
+def remap_waits(orig, new):
+    """`new` is `orig` with LDS operations inserted (a leading '+') or removed (a leading
+    '-': still counted in the original numbering, not issued): every s_waitcnt
+    lgkmcnt(N) of `orig` keeps waiting for the same original operations.  Two copies of
+    the body stand for the loop's steady state; the second is returned."""
+    n2 = new + new
+    res, k_orig, ops = [], 0, []   # ops issued: (is_orig, orig_index)
+    for l in n2:
+        tag = l[0] if l[:1] in "+-" else ""
+        body = l[1:] if tag else l
+        m = re.match(r"s_waitcnt lgkmcnt\((\d+)\)", body)
+        if m and not tag:
+            need = k_orig - int(m.group(1))          # original ops [0, need) complete
+            cand = [j for j, (io, oi) in enumerate(ops) if io and oi < need]
+            n2v = len(ops) - (max(cand) + 1) if cand else len(ops)
+            body = f"s_waitcnt lgkmcnt({min(15, n2v)})"
+        elif lgkm_ops(body):
+            if tag == "-":
+                k_orig += 1
+                continue
+            ops.append((tag != "+", k_orig if tag != "+" else -1))
+            if tag != "+":
+                k_orig += 1
+        elif tag == "-":
+            continue
+        res.append(body)
+    return res[len(res) // 2:]
+
+
+def dspub_transform(body, width=2):
+    """Publishing without the DPP shift register: every step's cell pair leaves by one
+    ds_write_b64 from every lane (lane 63 into the next band's ring chunk, the others into
+    a dummy area: per-lane address %[pds] + the chunk slot masked by %[pm63]), so the two
+    wave_shl moves per step go and the half publish keeps only its counter write.
+    width 1: only G (ds_write_b32; timing only)."""
+    out = [
+        "s_sub_u32 %[x3], %[b], 2",
+        "s_lshl_b32 %[x3], %[x3], 8",
+        "s_and_b32 %[x3], %[x3], 4095",
+        "s_add_u32 %[x3], %[x3], %[nb]",
+        "v_and_or_b32 v156, %[x3], %[pm63], %[pds]",
+    ]
+    out = ["+" + l if l.startswith("ds_") else l for l in out]
+    u, hold = 0, False
+    for l in body:
+        if "wave_shl" in l:
+            continue
+        if l.startswith("ds_write_b64") and "v156" in l:
+            out.append("-" + l)          # the half's data (the counter write stays)
+            continue
+        if l.startswith("v_and_or_b32 v156") :
+            continue
+        out.append(l)
+        m = re.match(r"v_max_i32_e32 (v\d+), v\d+, %\[hg\]$", l)
+        if m:
+            of = int(m.group(1)[1:])
+            og = of - 1
+            if width == 2:
+                out.append(f"+ds_write_b64 v156, v[{og}:{of}] offset:{8 * (u % 32)}")
+            else:
+                out.append(f"+ds_write_b32 v156, v{og} offset:{8 * (u % 32)}")
+            u += 1
+    # the block-start address for the second block of the body
+    res, blk = [], 0
+    for l in out:
+        res.append(l)
+    # second block: recompute the address after the first block's end (s_mov b, x1)
+    final = []
+    for l in res:
+        final.append(l)
+        if l.startswith("s_mov_b32 %[b], %[x1]") and blk == 0:
+            blk = 1
+            final += ["s_sub_u32 %[x3], %[b], 2", "s_lshl_b32 %[x3], %[x3], 8", "s_and_b32 %[x3], %[x3], 4095",
+                      "s_add_u32 %[x3], %[x3], %[nb]", "v_and_or_b32 v156, %[x3], %[pm63], %[pds]"]
+    return final
+
+
 def main():
     name, out = sys.argv[1], sys.argv[2]
     text = open("anyseq_amd/csrc/anyseq_block_asm.inc").read()
@@ -220,6 +331,15 @@ def main():
                 for l in sel:
                     f.write(f'    "{l}\\n" \\\n')
                 f.write('    ""\n')
+        sp = steady_path(macro_lines(text, name))
+        sp2 = sp + sp[:0]
+        for sub, lines in (("SPFULL", sp), ("DSFULL", remap_waits(sp, dspub_transform(sp))),
+                           ("DS1FULL", remap_waits(sp, dspub_transform(sp, 1)))):
+            f.write(f"#define MIX_{sub}_N {len(lines)}\n")
+            f.write(f"#define MIX_{sub} \\\n")
+            for l in lines:
+                f.write(f'    "{l}\\n" \\\n')
+            f.write('    ""\n')
         f.write("#define MIX_R2_CLOBBERS " + ", ".join(f'"v{n}"' for n in range(168, 178)) + "\n")
         f.write("#define MIX_R3_CLOBBERS " + ", ".join(f'"v{n}"' for n in range(168, 188)) + "\n")
         valu = [l for l in body if kind(l) == "valu"]

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include MIX_INC
@@ -23,6 +24,7 @@ struct alignas(16) Sh {
     int2 ring[kMaxW][16 * 32];
     int2 next[kMaxW][16 * 32];
     uint32_t ctr[kMaxW][8];
+    int2 dum[kMaxW][96];   // (DSFULL: the per-step publish of lanes 0..62)
 };
 
 template <int V>
@@ -48,6 +50,7 @@ __global__ __launch_bounds__(512) void mix(int nblocks, const uint8_t* codes, un
     const uint32_t skb = (uint32_t)(63 - lane), lo = 8u * (lane - 48), lid8 = 8u * lane;
     const uint32_t bvb = 0, bvs = RFL(1u);
     const uint32_t pm63 = lane == 63 ? 0xffffffffu : 0u, pdb = 0;
+    const uint32_t pds = lane == 63 ? 0u : la(&sh.dum[wave][lane]);
     const int ge = RFL(-1);
     const uint64_t hm = 0xffff000000000000ull, gp = 0;
     const uint8_t* sg = codes;
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(512) void mix(int nblocks, const uint8_t* codes, un
                    [ge] "s"(ge), [zlp] "v"(zlp), [rb] "s"(rb), [nb] "s"(nb), [apr] "v"(apr), [acn] "v"(acn),     \
                    [anp] "v"(anp), [anc] "v"(anc), [asf] "v"(asf), [atl] "v"(atl), [skb] "v"(skb), [lo] "v"(lo),  \
                    [lid8] "v"(lid8), [bvb] "v"(bvb), [bvs] "s"(bvs), [hm] "s"(hm), [gp] "s"(gp), [pm63] "v"(pm63),   \
-                   [pdb] "v"(pdb), [sg] "s"(sg)                                                              \
+                   [pdb] "v"(pdb), [sg] "s"(sg), [pds] "v"(pds)                                              \
                  : ANYSEQ_AF2_ASM_CLOBBERS, "memory")
 #define MIXLOOP2(NAME)                                                                                           \
     for (int it = 0; it < nblocks / 2; ++it)                                                                    \
@@ -108,6 +111,9 @@ __global__ __launch_bounds__(512) void mix(int nblocks, const uint8_t* codes, un
     if constexpr (V == 12) MIXLOOP2(MIX_R2VALU);
     if constexpr (V == 13) MIXLOOP3(MIX_R3FULL);
     if constexpr (V == 14) MIXLOOP3(MIX_R3VALU);
+    if constexpr (V == 15) MIXLOOP(MIX_SPFULL);
+    if constexpr (V == 16) MIXLOOP(MIX_DSFULL);
+    if constexpr (V == 17) MIXLOOP(MIX_DS1FULL);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
     sink[blockIdx.x * blockDim.x + threadIdx.x] = g + fdn + dg + e + hg + bx + tfg + tff + (int)st + eb + hgb + ec + hgc;
@@ -116,10 +122,10 @@ __global__ __launch_bounds__(512) void mix(int nblocks, const uint8_t* codes, un
 
 static const char* kNames[] = {"FULL", "VALU", "VALU+LDS", "VALU+SALU", "VALU+WAIT", "VALU+GLOB",
                                "NODPP", "NOSDWA", "NOMAX3", "PLAIN", "PLAIN64", "R2FULL", "R2VALU",
-                               "R3FULL", "R3VALU"};
+                               "R3FULL", "R3VALU", "SPFULL", "DSFULL", "DS1FULL"};
 static const int kN[] = {MIX_FULL_N, MIX_VALU_N, MIX_VALU_LDS_N, MIX_VALU_SALU_N, MIX_VALU_WAIT_N, MIX_VALU_GLOB_N,
                          MIX_NODPP_N, MIX_NOSDWA_N, MIX_NOMAX3_N, MIX_PLAIN_N, MIX_PLAIN64_N, MIX_R2FULL_N,
-                         MIX_R2VALU_N, MIX_R3FULL_N, MIX_R3VALU_N};
+                         MIX_R2VALU_N, MIX_R3FULL_N, MIX_R3VALU_N, MIX_SPFULL_N, MIX_DSFULL_N, MIX_DS1FULL_N};
 
 template <int V>
 double run(int waves, int wgs, const uint8_t* codes, int nblocks) {
@@ -157,6 +163,13 @@ int main() {
     (void)hipMalloc(&codes, (size_t)nblocks * 32 + 8192);
     (void)hipMemset(codes, 1, (size_t)nblocks * 32 + 8192);
     printf("%s\n", MIX_INC);
+    // the steady-state path, and publishing by a per-step ds_write instead of the shift register
+    all<15>(codes, nblocks);
+    all<16>(codes, nblocks);
+    all<17>(codes, nblocks);
+    all<15>(codes, nblocks, 128);
+    all<16>(codes, nblocks, 128);
+    if (getenv("MIX_ONLY_DS")) return 0;
     all<1>(codes, nblocks);
     all<2>(codes, nblocks);
     all<3>(codes, nblocks);
