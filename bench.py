@@ -245,8 +245,8 @@ def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: s
 # Hirschberg level is one band chain of its widest half, `cols + 1.28 rows` band steps
 # (a 64-row band trails the one above by 82 steps: 64 of skew, 16 of half-chunk
 # granularity, 2 of latency).  Clock and per-step costs measured on MI355X:
-CHAIN_CLOCK_GHZ = 2.4           # shader clock of the configs[2] fill (GRBM_GUI_ACTIVE / 8 XCDs / kernel time, profiles/r05j_pmc.json)
-CHAIN_LOOP_CYCLES = 57.0        # the production X-space loop alone, LDS publisher (aff_loop_micro, r05d/r05f)
+CHAIN_CLOCK_GHZ = 2.39          # shader clock of the configs[2] fill (GRBM_GUI_ACTIVE / 8 XCDs / kernel time, profiles/r06fin_pmc.json)
+CHAIN_LOOP_CYCLES = 54.4        # the production X-space loop's steady-state path alone, LDS publisher (mix_micro SPFULL, profiles/r06_ab.json)
 CHAIN_BARE_CYCLES = 42.0        # the bare X-space step, no publishing, no block overhead (aff_micro, r04)
 NORTH_STAR_GCUPS = 1400.0       # 70 % of the 2000 GCUPS HBM model (BASELINE.json north_star)
 
