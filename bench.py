@@ -818,8 +818,11 @@ def main():
     if world > 1 or args.sharded or args.config == 4:
         raise_hw_queues()
     if args.dry_run:
-        print(json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local_rank,
-                          "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))}), flush=True)
+        # (one write per line: the ranks share the launcher's stdout pipe, and print's separate
+        # newline write could interleave with another rank's line)
+        sys.stdout.write(json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local_rank,
+                                     "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))}) + "\n")
+        sys.stdout.flush()
         return
     if args.config is None:
         args.config = 2 if world == 1 else 4
