@@ -305,6 +305,50 @@ def dspub_transform(body, width=2):
     return final
 
 
+def packed_body(nrows):
+    """Projection of a packed 16-bit G-space step, VALU + lane moves only:
+    two lane-aligned problems in the low / high halves of every register, nrows rows per
+    lane, 64 steps.  Per row and step: E v_pk_max_i16; the weight pair from the two
+    problems' LUT bytes (one v_perm per problem every 4 steps, one v_perm per step packing
+    the step's two bytes zero-extended); diagonal v_pk_add_u16; the cell two v_pk_max_i16
+    (no packed max3); H+go v_pk_add_u16; F v_pk_max_i16.  Per step two DPP moves in (row 0's
+    top G and F-in) and two shift-register moves out (the last row's pair).  Registers
+    v64..v127 (the product loop's clobber range); values are not meaningful (timing only)."""
+    CA, CB = 64, 72                      # 32 steps of codes per problem
+    RB = lambda k: 80 + 12 * k           # per row: E, hg, G0, G1, F, lutAlo, lutAhi, lutBlo, lutBhi, wA, wB, aa
+    TF, TG0, TG1, WP, SRG, SRF, GO = 116, 117, 118, 119, 120, 121, 122
+    SEL = [123, 124, 125, 126]
+    assert nrows <= 3
+    out = []
+    e = out.append
+    for step in range(64):
+        u = step % 32
+        cur, prv = step % 2, 1 - step % 2
+        tg, dg = (TG0, TG1) if cur == 0 else (TG1, TG0)
+        last = nrows - 1
+        for k in range(nrows):
+            b = RB(k)
+            if u % 4 == 0:
+                e(f"v_perm_b32 v{b + 9}, v{b + 6}, v{b + 5}, v{CA + u // 4}")
+                e(f"v_perm_b32 v{b + 10}, v{b + 8}, v{b + 7}, v{CB + u // 4}")
+            e(f"v_pk_max_i16 v{b}, v{b}, v{b + 1}")
+            if k == 0:
+                # the lane above's last row (previous step's cell and F-down)
+                e(f"v_mov_b32_dpp v{TF}, v{RB(last) + 4} wave_shr:1 row_mask:0xf bank_mask:0xf")
+                e(f"v_mov_b32_dpp v{tg}, v{RB(last) + 2 + prv} wave_shr:1 row_mask:0xf bank_mask:0xf")
+            e(f"v_perm_b32 v{WP}, v{b + 10}, v{b + 9}, v{SEL[u % 4]}")
+            diag = dg if k == 0 else RB(k - 1) + 2 + prv
+            e(f"v_pk_add_u16 v{b + 11}, v{diag}, v{WP}")
+            fin = TF if k == 0 else RB(k - 1) + 4
+            e(f"v_pk_max_i16 v{b + 2 + cur}, v{b + 11}, v{b}")
+            e(f"v_pk_max_i16 v{b + 2 + cur}, v{b + 2 + cur}, v{fin}")
+            e(f"v_pk_add_u16 v{b + 1}, v{b + 2 + cur}, v{GO}")
+            e(f"v_pk_max_i16 v{b + 4}, v{fin}, v{b + 1}")
+        e(f"v_mov_b32_dpp v{SRG}, v{RB(last) + 2 + cur} wave_shl:1 row_mask:0xf bank_mask:0xf")
+        e(f"v_mov_b32_dpp v{SRF}, v{RB(last) + 4} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    return out
+
+
 def main():
     name, out = sys.argv[1], sys.argv[2]
     text = open("anyseq_amd/csrc/anyseq_block_asm.inc").read()
@@ -337,6 +381,13 @@ def main():
                            ("DS1FULL", remap_waits(sp, dspub_transform(sp, 1)))):
             f.write(f"#define MIX_{sub}_N {len(lines)}\n")
             f.write(f"#define MIX_{sub} \\\n")
+            for l in lines:
+                f.write(f'    "{l}\\n" \\\n')
+            f.write('    ""\n')
+        for nr in (2, 3):
+            lines = packed_body(nr)
+            f.write(f"#define MIX_PK{nr}_N {len(lines)}\n")
+            f.write(f"#define MIX_PK{nr} \\\n")
             for l in lines:
                 f.write(f'    "{l}\\n" \\\n')
             f.write('    ""\n')

@@ -114,6 +114,8 @@ __global__ __launch_bounds__(512) void mix(int nblocks, const uint8_t* codes, un
     if constexpr (V == 15) MIXLOOP(MIX_SPFULL);
     if constexpr (V == 16) MIXLOOP(MIX_DSFULL);
     if constexpr (V == 17) MIXLOOP(MIX_DS1FULL);
+    if constexpr (V == 18) MIXLOOP(MIX_PK2);
+    if constexpr (V == 19) MIXLOOP(MIX_PK3);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
     sink[blockIdx.x * blockDim.x + threadIdx.x] = g + fdn + dg + e + hg + bx + tfg + tff + (int)st + eb + hgb + ec + hgc;
@@ -122,10 +124,11 @@ __global__ __launch_bounds__(512) void mix(int nblocks, const uint8_t* codes, un
 
 static const char* kNames[] = {"FULL", "VALU", "VALU+LDS", "VALU+SALU", "VALU+WAIT", "VALU+GLOB",
                                "NODPP", "NOSDWA", "NOMAX3", "PLAIN", "PLAIN64", "R2FULL", "R2VALU",
-                               "R3FULL", "R3VALU", "SPFULL", "DSFULL", "DS1FULL"};
+                               "R3FULL", "R3VALU", "SPFULL", "DSFULL", "DS1FULL", "PK2", "PK3"};
 static const int kN[] = {MIX_FULL_N, MIX_VALU_N, MIX_VALU_LDS_N, MIX_VALU_SALU_N, MIX_VALU_WAIT_N, MIX_VALU_GLOB_N,
                          MIX_NODPP_N, MIX_NOSDWA_N, MIX_NOMAX3_N, MIX_PLAIN_N, MIX_PLAIN64_N, MIX_R2FULL_N,
-                         MIX_R2VALU_N, MIX_R3FULL_N, MIX_R3VALU_N, MIX_SPFULL_N, MIX_DSFULL_N, MIX_DS1FULL_N};
+                         MIX_R2VALU_N, MIX_R3FULL_N, MIX_R3VALU_N, MIX_SPFULL_N, MIX_DSFULL_N, MIX_DS1FULL_N, MIX_PK2_N,
+                         MIX_PK3_N};
 
 template <int V>
 double run(int waves, int wgs, const uint8_t* codes, int nblocks) {
@@ -170,6 +173,13 @@ int main() {
     all<15>(codes, nblocks, 128);
     all<16>(codes, nblocks, 128);
     if (getenv("MIX_ONLY_DS")) return 0;
+    // the packed 16-bit projection (two problems per register, 2 / 3 rows per lane: 256 /
+    // 384 cells per wave step) against the product's three-row loop and its VALU subset
+    all<18>(codes, nblocks);
+    all<19>(codes, nblocks);
+    all<13>(codes, nblocks);
+    all<14>(codes, nblocks);
+    if (getenv("MIX_ONLY_PK")) return 0;
     all<1>(codes, nblocks);
     all<2>(codes, nblocks);
     all<3>(codes, nblocks);
