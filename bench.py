@@ -21,9 +21,9 @@ Other workloads: --config 1 (configs[1]: NW linear score, 65536^2), --config 3
 
 Every line carries:
   * roofline  — the dominant kernel (the DP fill) against the §8(d) model of 4 B
-    per cell (peak 8 TB/s), plus the VALU-issue ceiling of the same kernel
-    (``roofline.valu_model``) and the PMC-measured HBM bytes when a profile of this
-    build exists under profiles/ (``traffic``);
+    per cell (bound "hbm", peak 8 TB/s), the PMC-measured HBM bytes per launch when a
+    profile of this build exists under profiles/ (``traffic``), and the VALU-issue
+    ceiling of the same kernel, which is what binds it (``roofline.valu``);
   * cpu_baseline — the oracle restatement of the same workload (a bounded
     prefix sample), at T = 4 (the reference's get_thread_count(),
     backend_cpu.impala:13) and at T = the host cores available, median and min
@@ -190,11 +190,13 @@ def cpu_baseline(what: str, work, cells: int, sample: str, runs: int):
 
 def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: str, traffic_tag: str,
              rows: int = 1, end_to_end=None):
-    """The dominant kernel's roofline.  The PMC counters (profiles/) show
-    the fill bound by VALU issue along the band chain, not by HBM: it keeps every cell in
-    VGPRs and moves ~1 % of the 4 B/cell model's bytes.  So `bound` is "valu" (GCUPS
-    against the VALU-issue peak for the kernel's instructions per cell), and the north
-    star's 4 B/cell HBM model stays beside it as a labelled secondary (`hbm_model`)."""
+    """The dominant kernel's roofline in the contract's form: `bound` "hbm", `achieved` =
+    the §8(d) algorithmic bytes (4 B per DP cell) per launch / the launch's mean duration,
+    `peak` 8 TB/s, `frac`, and `traffic` = the PMC-measured HBM bytes per launch of this
+    build (profiles/).  The fill keeps every cell in VGPRs and moves ~1-3 % of those bytes
+    (the PMC traffic), so the 4 B/cell figure is a model, not its limit: what binds it is
+    VALU issue (`valu`: GCUPS against the chip's and the design's VALU ceilings for the
+    kernel's instructions per cell) along the band chain (`chain_model`, configs[2])."""
     ok = kernel_ms > 0
     achieved_gbs = cells_per_launch * BYTES_PER_CELL / (kernel_ms * 1e-3) / 1e9 if ok else None
     traffic, traffic_src = load_traffic(traffic_tag)
@@ -206,23 +208,23 @@ def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: s
     design = VALU_DESIGN_WAVE_INSTR * 64 / v / 1e9
     hbm_frac = achieved_gbs / HBM_PEAK_GBS if achieved_gbs else None
     out = {
-        "bound": "valu", "achieved": round(gcups, 2) if gcups else None, "peak": round(peak, 1), "unit": "GCUPS",
-        "frac": round(gcups / peak, 4) if gcups else None,
+        "bound": "hbm", "achieved": round(achieved_gbs, 2) if achieved_gbs else None, "peak": HBM_PEAK_GBS,
+        "unit": "GB/s", "frac": round(hbm_frac, 4) if hbm_frac else None,
         "traffic": traffic, "traffic_source": traffic_src,
-        "binding": "band-chain latency: per-step VALU issue x (steps + bands x per-hop lag), DESIGN.md 3.5",
+        "model": f"{BYTES_PER_CELL} B/cell x DP cells per launch (SURVEY.md 8(d), the north star's scale) / "
+                 "the launch's mean duration; not a limit of this kernel, which stores only hand-off rows",
+        "traffic_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic and ok else None,
+        "traffic_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic and ok else None,
+        "binding": "VALU issue along the band chain: per-step VALU issue x (steps + bands x per-hop lag), "
+                   "DESIGN.md 3.5",
         "kernel": kernel, "kernel_ms": round(kernel_ms, 4), "cells_per_launch": int(cells_per_launch),
-        "valu_model": {"instr_per_wave_step": round(v, 3), "cells_per_wave_step": 64, "rows_per_lane": rows,
-                       "chip_peak": "256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU",
-                       "design_ceiling_gcups": round(design, 1),
-                       "design_frac": round(gcups / design, 4) if gcups else None,
-                       "design": "one compute wave per SIMD: one wave64 VALU per 4 cycles (a wave alone)"},
-        "hbm_model": {
-            "achieved": round(achieved_gbs, 2) if achieved_gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved_gbs / HBM_PEAK_GBS, 4) if achieved_gbs else None,
-            "model": f"{BYTES_PER_CELL} B/cell x DP cells per launch (SURVEY.md 8(d), the north star's scale); "
-                     "not a limit of this kernel, which stores only hand-off rows",
-            "traffic_gbs": round(traffic / (kernel_ms * 1e-3) / 1e9, 2) if traffic and ok else None,
-            "traffic_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if traffic and ok else None},
+        "valu": {"bound": "valu", "achieved": round(gcups, 2) if gcups else None, "peak": round(peak, 1),
+                 "unit": "GCUPS", "frac": round(gcups / peak, 4) if gcups else None,
+                 "instr_per_wave_step": round(v, 3), "cells_per_wave_step": 64, "rows_per_lane": rows,
+                 "chip_peak": "256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU",
+                 "design_ceiling_gcups": round(design, 1),
+                 "design_frac": round(gcups / design, 4) if gcups else None,
+                 "design": "one compute wave per SIMD: one wave64 VALU per 4 cycles (a wave alone)"},
     }
     if end_to_end:
         # the figure the north star is quoted in (verdict round 5, item 6): the whole step's
@@ -230,13 +232,13 @@ def roofline(kernel: str, cells_per_launch: float, kernel_ms: float, valu_key: s
         # sits below the fill launch's own fraction
         cells, step_ms = end_to_end
         e2e = cells * BYTES_PER_CELL / (step_ms * 1e-3) / 1e9 if step_ms > 0 else None
-        out["hbm_model"]["frac_end_to_end"] = round(e2e / HBM_PEAK_GBS, 4) if e2e else None
-        out["hbm_model"]["end_to_end"] = "n*m cells per step x 4 B / ms_per_step / 8 TB/s"
+        out["frac_end_to_end"] = round(e2e / HBM_PEAK_GBS, 4) if e2e else None
+        out["end_to_end"] = "n*m cells per step x 4 B / ms_per_step / 8 TB/s"
     if hbm_frac and hbm_frac > 1:
-        out["hbm_model"]["note"] = (
+        out["note"] = (
             f"frac > 1: the 4 B/cell model is not a bound of this kernel, which keeps every cell in VGPRs "
-            f"(PMC traffic {out['hbm_model']['traffic_frac']} of peak) and stores only hand-off rows; every cell "
-            f"is computed -- PMC SQ_INSTS_VALU per 64 cells {round(v, 2)} (valu_model) x cells per launch "
+            f"(PMC traffic {out['traffic_frac']} of peak) and stores only hand-off rows; every cell "
+            f"is computed -- PMC SQ_INSTS_VALU per 64 cells {round(v, 2)} (valu) x cells per launch "
             f"(DESIGN.md 5)")
     return out
 
