@@ -478,8 +478,8 @@ void audit_probs(const std::vector<DPProblem>& probs, bool aff) {
 // XCD-local groups (FillParams::xq): the affine fill of a single-GPU
 // launch (no concurrent shard fill it could wait on: a shard launch passes its own grid)
 // of a multiple of 8 workgroups, dealt grid / 8 per XCD, when the tuning asks for it;
-// returns the run of consecutive groups per XCD, or 0 (one queue).  A workgroup whose
-// XCD queue is empty takes from the others, so every group runs whatever the placement.
+// returns the run of consecutive groups per XCD, or 0 (one queue).  Off by default and UNSAFE under shared CUs:
+// an XCD with no resident workgroup leaves its queue's groups undealt while others wait on them.
 int xcd_run(const Engine& E, int grid, bool aff, int grid_req = 0) {
     if (!aff || !g_tuning.xcdq || grid_req > 0 || grid > E.num_cus || grid < kXcds || grid % kXcds != 0) return 0;
     return grid / kXcds;
