@@ -23,7 +23,10 @@ $(SRC)/anyseq_shard.o: $(SRC)/anyseq_shard.cpp $(SRC)/anyseq_internal.h $(SRC)/a
 $(SRC)/anyseq_io.o: $(SRC)/anyseq_io.cpp include/anyseq.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(SRC)/anyseq_kernels.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o
+$(SRC)/anyseq_aux.o: $(SRC)/anyseq_aux.hip $(SRC)/anyseq_internal.h
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(SRC)/anyseq_kernels.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o $(SRC)/anyseq_aux.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -Wl,-z,defs -o $@ $^ -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
 oracle:
@@ -31,9 +34,9 @@ oracle:
 
 # diagnostic build with s_memtime stamps (tools only; never loaded by the product path)
 stamps: anyseq_amd/libanyseq_stamps.so
-anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o $(SRC)/anyseq_internal.h $(SRC)/anyseq_block_asm.inc
+anyseq_amd/libanyseq_stamps.so: $(SRC)/anyseq_kernels.hip $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o $(SRC)/anyseq_aux.o $(SRC)/anyseq_internal.h $(SRC)/anyseq_block_asm.inc
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -c $(SRC)/anyseq_kernels.hip -o $(SRC)/anyseq_kernels_stamps.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(SRC)/anyseq_kernels_stamps.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o $(SRC)/anyseq_aux.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
 # experimental build for A/B runs: the affine loop generated under other generator knobs
 # (EXPGEN, e.g. `make exp EXPGEN="ANYSEQ_GEN_LEAN=0"`) as anyseq_amd/libanyseq_exp.so,
@@ -44,13 +47,13 @@ EXPDEF ?=
 exp:
 	mkdir -p build && env $(EXPGEN) python3 tools/gen_block_asm.py build/exp_asm.inc > /dev/null
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(EXPDEF) -DANYSEQ_ASM_INC='"$(CURDIR)/build/exp_asm.inc"' -c $(SRC)/anyseq_kernels.hip -o build/anyseq_kernels_exp.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -Wl,-z,defs -o anyseq_amd/libanyseq_exp.so build/anyseq_kernels_exp.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
+	$(HIPCC) --offload-arch=$(ARCH) -shared -Wl,-z,defs -o anyseq_amd/libanyseq_exp.so build/anyseq_kernels_exp.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o $(SRC)/anyseq_aux.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
 # diagnostic build with only the steady-state stamps (band lags at a product-like step)
 stamps_light:
 	mkdir -p build && ANYSEQ_GEN_TSLIGHT=1 python3 tools/gen_block_asm.py build/light_asm.inc > /dev/null
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DANYSEQ_STAMPS -DANYSEQ_ASM_INC='"$(CURDIR)/build/light_asm.inc"' -c $(SRC)/anyseq_kernels.hip -o build/anyseq_kernels_light.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o anyseq_amd/libanyseq_stamps_light.so build/anyseq_kernels_light.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o anyseq_amd/libanyseq_stamps_light.so build/anyseq_kernels_light.o $(SRC)/anyseq_engine.o $(SRC)/anyseq_shard.o $(SRC)/anyseq_io.o $(SRC)/anyseq_aux.o -L/opt/rocm/lib -lrccl -lhsa-runtime64
 
 clean:
 	rm -f $(SRC)/*.o $(LIB) anyseq_amd/libanyseq_*.so

@@ -103,6 +103,8 @@ _lib.anyseq_last_fill_stats.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.
 _lib.anyseq_last_shard_plan.restype = _c_int
 _lib.anyseq_last_fill_multi_row_launches.restype = _c_int
 _lib.anyseq_last_fill_multi_row_launches.argtypes = [ctypes.POINTER(_c_int)]
+_lib.anyseq_last_inherit_stats.restype = ctypes.c_int64
+_lib.anyseq_last_inherit_stats.argtypes = [ctypes.POINTER(ctypes.c_int64)]
 _lib.anyseq_main_random_pair.argtypes = [_c_i64, _c_i64, _vp, ctypes.POINTER(_c_i64), _vp,
                                          ctypes.POINTER(_c_i64)]
 
@@ -300,6 +302,15 @@ def last_fill_multi_row_launches():
     the most rows per lane among them); resets both."""
     r = _c_int(1)
     n = int(_lib.anyseq_last_fill_multi_row_launches(ctypes.byref(r)))
+    return n, r.value
+
+
+def last_inherit_stats():
+    """(halves run as two column blocks recording their child's column, halves taken as
+    such a recorded column instead of a fill) of this thread's affine constructs since the
+    previous call (host-built levels, option "inherit_halves"); resets both."""
+    r = ctypes.c_int64(0)
+    n = int(_lib.anyseq_last_inherit_stats(ctypes.byref(r)))
     return n, r.value
 
 

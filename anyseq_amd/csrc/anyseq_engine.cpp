@@ -50,6 +50,7 @@ hipError_t anyseq_launch_aff_hb_join(const void* parts, int nparts, int half, co
                                      const int32_t* RH, const int32_t* RE, const int32_t* pbest, int go, int ge,
                                      int32_t* splits, int32_t* types, int32_t* score, hipStream_t st);
 hipError_t anyseq_launch_aff_row_to_col(const void* jobs, int njobs, int maxn, int nge, hipStream_t st);
+hipError_t anyseq_launch_i32_jobs(const void* jobs, int njobs, int maxn, hipStream_t st);
 hipError_t anyseq_launch_fill_prep(uint32_t* zero, int nzero, int32_t* init, int ninit, int32_t init_value,
                                    void* sent, size_t sent_bytes, uint32_t sent_value, const void* up_src, void* up_dst,
                                    size_t up_bytes, hipStream_t st);
@@ -91,6 +92,7 @@ thread_local int g_fill_rmax = 1;   // the most rows per lane among them
 thread_local int g_fill_stages = 0;
 thread_local int g_shard_blocked_levels = 0;   // anyseq_last_shard_plan
 thread_local int64_t g_fill_cells = 0;
+thread_local int64_t g_inherit_stats[2] = {0, 0};   // split halves, reused halves (anyseq_last_inherit_stats)
 
 int env_int_early(const char* name) {
     const char* v = getenv(name);
@@ -342,6 +344,7 @@ void init_tuning_locked() {
     g_tuning.devfinal = env_int("ANYSEQ_AFF_DEVFINAL", g_tuning.devfinal);
     g_tuning.xcdq = env_int("ANYSEQ_XCD_GROUPS", g_tuning.xcdq);
     g_tuning.ctrue = env_int("ANYSEQ_CONSTRUCT_TRUE", g_tuning.ctrue);
+    g_tuning.inherit = env_int("ANYSEQ_INHERIT", g_tuning.inherit);
     g_tuning_init = true;
 }
 
@@ -1797,6 +1800,25 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         HIPCHECK(hipStreamSynchronize(st));   // h_status: its upload before the first download
     }
     int handover = 0;
+    // Inherited halves (one GPU, global / semiglobal): a half of a
+    // throughput-bound level may run as two column blocks, the first ending at its child
+    // part's split -- that block's last column (H, E) is then also the child half's last
+    // column on the child's rows (same anchor, same borders, a prefix of the columns and
+    // rows), so at the next level the child half is a copy instead of a fill.  The left
+    // half's child is the left child part's left half, the right half's the right child
+    // part's right half.  cap*_prev: per part of the previous level, whether its half
+    // recorded the column (the right half's by reversed row from its part's first row).
+    const bool inh_on = !sharded && g_tuning.inherit > 0 && !local;
+    std::vector<uint8_t> capL_prev, capR_prev;
+    std::vector<int> capR_off_prev;
+    int32_t *CLH = nullptr, *CLE = nullptr, *CRH = nullptr, *CRE = nullptr;
+    if (inh_on && !planned) {
+        CLH = (int32_t*)E.capLH.get(nn * 4);
+        CLE = (int32_t*)E.capLE.get(nn * 4);
+        CRH = (int32_t*)E.capRH.get(nn * 4);
+        CRE = (int32_t*)E.capRE.get(nn * 4);
+    }
+    const int inh_nge = -sc.gap_extend;
     for (int parts = 1; !planned && parts < sp.nb; parts *= 2) {
         ++g_stage_level;
         // free-end best cells, 2 per part, per view
@@ -1896,6 +1918,59 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             }
             if (g_shard_blocked_levels == g_stage_level - 1) g_shard_blocked_levels = g_stage_level;
         }
+        // inherited halves of this level: split halves' second blocks (launched after the
+        // first blocks), the copies of the reused halves (before the fills) and the frame
+        // corrections of the second blocks' columns (after them)
+        const bool inh_level = inh_on && 2 * parts < sp.nb &&
+                               (g_tuning.inherit >= 2 || [&] {
+                                   const int64_t rows = std::max<int64_t>(1, (int64_t)n / parts), w = level_half(parts);
+                                   const int64_t chain = w + rows * 128 / 100,
+                                                 work = 2 * (int64_t)parts * ((rows + 63) / 64) * (w + 64);
+                                   return aff_waves_for(chain, work, g_tuning.grida > 0 ? g_tuning.grida : E.num_cus) >= 7;
+                               }());
+        std::vector<uint8_t> capL_cur(inh_on ? (size_t)parts : 0, 0), capR_cur(inh_on ? (size_t)parts : 0, 0);
+        std::vector<int> capR_off_cur(inh_on ? (size_t)parts : 0, 0);
+        std::vector<DPProblem> probsB;
+        std::vector<I32Job> copy_jobs, shift_jobs;
+        // a half as two column blocks: [0, w1) records its last column into capH / capE,
+        // [w1, w) takes it as its left border (the sharded score's left_in, complete before
+        // its launch) in a frame moved by the top border's slope (NORMAL / EFREE: w1 |ge|;
+        // the free borders are flat), moved back by a job; a best cell is shared (flat
+        // frames only)
+        auto split_half = [&](int qoff, int qstep, int h, int soff, int sstep, int w, int w1, int bm, int am,
+                              int32_t* best, int32_t* capH, int32_t* capE, int32_t* H, int32_t* Ecol) {
+            DPProblem A = aff_problem(cq, qoff, qstep, h, cs, soff, sstep, w1);
+            A.bmode = bm;
+            A.amode = am;
+            A.best = best;
+            A.out_col = capH;
+            A.out_col_e = capE;
+            probs_of[0].push_back(A);
+            DPProblem B = aff_problem(cq, qoff, qstep, h, cs, soff + sstep * w1, sstep, w - w1);
+            B.bmode = bm;
+            B.amode = am;
+            B.best = best;
+            B.out_col = H;
+            B.out_col_e = Ecol;
+            B.left_in = capH;
+            B.left_in_e = capE;
+            const int shift = (bm == BM_NORMAL || bm == BM_EFREE) ? w1 * inh_nge : 0;
+            B.left_shift = shift;
+            probsB.push_back(B);
+            if (shift) {
+                shift_jobs.push_back(I32Job{H, H, h, -shift});
+                shift_jobs.push_back(I32Job{Ecol, Ecol, h, -shift});
+            }
+        };
+        // may the half (border mode bm, kind bits am) run split?  No clamp, no EPAID
+        // corner (the shard frame's corner is go only under NORMAL), a best only in a flat frame
+        auto splittable = [&](int bm, int am) {
+            if (am & AM_CLAMP) return false;
+            if (bm == BM_EPAID || bm == BM_FREE_LOCAL) return false;
+            // (a best of the last row: the blocks' last rows are the half's; not of every cell)
+            if ((am & AM_BEST_LASTCOL) != 0 && (am & AM_BEST_LASTCOL) != AM_BEST_LAST) return false;
+            return (am & AM_BEST_LASTCOL) == 0 || !(bm == BM_NORMAL || bm == BM_EFREE);
+        };
         for (int p = 0; p < parts && !blocked; ++p) {
             const PartInfo& pi = pinfo[p];
             if ((pi.flags & 12) || pi.len <= 0) continue;
@@ -1904,6 +1979,44 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             const bool sfree = pi.flags & 1, efree = pi.flags & 2;
             // (half_index advances on every rank, so all ranks agree on the owners)
             const int ol = owner(half_index++), orr = owner(half_index++);
+            if (inh_on) {   // (one view: not sharded)
+                int32_t* pb = pbest0;
+                const int am_l = (pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0);
+                const int am_r = (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0);
+                // left half: the left child of a part whose left half recorded its column,
+                // unless it needs a best cell of its own
+                if (p % 2 == 0 && parts > 1 && capL_prev[p / 2] && am_l == 0) {
+                    copy_jobs.push_back(I32Job{CLH + off, LH0 + off, len, 0});
+                    copy_jobs.push_back(I32Job{CLE + off, LE0 + off, len, 0});
+                } else {
+                    const AffPartGeo cg = aff_part_geo(sp.nb, m, 2 * parts, 2 * p);
+                    if (inh_level && cg.lw > 0 && cg.hw > 0 && cg.lw < half && splittable(pi.smode, am_l)) {
+                        split_half(off, 1, len, hoj_l, 1, half, cg.lw, pi.smode, am_l, efree ? pb + 2 * p : nullptr,
+                                   CLH + off, CLE + off, LH0 + off, LE0 + off);
+                        capL_cur[p] = 1;
+                    } else {
+                        add_half(probs_of[0], jobs, rowpool, cq, off, 1, len, cs, hoj_l, 1, half, pi.smode, am_l,
+                                 efree ? pb + 2 * p : nullptr, LH0 + off, LE0 + off);
+                    }
+                }
+                // right half: the right child of a part whose right half recorded its column
+                if (p % 2 == 1 && capR_prev[p / 2] && am_r == 0) {
+                    copy_jobs.push_back(I32Job{CRH + capR_off_prev[p / 2], RH0 + off, len, 0});
+                    copy_jobs.push_back(I32Job{CRE + capR_off_prev[p / 2], RE0 + off, len, 0});
+                } else {
+                    const AffPartGeo cg = aff_part_geo(sp.nb, m, 2 * parts, 2 * p + 1);
+                    if (inh_level && cg.lw > 0 && cg.hw > 0 && cg.hw < hw && splittable(pi.emode, am_r)) {
+                        split_half(off + len - 1, -1, len, hoj_r + hw - 1, -1, hw, cg.hw, pi.emode, am_r,
+                                   sfree ? pb + 2 * p + 1 : nullptr, CRH + off, CRE + off, RH0 + off, RE0 + off);
+                        capR_cur[p] = 1;
+                        capR_off_cur[p] = off;
+                    } else {
+                        add_half(probs_of[0], jobs, rowpool, cq, off + len - 1, -1, len, cs, hoj_r + hw - 1, -1, hw,
+                                 pi.emode, am_r, sfree ? pb + 2 * p + 1 : nullptr, RH0 + off, RE0 + off);
+                    }
+                }
+                continue;
+            }
             for (int v = 0; v < nviews; ++v) {
                 const size_t vo = (size_t)v * nn;
                 int32_t* pb = pbest0 + (size_t)v * 2 * parts;
@@ -1931,7 +2044,33 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
         bool pending_fill = false;
         const char* d_up = nullptr;
         const double t_built = now_us();
-        for (int v = 0; v < nviews; ++v) {
+        // inherited halves: the copy and frame jobs in one upload, the copies before the fills
+        const char* d_aux = nullptr;
+        if (!copy_jobs.empty() || !shift_jobs.empty()) {
+            const size_t nb_aux = (copy_jobs.size() + shift_jobs.size()) * sizeof(I32Job);
+            char* ha = (char*)E.pin_aux.get(nb_aux);
+            memcpy(ha, copy_jobs.data(), copy_jobs.size() * sizeof(I32Job));
+            memcpy(ha + copy_jobs.size() * sizeof(I32Job), shift_jobs.data(), shift_jobs.size() * sizeof(I32Job));
+            char* da = (char*)E.auxjobs.get(nb_aux);
+            HIPCHECK(hipMemcpyAsync(da, ha, nb_aux, hipMemcpyHostToDevice, st));
+            d_aux = da;
+        }
+        auto run_jobs = [&](const std::vector<I32Job>& J, const char* d) {
+            int maxn = 0;
+            for (const I32Job& j : J) maxn = std::max(maxn, j.n);
+            HIPCHECK(anyseq_launch_i32_jobs(d, (int)J.size(), maxn, st));
+        };
+        if (!copy_jobs.empty()) run_jobs(copy_jobs, d_aux);
+        if (!probsB.empty()) {
+            // split halves: the first blocks (with the unsplit halves) complete before the
+            // second blocks start, which carry the level's upload (one view: not sharded)
+            fill_async(E, E.fc, probs_of[0], fp, st, 0, nullptr, 0, pbest0, 2 * parts, kAffNegH);
+            fill_finish(E.fc);
+            fill_async(E, E.fc, probsB, fp, st, 0, up, pb + jb, nullptr, 0, 0);
+            d_up = (const char*)E.fc.d_extra;
+            pending_fill = true;
+        }
+        for (int v = 0; v < nviews && probsB.empty(); ++v) {
             auto& probs = probs_of[v];
             int32_t* pbv = pbest0 + (size_t)v * 2 * parts;
             if (probs.empty()) {
@@ -1963,6 +2102,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             for (const auto& J : jobs) maxn = std::max(maxn, J.n);
             HIPCHECK(anyseq_launch_aff_row_to_col(d_up + pb, (int)jobs.size(), maxn, -sc.gap_extend, st));
             stage_check(st, "aff_row_to_col");
+        }
+        if (!shift_jobs.empty()) {   // split halves' second blocks: their columns back to the half's frame
+            run_jobs(shift_jobs, d_aux + copy_jobs.size() * sizeof(I32Job));
+            stage_check(st, "inherited halves: frames");
         }
         if (sharded) {   // every rank gets every part's columns and best cells
             if (emulate) {
@@ -2015,6 +2158,13 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             score = kind == KIND_SEMIGLOBAL ? std::max(s32, 0) : s32;
             level1 = false;
             if (kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
+        }
+        if (inh_on) {
+            capL_prev.swap(capL_cur);
+            capR_prev.swap(capR_cur);
+            capR_off_prev.swap(capR_off_cur);
+            g_inherit_stats[0] += (int64_t)probsB.size();
+            g_inherit_stats[1] += (int64_t)copy_jobs.size() / 2;
         }
     }
     if (handover > 0) {
@@ -2425,6 +2575,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "plan_hw_queues") g_tuning.plan_queues = value;
     else if (n == "xcd_groups") g_tuning.xcdq = value;
     else if (n == "construct_mode") g_tuning.ctrue = value;
+    else if (n == "inherit_halves") g_tuning.inherit = value;
     else return -1;
     return 0;
 }
@@ -2440,6 +2591,13 @@ void anyseq_last_fill_stats(double* ms, int* launches, int64_t* cells) {
     g_fill_ms = 0.0;
     g_fill_launches = 0;
     g_fill_cells = 0;
+}
+
+int64_t anyseq_last_inherit_stats(int64_t* reused) {
+    const int64_t v = g_inherit_stats[0];
+    if (reused) *reused = g_inherit_stats[1];
+    g_inherit_stats[0] = g_inherit_stats[1] = 0;
+    return v;
 }
 
 int anyseq_last_fill_multi_row_launches(int* max_rows) {

@@ -124,6 +124,11 @@ struct Tuning {
     // which is the linear recurrence.  The six import.h symbols
     // always keep the compat semantics.
     int ctrue = 0;
+    // affine construct, host-built levels: inherited halves -- a filled
+    // half of a throughput-bound level also records its child's split column, and the
+    // child's half is then a lookup instead of a fill.  0 off, 1 throughput-bound levels
+    // (the default once measured), 2 every level (tests).
+    int inherit = 0;
 };
 extern Tuning g_tuning;
 
@@ -189,6 +194,10 @@ struct Engine {
     DevBuf pl_meta, pl_rowbuf, pl_parts, pl_jobs;
     DevBuf pl_scode;           // the planned levels' subject-code rows (DPProblem::scode)
     DevBuf tst;                // diagnostics: tail-launch stamps (ANYSEQ_TAIL_STAMPS)
+    // host-built levels, inherited halves: the recorded child columns
+    // (H, E by query row, left and right halves) and the level's copy / frame jobs
+    DevBuf capLH, capLE, capRH, capRE, auxjobs;
+    PinBuf pin_aux;
     std::vector<hipEvent_t> pl_ev;
     bool pl_dirty = true;      // pl_rowbuf may hold non-sentinel words (fresh, or a failed call)
     explicit Engine(int dev);

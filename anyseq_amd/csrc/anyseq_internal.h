@@ -238,6 +238,14 @@ struct RowToCol {
     int32_t c0;     // G space: the row's first column in the half (a column block of a sharded level, §6.2)
 };
 
+// Inherited Hirschberg halves (anyseq_aux.hip): dst[i] = src[i] + delta, i < n.
+struct I32Job {
+    const int32_t* src;
+    int32_t* dst;
+    int32_t n;
+    int32_t delta;
+};
+
 // Device-planned Hirschberg level of the affine construct (DESIGN.md §3.7,
 // aff_level_plan_kernel): the level's part table, half descriptors, group table and
 // row-to-column jobs are built on the device from the previous level's splits, so the

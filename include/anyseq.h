@@ -127,6 +127,11 @@ int anyseq_last_shard_plan(void);
  * "affine_rows_per_lane"); *max_rows (may be null) gets the most rows per lane among the
  * launches (1 when none).  Resets both. */
 int anyseq_last_fill_multi_row_launches(int* max_rows);
+/* Affine construct, host-built levels (option "inherit_halves"): the
+ * halves of the calling thread's constructs since the previous call that ran as two column
+ * blocks recording their child's column (the return value), and the halves taken as such a
+ * recorded column instead of a fill (*reused, may be null).  Resets both. */
+int64_t anyseq_last_inherit_stats(int64_t* reused);
 
 /* ---- column-block sharded score (build-defined) ----
  * Subject columns are split into contiguous blocks, block g = [g*m/N, (g+1)*m/N);
