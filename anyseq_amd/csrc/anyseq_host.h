@@ -127,8 +127,8 @@ struct Tuning {
     // affine construct, host-built levels: inherited halves -- a filled
     // half of a throughput-bound level also records its child's split column, and the
     // child's half is then a lookup instead of a fill.  0 off, 1 throughput-bound levels
-    // (the default once measured), 2 every level (tests).
-    int inherit = 0;
+    // (default), 2 every level (tests).
+    int inherit = 1;
 };
 extern Tuning g_tuning;
 

@@ -24,7 +24,7 @@ def inherit(anyseq):
     anyseq.set_option("inherit_halves", 2)
     anyseq.last_inherit_stats()
     yield anyseq
-    anyseq.set_option("inherit_halves", 0)
+    anyseq.set_option("inherit_halves", 1)
     anyseq.set_option("affine_device_plan", 1)
 
 
