@@ -345,6 +345,7 @@ void init_tuning_locked() {
     g_tuning.xcdq = env_int("ANYSEQ_XCD_GROUPS", g_tuning.xcdq);
     g_tuning.ctrue = env_int("ANYSEQ_CONSTRUCT_TRUE", g_tuning.ctrue);
     g_tuning.inherit = env_int("ANYSEQ_INHERIT", g_tuning.inherit);
+    g_tuning.inherit_depth = env_int("ANYSEQ_INHERIT_DEPTH", g_tuning.inherit_depth);
     g_tuning_init = true;
 }
 
@@ -1809,14 +1810,21 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     // part's right half.  cap*_prev: per part of the previous level, whether its half
     // recorded the column (the right half's by reversed row from its part's first row).
     const bool inh_on = !sharded && g_tuning.inherit > 0 && !local;
-    std::vector<uint8_t> capL_prev, capR_prev;
-    std::vector<int> capR_off_prev;
-    int32_t *CLH = nullptr, *CLE = nullptr, *CRH = nullptr, *CRE = nullptr;
+    // cap[side][d][0/1]: the depth-d recorded column (H / E by query row; d = 1: the
+    // child's, d = 2: the grandchild's, ...), side 0 left halves, 1 right halves
+    constexpr int kInhMax = 4;
+    const int inh_depth = std::max(1, std::min(kInhMax, g_tuning.inherit_depth));
+    struct InhChain {
+        int j = 0, mx = 0, base = 0;   // depth of the child half's column (0: none), deepest recorded, recorder's first row
+    };
+    std::vector<InhChain> chL_prev, chR_prev;
+    int32_t* cap[2][kInhMax + 1][2] = {};
     if (inh_on && !planned) {
-        CLH = (int32_t*)E.capLH.get(nn * 4);
-        CLE = (int32_t*)E.capLE.get(nn * 4);
-        CRH = (int32_t*)E.capRH.get(nn * 4);
-        CRE = (int32_t*)E.capRE.get(nn * 4);
+        for (int side = 0; side < 2; ++side) {
+            int32_t* b = (int32_t*)(side ? E.capR : E.capL).get((size_t)inh_depth * 2 * nn * 4);
+            for (int d = 1; d <= inh_depth; ++d)
+                for (int k = 0; k < 2; ++k) cap[side][d][k] = b + ((size_t)(d - 1) * 2 + k) * nn;
+        }
     }
     const int inh_nge = -sc.gap_extend;
     for (int parts = 1; !planned && parts < sp.nb; parts *= 2) {
@@ -1928,39 +1936,67 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                                                  work = 2 * (int64_t)parts * ((rows + 63) / 64) * (w + 64);
                                    return aff_waves_for(chain, work, g_tuning.grida > 0 ? g_tuning.grida : E.num_cus) >= 7;
                                }());
-        std::vector<uint8_t> capL_cur(inh_on ? (size_t)parts : 0, 0), capR_cur(inh_on ? (size_t)parts : 0, 0);
-        std::vector<int> capR_off_cur(inh_on ? (size_t)parts : 0, 0);
-        std::vector<DPProblem> probsB;
+        std::vector<InhChain> chL_cur(inh_on ? (size_t)parts : 0), chR_cur(inh_on ? (size_t)parts : 0);
+        std::vector<std::vector<DPProblem>> later;   // split halves' blocks 2, 3, .. (one launch each, in order)
         std::vector<I32Job> copy_jobs, shift_jobs;
-        // a half as two column blocks: [0, w1) records its last column into capH / capE,
-        // [w1, w) takes it as its left border (the sharded score's left_in, complete before
-        // its launch) in a frame moved by the top border's slope (NORMAL / EFREE: w1 |ge|;
-        // the free borders are flat), moved back by a job; a best cell is shared (flat
-        // frames only)
-        auto split_half = [&](int qoff, int qstep, int h, int soff, int sstep, int w, int w1, int bm, int am,
-                              int32_t* best, int32_t* capH, int32_t* capE, int32_t* H, int32_t* Ecol) {
-            DPProblem A = aff_problem(cq, qoff, qstep, h, cs, soff, sstep, w1);
-            A.bmode = bm;
-            A.amode = am;
-            A.best = best;
-            A.out_col = capH;
-            A.out_col_e = capE;
-            probs_of[0].push_back(A);
-            DPProblem B = aff_problem(cq, qoff, qstep, h, cs, soff + sstep * w1, sstep, w - w1);
-            B.bmode = bm;
-            B.amode = am;
-            B.best = best;
-            B.out_col = H;
-            B.out_col_e = Ecol;
-            B.left_in = capH;
-            B.left_in_e = capE;
-            const int shift = (bm == BM_NORMAL || bm == BM_EFREE) ? w1 * inh_nge : 0;
-            B.left_shift = shift;
-            probsB.push_back(B);
-            if (shift) {
-                shift_jobs.push_back(I32Job{H, H, h, -shift});
-                shift_jobs.push_back(I32Job{Ecol, Ecol, h, -shift});
+        int64_t n_split = 0, n_reused = 0;
+        // a half as column blocks cut at `cuts` (ascending): block i < last records its last
+        // column into caps[i] (the deepest descendant's first), block i > 0 takes block i-1's
+        // as its complete left border (the sharded score's left_in) in its own frame, moved
+        // by the top border's slope (NORMAL / EFREE: |ge| per column of the block's start;
+        // the free borders are flat) and moved back by a job after the level's last launch;
+        // a best cell is shared (flat frames only)
+        auto split_half = [&](int qoff, int qstep, int h, int soff, int sstep, int w, const std::vector<int>& cuts,
+                              int bm, int am, int32_t* best, const std::vector<std::pair<int32_t*, int32_t*>>& caps,
+                              int32_t* H, int32_t* Ecol) {
+            const bool flat = !(bm == BM_NORMAL || bm == BM_EFREE);
+            const int nbk = (int)cuts.size() + 1;
+            for (int i = 0; i < nbk; ++i) {
+                const int s0 = i == 0 ? 0 : cuts[i - 1], e0 = i + 1 < nbk ? cuts[i] : w;
+                DPProblem P = aff_problem(cq, qoff, qstep, h, cs, soff + sstep * s0, sstep, e0 - s0);
+                P.bmode = bm;
+                P.amode = am;
+                P.best = best;
+                int32_t* oh = i + 1 < nbk ? caps[i].first : H;
+                int32_t* oe = i + 1 < nbk ? caps[i].second : Ecol;
+                P.out_col = oh;
+                P.out_col_e = oe;
+                if (i > 0) {
+                    P.left_in = caps[i - 1].first;
+                    P.left_in_e = caps[i - 1].second;
+                    const int sp0 = i >= 2 ? cuts[i - 2] : 0;   // block i-1's first column (its frame)
+                    P.left_shift = flat ? 0 : (s0 - sp0) * inh_nge;
+                }
+                if (i == 0) {
+                    probs_of[0].push_back(P);
+                } else {
+                    if ((int)later.size() < i) later.resize(i);
+                    later[i - 1].push_back(P);
+                }
+                if (!flat && s0 > 0) {
+                    shift_jobs.push_back(I32Job{oh, oh, h, -s0 * inh_nge});
+                    shift_jobs.push_back(I32Job{oe, oe, h, -s0 * inh_nge});
+                }
             }
+            ++n_split;
+        };
+        // the columns a half of part p can record: its leftmost (side 0) / rightmost (1)
+        // descendant's half width at each of the next inh_depth levels, while they split
+        auto desc_cuts = [&](int p, int side, int width) {
+            std::vector<int> c;
+            int prev = width;
+            for (int d = 1; d <= inh_depth; ++d) {
+                const int64_t P2 = (int64_t)parts << d;
+                if (P2 >= sp.nb) break;
+                const int q = side == 0 ? (int)((int64_t)p << d) : (int)(((int64_t)(p + 1) << d) - 1);
+                const AffPartGeo g = aff_part_geo(sp.nb, m, (int)P2, q);
+                const int cw = side == 0 ? g.lw : g.hw;
+                if (g.lw <= 0 || g.hw <= 0 || cw <= 0 || cw >= prev) break;
+                c.push_back(cw);
+                prev = cw;
+            }
+            std::reverse(c.begin(), c.end());   // ascending: the deepest descendant's first
+            return c;
         };
         // may the half (border mode bm, kind bits am) run split?  No clamp, no EPAID
         // corner (the shard frame's corner is go only under NORMAL), a best only in a flat frame
@@ -1983,38 +2019,45 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                 int32_t* pb = pbest0;
                 const int am_l = (pi.smode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (efree ? best_bits : 0);
                 const int am_r = (pi.emode == BM_FREE_LOCAL ? AM_CLAMP : 0) | (sfree ? best_bits : 0);
-                // left half: the left child of a part whose left half recorded its column,
-                // unless it needs a best cell of its own
-                if (p % 2 == 0 && parts > 1 && capL_prev[p / 2] && am_l == 0) {
-                    copy_jobs.push_back(I32Job{CLH + off, LH0 + off, len, 0});
-                    copy_jobs.push_back(I32Job{CLE + off, LE0 + off, len, 0});
-                } else {
-                    const AffPartGeo cg = aff_part_geo(sp.nb, m, 2 * parts, 2 * p);
-                    if (inh_level && cg.lw > 0 && cg.hw > 0 && cg.lw < half && splittable(pi.smode, am_l)) {
-                        split_half(off, 1, len, hoj_l, 1, half, cg.lw, pi.smode, am_l, efree ? pb + 2 * p : nullptr,
-                                   CLH + off, CLE + off, LH0 + off, LE0 + off);
-                        capL_cur[p] = 1;
-                    } else {
-                        add_half(probs_of[0], jobs, rowpool, cq, off, 1, len, cs, hoj_l, 1, half, pi.smode, am_l,
-                                 efree ? pb + 2 * p : nullptr, LH0 + off, LE0 + off);
+                // One side's half: the chain it inherits (the leftmost / rightmost descendant
+                // line of a half that recorded columns), then copy it (no best cell of its
+                // own), split it (recording its own descendants' columns), or fill it whole
+                // and pass the inherited chain on to its child.
+                auto side_half = [&](int side, const InhChain& in, int am, int bm, int width, int qoff, int qstep,
+                                     int soff, int sstep, int32_t* best, int32_t* H, int32_t* Ecol) {
+                    InhChain out;
+                    if (in.j > 0 && am == 0) {
+                        copy_jobs.push_back(I32Job{cap[side][in.j][0] + in.base, H, len, 0});
+                        copy_jobs.push_back(I32Job{cap[side][in.j][1] + in.base, Ecol, len, 0});
+                        ++n_reused;
+                        if (in.j < in.mx) out = InhChain{in.j + 1, in.mx, in.base};
+                        return out;
                     }
-                }
-                // right half: the right child of a part whose right half recorded its column
-                if (p % 2 == 1 && capR_prev[p / 2] && am_r == 0) {
-                    copy_jobs.push_back(I32Job{CRH + capR_off_prev[p / 2], RH0 + off, len, 0});
-                    copy_jobs.push_back(I32Job{CRE + capR_off_prev[p / 2], RE0 + off, len, 0});
-                } else {
-                    const AffPartGeo cg = aff_part_geo(sp.nb, m, 2 * parts, 2 * p + 1);
-                    if (inh_level && cg.lw > 0 && cg.hw > 0 && cg.hw < hw && splittable(pi.emode, am_r)) {
-                        split_half(off + len - 1, -1, len, hoj_r + hw - 1, -1, hw, cg.hw, pi.emode, am_r,
-                                   sfree ? pb + 2 * p + 1 : nullptr, CRH + off, CRE + off, RH0 + off, RE0 + off);
-                        capR_cur[p] = 1;
-                        capR_off_cur[p] = off;
-                    } else {
-                        add_half(probs_of[0], jobs, rowpool, cq, off + len - 1, -1, len, cs, hoj_r + hw - 1, -1, hw,
-                                 pi.emode, am_r, sfree ? pb + 2 * p + 1 : nullptr, RH0 + off, RE0 + off);
+                    const std::vector<int> cuts =
+                        inh_level && splittable(bm, am) ? desc_cuts(p, side, width) : std::vector<int>();
+                    if (!cuts.empty()) {
+                        const int D = (int)cuts.size();
+                        // recorded columns by query row: a left half's rows from `off` up, a right
+                        // half's (reversed) from its last row down, at n-1-row -- so the columns of
+                        // different parts never overlap, whatever the levels between write
+                        const int base = side == 0 ? off : n - (off + len);
+                        std::vector<std::pair<int32_t*, int32_t*>> caps;
+                        for (int i = 0; i < D; ++i)   // cuts[i] is the depth D - i descendant's width
+                            caps.emplace_back(cap[side][D - i][0] + base, cap[side][D - i][1] + base);
+                        split_half(qoff, qstep, len, soff, sstep, width, cuts, bm, am, best, caps, H, Ecol);
+                        return InhChain{1, D, base};
                     }
-                }
+                    add_half(probs_of[0], jobs, rowpool, cq, qoff, qstep, len, cs, soff, sstep, width, bm, am, best, H,
+                             Ecol);
+                    if (in.j > 0 && in.j < in.mx) out = InhChain{in.j + 1, in.mx, in.base};
+                    return out;
+                };
+                const InhChain none;
+                chL_cur[p] = side_half(0, p % 2 == 0 && parts > 1 ? chL_prev[p / 2] : none, am_l, pi.smode, half,
+                                       off, 1, hoj_l, 1, efree ? pb + 2 * p : nullptr, LH0 + off, LE0 + off);
+                chR_cur[p] = side_half(1, p % 2 == 1 ? chR_prev[p / 2] : none, am_r, pi.emode, hw, off + len - 1,
+                                       -1, hoj_r + hw - 1, -1, sfree ? pb + 2 * p + 1 : nullptr, RH0 + off,
+                                       RE0 + off);
                 continue;
             }
             for (int v = 0; v < nviews; ++v) {
@@ -2061,16 +2104,20 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             HIPCHECK(anyseq_launch_i32_jobs(d, (int)J.size(), maxn, st));
         };
         if (!copy_jobs.empty()) run_jobs(copy_jobs, d_aux);
-        if (!probsB.empty()) {
-            // split halves: the first blocks (with the unsplit halves) complete before the
-            // second blocks start, which carry the level's upload (one view: not sharded)
+        if (!later.empty()) {
+            // split halves: their first blocks (with the unsplit halves), then each further
+            // block in its own launch behind the one before; the last carries the level's
+            // upload (one view: not sharded)
             fill_async(E, E.fc, probs_of[0], fp, st, 0, nullptr, 0, pbest0, 2 * parts, kAffNegH);
-            fill_finish(E.fc);
-            fill_async(E, E.fc, probsB, fp, st, 0, up, pb + jb, nullptr, 0, 0);
+            for (size_t i = 0; i < later.size(); ++i) {
+                fill_finish(E.fc);
+                const bool last = i + 1 == later.size();
+                fill_async(E, E.fc, later[i], fp, st, 0, last ? up : nullptr, last ? pb + jb : 0, nullptr, 0, 0);
+            }
             d_up = (const char*)E.fc.d_extra;
             pending_fill = true;
         }
-        for (int v = 0; v < nviews && probsB.empty(); ++v) {
+        for (int v = 0; v < nviews && later.empty(); ++v) {
             auto& probs = probs_of[v];
             int32_t* pbv = pbest0 + (size_t)v * 2 * parts;
             if (probs.empty()) {
@@ -2160,11 +2207,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             if (kind != KIND_GLOBAL && score <= 0) return score;   // the empty alignment
         }
         if (inh_on) {
-            capL_prev.swap(capL_cur);
-            capR_prev.swap(capR_cur);
-            capR_off_prev.swap(capR_off_cur);
-            g_inherit_stats[0] += (int64_t)probsB.size();
-            g_inherit_stats[1] += (int64_t)copy_jobs.size() / 2;
+            chL_prev.swap(chL_cur);
+            chR_prev.swap(chR_cur);
+            g_inherit_stats[0] += n_split;
+            g_inherit_stats[1] += n_reused;
         }
     }
     if (handover > 0) {
@@ -2576,6 +2622,7 @@ int anyseq_set_option(const char* name, int value) {
     else if (n == "xcd_groups") g_tuning.xcdq = value;
     else if (n == "construct_mode") g_tuning.ctrue = value;
     else if (n == "inherit_halves") g_tuning.inherit = value;
+    else if (n == "inherit_depth") g_tuning.inherit_depth = value;
     else return -1;
     return 0;
 }

@@ -129,6 +129,7 @@ struct Tuning {
     // child's half is then a lookup instead of a fill.  0 off, 1 throughput-bound levels
     // (default), 2 every level (tests).
     int inherit = 1;
+    int inherit_depth = 2;   // descendant columns a split half records (1..4)
 };
 extern Tuning g_tuning;
 
@@ -196,7 +197,7 @@ struct Engine {
     DevBuf tst;                // diagnostics: tail-launch stamps (ANYSEQ_TAIL_STAMPS)
     // host-built levels, inherited halves: the recorded child columns
     // (H, E by query row, left and right halves) and the level's copy / frame jobs
-    DevBuf capLH, capLE, capRH, capRE, auxjobs;
+    DevBuf capL, capR, auxjobs;
     PinBuf pin_aux;
     std::vector<hipEvent_t> pl_ev;
     bool pl_dirty = true;      // pl_rowbuf may hold non-sentinel words (fresh, or a failed call)

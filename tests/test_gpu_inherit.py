@@ -1,8 +1,9 @@
 """GPU parity of the inherited Hirschberg halves (option "inherit_halves").
 
 Host-built levels (affine_device_plan 0) with every level forced to split its eligible
-halves into two column blocks, the first recording its child part's split column, and the
-next level taking the child half from that column instead of a fill.  The construct must be
+halves into column blocks, each block but the last recording the split column of one of the
+half's next descendants (depth 1-3), and the later levels taking those descendants' halves
+from the recorded columns instead of a fill.  The construct must be
 bit-exact with the oracle restatement (oracle_affine_construct: every half filled), score
 and both sparse strings; the stats show that halves were split and reused, so the test
 covers the path it names.  Local constructs (clamped halves) never split.
@@ -18,12 +19,16 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SCHEMES = [(2, -1, -2, -1), (1, -3, -5, -2), (5, -4, -10, -1), (3, -2, -1, -3)]
 
 
-@pytest.fixture
-def inherit(anyseq):
+@pytest.fixture(params=[1, 2, 3], ids=["depth1", "depth2", "depth3"])
+def inherit(anyseq, request):
+    """Host-built levels, every level splitting; a split half records the columns of its
+    next 1 / 2 / 3 descendants (option inherit_depth)."""
     anyseq.set_option("affine_device_plan", 0)
     anyseq.set_option("inherit_halves", 2)
+    anyseq.set_option("inherit_depth", request.param)
     anyseq.last_inherit_stats()
     yield anyseq
+    anyseq.set_option("inherit_depth", 2)
     anyseq.set_option("inherit_halves", 1)
     anyseq.set_option("affine_device_plan", 1)
 
