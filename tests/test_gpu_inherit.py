@@ -129,3 +129,20 @@ def test_inherit_config3_prefix(inherit):
     assert (hashlib.sha256(aq).hexdigest(), hashlib.sha256(as_).hexdigest()) == (g["sha_alq"], g["sha_als"])
     split, reused = inherit.last_inherit_stats()
     assert split > 0 and reused > 0, (split, reused)
+
+
+@pytest.mark.parametrize("kind", ["global", "semiglobal"])
+def test_host_built_linear_true_construct_refused(inherit, oracle, kind):
+    """The extended API's linear true construct (construct_mode 1, gap open 0) is exact on
+    the device-planned levels (tests/test_gpu_linear_true_construct.py) but not on the
+    host-built ones (round 6: wrong scores with every loop / transposition knob,
+    tools/lin_host_probe.py), so those refuse it loudly instead of answering wrong."""
+    import anyseq_amd
+    rng = random.Random(76)
+    q, s = related(rng, 2000)
+    inherit.set_option("construct_mode", 1)
+    try:
+        with pytest.raises(anyseq_amd.AnySeqError, match="device-planned levels only"):
+            inherit.construct(kind, q, s[:2100], match=2, mismatch=-1, gap_open=0, gap_extend=-1)
+    finally:
+        inherit.set_option("construct_mode", 0)
