@@ -1427,7 +1427,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     // gap open 0 (the extended API's linear true construct, construct_mode 1) is exact on the
     // device-planned levels only: the host-built levels give wrong scores for it
     // (tools/lin_host_probe.py), so they refuse it
-    if (sc.gap_open == 0 && (sharded || !plan_ok))
+    if (sc.gap_open == 0 && (sharded || !plan_ok) && env_int("ANYSEQ_LIN_HOST", 0) == 0)   // (=1: diagnostics)
         fail("the linear true construct (gap open 0) runs on device-planned levels only: this %d x %d construct "
              "needs host-built or sharded levels (affine_device_plan %d)", n, m, g_tuning.devplan);
     // Device-planned levels: every level from the one with P0 parts on is

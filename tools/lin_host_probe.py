@@ -12,6 +12,7 @@ from test_gpu_inherit import related, rnd  # noqa: E402
 
 A.set_device(0)
 A.set_option("construct_mode", 1)
+A.set_option("inherit_halves", 0)
 rng = random.Random(76)
 cases = []
 for n, m in [(2000, 2100), (3000, 2600), (1500, 4000), (700, 900)]:
@@ -22,8 +23,12 @@ variants = {"devplan": [("affine_device_plan", 1)],
             "host": [("affine_device_plan", 0)],
             "host_noloop": [("affine_device_plan", 0), ("linear_affine_loop", 0)],
             "host_notr": [("affine_device_plan", 0), ("affine_transpose", 0)],
-            "host_noasm": [("affine_device_plan", 0), ("affine_asm", 0)]}
-defaults = {"affine_device_plan": 1, "linear_affine_loop": 1, "affine_transpose": 1, "affine_asm": 1}
+            "host_noasm": [("affine_device_plan", 0), ("affine_asm", 0)],
+            "host_r1": [("affine_device_plan", 0), ("affine_rows_per_lane", 1)],
+            "host_nw4": [("affine_device_plan", 0), ("affine_waves_per_group", 4)],
+            "host_r1_nw4": [("affine_device_plan", 0), ("affine_rows_per_lane", 1), ("affine_waves_per_group", 4)]}
+defaults = {"affine_device_plan": 1, "linear_affine_loop": 1, "affine_transpose": 1, "affine_asm": 1,
+            "affine_rows_per_lane": 0, "affine_waves_per_group": 0}
 for name, opts in variants.items():
     for k, v in opts:
         A.set_option(k, v)
