@@ -1314,6 +1314,10 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
                          int m, uint8_t* d_alq, uint8_t* d_als, hipStream_t st, const ConstructShards* shards,
                          bool clear) {
     FillParams fp = make_params(KIND_GLOBAL, sc);
+    // the affine fill for every level, gap open 0 included (its linear loop): make_params
+    // marks open 0 as a linear fill, which would send the host-built levels' affine problems
+    // to fill_kernel (round 6: wrong linear true constructs there, tools/lin_host_probe.py)
+    fp.affine = 1;
     hstamp("enter");
     // the level fills compare alphabet codes; the final blocks emit the raw bytes (the
     // strings' prefill rides in the coding launch)
@@ -1424,12 +1428,6 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     };
     bool planned = false, dev_final = false;
     const bool plan_ok = g_tuning.devplan && plan_rowbuf_bytes() <= ((size_t)8 << 30) && n < 8192 * 4096 - 1;
-    // gap open 0 (the extended API's linear true construct, construct_mode 1) is exact on the
-    // device-planned levels only: the host-built levels give wrong scores for it
-    // (tools/lin_host_probe.py), so they refuse it
-    if (sc.gap_open == 0 && (sharded || !plan_ok) && env_int("ANYSEQ_LIN_HOST", 0) == 0)   // (=1: diagnostics)
-        fail("the linear true construct (gap open 0) runs on device-planned levels only: this %d x %d construct "
-             "needs host-built or sharded levels (affine_device_plan %d)", n, m, g_tuning.devplan);
     // Device-planned levels: every level from the one with P0 parts on is
     // enqueued up front -- plan (aff_level_plan_kernel builds the level from the splits on
     // the device), prep, fill, row-to-column, join -- and the splits come back in ONE
@@ -1815,8 +1813,7 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     // half's child is the left child part's left half, the right half's the right child
     // part's right half.  cap*_prev: per part of the previous level, whether its half
     // recorded the column (the right half's by reversed row from its part's first row).
-    // (gap open 0 never reaches the host-built levels, below)
-    const bool inh_on = !sharded && g_tuning.inherit > 0 && !local && sc.gap_open != 0;
+    const bool inh_on = !sharded && g_tuning.inherit > 0 && !local;
     // cap[side][d][0/1]: the depth-d recorded column (H / E by query row; d = 1: the
     // child's, d = 2: the grandchild's, ...), side 0 left halves, 1 right halves
     constexpr int kInhMax = 4;

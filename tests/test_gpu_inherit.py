@@ -132,17 +132,34 @@ def test_inherit_config3_prefix(inherit):
 
 
 @pytest.mark.parametrize("kind", ["global", "semiglobal"])
-def test_host_built_linear_true_construct_refused(inherit, oracle, kind):
-    """The extended API's linear true construct (construct_mode 1, gap open 0) is exact on
-    the device-planned levels (tests/test_gpu_linear_true_construct.py) but not on the
-    host-built ones (round 6: wrong scores with every loop / transposition knob,
-    tools/lin_host_probe.py), so those refuse it loudly instead of answering wrong."""
-    import anyseq_amd
+def test_inherit_linear_true_construct(inherit, oracle, kind):
+    """Linear gaps through the extended API's true construct (construct_mode 1: the affine
+    construct with gap open 0, the affine fill's linear loop) on host-built levels with
+    every level splitting: bit-exact.  (Before round 6's fix the host-built levels sent gap
+    open 0 to the linear fill_kernel: wrong scores, tools/lin_host_probe.py.)"""
     rng = random.Random(76)
-    q, s = related(rng, 2000)
     inherit.set_option("construct_mode", 1)
     try:
-        with pytest.raises(anyseq_amd.AnySeqError, match="device-planned levels only"):
-            inherit.construct(kind, q, s[:2100], match=2, mismatch=-1, gap_open=0, gap_extend=-1)
+        for n, m in [(2000, 2100), (3000, 2600), (1500, 4000), (700, 900)]:
+            q, s = related(rng, n)
+            s = s[:m] if len(s) >= m else s + rnd(rng, m - len(s))
+            for sc in ((2, -1, 0, -1), (1, -3, 0, -2)):
+                same(inherit, oracle, kind, q, s, sc)
+    finally:
+        inherit.set_option("construct_mode", 0)
+    split, reused = inherit.last_inherit_stats()
+    assert split > 0 and reused > 0, (split, reused)
+
+
+def test_host_built_linear_true_construct_local(inherit, oracle):
+    """The local linear true construct on host-built levels (clamped halves never split)."""
+    rng = random.Random(77)
+    inherit.set_option("construct_mode", 1)
+    try:
+        for n, m in [(2000, 2100), (1500, 4000)]:
+            q, s = related(rng, n)
+            s = s[:m] if len(s) >= m else s + rnd(rng, m - len(s))
+            for sc in ((2, -1, 0, -1), (1, -3, 0, -2)):
+                same(inherit, oracle, "local", q, s, sc)
     finally:
         inherit.set_option("construct_mode", 0)

@@ -1,5 +1,6 @@
 """Probe: the linear true construct (construct_mode 1, gap open 0) on host-built affine levels
-(affine_device_plan 0) under knob variants, against the oracle."""
+(affine_device_plan 0) under knob variants, against the oracle (round 6: found the host-built
+levels launching gap open 0 on the linear fill_kernel)."""
 import os
 import random
 import sys
