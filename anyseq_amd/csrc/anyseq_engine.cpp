@@ -1806,20 +1806,20 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
     }
     int handover = 0;
     // Inherited halves (one GPU, global / semiglobal): a half of a
-    // throughput-bound level may run as two column blocks, the first ending at its child
-    // part's split -- that block's last column (H, E) is then also the child half's last
-    // column on the child's rows (same anchor, same borders, a prefix of the columns and
-    // rows), so at the next level the child half is a copy instead of a fill.  The left
-    // half's child is the left child part's left half, the right half's the right child
-    // part's right half.  cap*_prev: per part of the previous level, whether its half
-    // recorded the column (the right half's by reversed row from its part's first row).
+    // throughput-bound level may run as column blocks cut at its next descendants' splits --
+    // a block's last column (H, E) is then also that descendant half's last column on the
+    // descendant's rows (same anchor, same borders, a prefix of the columns and rows), so
+    // at that level the descendant half is a copy instead of a fill.  A left half's line is
+    // its leftmost descendants' left halves, a right half's its rightmost descendants' right
+    // halves.  ch*_prev: per part of the previous level, the recorded chain its child half
+    // takes (left halves' columns by query row, right halves' by n-1-row).
     const bool inh_on = !sharded && g_tuning.inherit > 0 && !local;
     // cap[side][d][0/1]: the depth-d recorded column (H / E by query row; d = 1: the
     // child's, d = 2: the grandchild's, ...), side 0 left halves, 1 right halves
     constexpr int kInhMax = 4;
     const int inh_depth = std::max(1, std::min(kInhMax, g_tuning.inherit_depth));
     struct InhChain {
-        int j = 0, mx = 0, base = 0;   // depth of the child half's column (0: none), deepest recorded, recorder's first row
+        int j = 0, mx = 0, base = 0;   // depth of the child half's column (0: none), deepest recorded, column offset
     };
     std::vector<InhChain> chL_prev, chR_prev;
     int32_t* cap[2][kInhMax + 1][2] = {};
@@ -1930,9 +1930,9 @@ int64_t aff_construct_hb(Engine& E, int kind, const anyseq_scoring& sc, const ui
             }
             if (g_shard_blocked_levels == g_stage_level - 1) g_shard_blocked_levels = g_stage_level;
         }
-        // inherited halves of this level: split halves' second blocks (launched after the
+        // inherited halves of this level: split halves' later blocks (a launch each, after the
         // first blocks), the copies of the reused halves (before the fills) and the frame
-        // corrections of the second blocks' columns (after them)
+        // corrections of the later blocks' columns (after them)
         const bool inh_level = inh_on && 2 * parts < sp.nb &&
                                (g_tuning.inherit >= 2 || [&] {
                                    const int64_t rows = std::max<int64_t>(1, (int64_t)n / parts), w = level_half(parts);
